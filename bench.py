@@ -1,0 +1,205 @@
+"""Benchmark: the ZeRO sharded-optimizer step on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[3]): the SmolLM3-3B-shaped synthetic
+parameter set — 326 tensors, 3,075,098,624 params, bf16 params and grads, fp32 master / exp_avg /
+exp_avg_sq — stepped by ``zero_amd.zero2.ShardedOptimizer(torch.optim.Adam(lr=1e-3))`` at N GPUs.
+One *step* = one ``ShardedOptimizer.step()`` over the full parameter set with synthetic grads
+already resident in HBM: pack → RCCL reduce-scatter → fused Adam → RCCL all-gather → unpack
+(N=1: one fused Adam launch).  value = params/s = 3,075,098,624 / step time (whole job; total work
+is fixed as N grows → "strong" scaling).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]  (N>1 under torch.distributed.run)
+Prints ONE JSON line on rank 0 (plus diagnostics on stderr).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "distributed-training-sandbox_amd"))
+sys.path.insert(0, str(REPO))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured copy)
+METRIC = "ZeRO step time & params/sec at 1/2/4/8 GPU; Adam HBM GB/s vs peak"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(shapes, sample_elems: int, min_seconds: float = 10.0):
+    """The C oracle (oracle/adam_oracle.c, a restatement of torch.optim.Adam + ZeRO /ws) doing the
+    same N=1 ZeRO-2 step (bf16 grads → fp32 master/m/v → bf16 params) on a bounded sample."""
+    import numpy as np
+
+    from oracle import c_oracle
+
+    n = ntens = 0
+    for s in shapes:
+        k = int(np.prod(s))
+        if n + k > sample_elems and ntens:
+            break
+        n += k
+        ntens += 1
+    rng = np.random.default_rng(0)
+    master = (rng.standard_normal(n, dtype=np.float32) * 0.02)
+    g = (rng.standard_normal(n, dtype=np.float32) * 1e-3).view(np.uint32)
+    g = ((g + 0x7FFF + ((g >> 16) & 1)) >> 16).astype(np.uint16)
+    m = np.zeros(n, np.float32)
+    v = np.zeros(n, np.float32)
+    p = np.zeros(n, np.uint16)
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        steps += 1
+        c_oracle.adam_bf16(master, p, g, m, v, c_oracle.hparams(step=steps))
+        el = time.perf_counter() - t0
+        if el >= min_seconds or steps >= 200:
+            break
+    return dict(value=n * steps / el, unit="params/s", cores=c_oracle.num_threads(), kind="port",
+                sample=f"first {n:,} params (leading {ntens} tensors of the set), "
+                       f"{steps} steps of the ws=1 ZeRO-2 step (bf16 grads, fp32 master/m/v, "
+                       f"bf16 params out) by oracle/adam_oracle.c, {el:.1f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C4", choices=["C2", "C3", "C4", "C5"])
+    ap.add_argument("--zero", type=int, default=2, choices=[1, 2])
+    ap.add_argument("--layout", default="reference", choices=["reference", "flat"])
+    ap.add_argument("--bucket-mb", type=float, default=256.0)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=256 << 20)
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC HBM-bytes summary (profiles/*.json) for the roofline 'traffic' field")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from zero_amd import zero1, zero2
+    from zero_amd.shapes import CONFIGS
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29531")
+    dist.init_process_group("nccl" if world > 1 else "gloo", rank=rank, world_size=world,
+                            device_id=dev if world > 1 else None)
+
+    name, shape_fn = CONFIGS[args.config]
+    shapes = shape_fn()
+    total = int(sum(int(np.prod(s)) for s in shapes))
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(0)
+    params = []
+    for s in shapes:
+        t = torch.empty(s, dtype=torch.float32, device=dev).normal_(0.0, 0.02, generator=gen).to(dt)
+        params.append(torch.nn.Parameter(t))
+    gen.manual_seed(1000 * 0 + rank)
+    grads = []
+    for s in shapes:
+        grads.append((torch.empty(s, dtype=torch.float32, device=dev).normal_(generator=gen) * 1e-3).to(dt))
+    torch.cuda.synchronize()
+    mod = zero1 if args.zero == 1 else zero2
+    opt = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), layout=args.layout,
+                               bucket_mb=args.bucket_mb, sync=False)
+
+    def step():
+        for p, g in zip(params, grads):
+            p.grad = g
+        opt.step()
+
+    for _ in range(args.warmup):
+        step()
+    eng = opt.engine
+    eng.timing_events = []
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    eng_events = eng.timing_events
+    eng.timing_events = None
+    el_t = torch.tensor([el], dtype=torch.float64, device=dev if world > 1 else "cpu")
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    el = float(el_t.item())
+    ms = el / args.steps * 1e3
+
+    # Adam roofline: algorithmic bytes / kernel time, per launch, from HIP events on the launch stream
+    adam_ms = sum(a.elapsed_time(b) for a, b, _ in eng_events)
+    adam_bytes = sum(nb for _, _, nb in eng_events)
+    launches = len(eng_events)
+    achieved = adam_bytes / (adam_ms / 1e3) / 1e9 if adam_ms > 0 else 0.0
+    stats = torch.tensor([achieved, adam_ms / max(launches, 1), adam_bytes / max(launches, 1)],
+                         dtype=torch.float64, device=dev if world > 1 else "cpu")
+    if world > 1:  # report the slowest rank's Adam
+        dist.all_reduce(stats, op=dist.ReduceOp.MIN)
+    achieved = float(stats[0])
+    traffic = None
+    traffic_src = None
+    tj = Path(args.traffic_json) if args.traffic_json else None
+    if tj is not None and tj.exists():
+        d = json.loads(tj.read_text())
+        traffic = d.get("hbm_bytes_per_launch")
+        traffic_src = str(tj.relative_to(REPO) if tj.is_absolute() else tj)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": total / (ms / 1e3),
+            "unit": "params/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{args.config} {name} synthetic parameter set: ZeRO-{args.zero} "
+                            f"ShardedOptimizer(Adam lr=1e-3).step(), grads resident in HBM",
+                "params": total, "tensors": len(shapes),
+                "param_dtype": args.dtype, "grad_dtype": args.dtype,
+                "state_dtype": "fp32 (master, exp_avg, exp_avg_sq)",
+                "zero": args.zero, "layout": args.layout, "bucket_mb": args.bucket_mb,
+                "buckets": eng.K, "parallelism": f"dp{world}",
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "kernel": "adam_segments_kernel",
+                "avg_launch_ms": float(stats[1]), "alg_bytes_per_launch": float(stats[2]),
+                "launches_per_step": launches / args.steps,
+                "traffic_source": traffic_src,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(shapes, args.cpu_sample)
+        print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

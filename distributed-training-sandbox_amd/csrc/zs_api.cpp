@@ -1,0 +1,23 @@
+// ABI version and thread-local error reporting for the zero_amd C ABI.
+#include <cstdarg>
+#include <cstdio>
+
+#include "zs_common.h"
+
+namespace {
+thread_local char g_last_error[1024] = "";
+}
+
+namespace zs {
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(g_last_error, sizeof g_last_error, fmt, ap);
+  va_end(ap);
+}
+}  // namespace zs
+
+extern "C" {
+int zs_abi_version(void) { return ZS_ABI_VERSION; }
+const char* zs_last_error(void) { return g_last_error; }
+}

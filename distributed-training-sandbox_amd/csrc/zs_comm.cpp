@@ -1,0 +1,138 @@
+// RCCL over xGMI: one communicator per ShardedOptimizer, bucketed collectives on a caller stream.
+//
+// The reference issues one blocking c10d collective per parameter tensor (zero1.py:81-84,
+// zero1.py:95-102, zero2.py:94-113, zero2.py:126-133, zero3.py:38-39, zero3.py:146) followed by
+// torch.cuda.synchronize().  Here every collective moves a whole bucket and is only enqueued:
+// ordering against the pack / Adam / unpack kernels is by stream and event, never by host sync.
+//
+// Binding: the library links librccl.so.1 / libamdhip64.so.7 by SONAME; the Python loader imports
+// torch first so both resolve to torch's already-loaded copies (one HIP runtime, one RCCL).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <new>
+
+#include "zs_common.h"
+
+struct zs_comm {
+  ncclComm_t comm = nullptr;
+  int ws = 1, rank = 0;
+};
+
+static_assert(sizeof(ncclUniqueId) == ZS_UNIQUE_ID_BYTES, "ncclUniqueId size changed");
+
+#define ZS_NCCL(expr)                                                                   \
+  do {                                                                                  \
+    ncclResult_t r_ = (expr);                                                           \
+    if (r_ != ncclSuccess)                                                              \
+      return zs::fail(ZS_ERR_RCCL, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(r_), \
+                      __FILE__, __LINE__);                                              \
+  } while (0)
+
+static int to_nccl(int dtype, ncclDataType_t* t) {
+  switch (dtype) {
+    case ZS_F32: *t = ncclFloat32; return ZS_OK;
+    case ZS_BF16: *t = ncclBfloat16; return ZS_OK;
+    default: return zs::fail(ZS_ERR_INVALID, "unsupported dtype %d", dtype);
+  }
+}
+
+extern "C" {
+
+int zs_comm_unique_id(void* out128) {
+  ZS_REQUIRE(out128 != nullptr, "zs_comm_unique_id: out is NULL");
+  ncclUniqueId id;
+  ZS_NCCL(ncclGetUniqueId(&id));
+  std::memcpy(out128, &id, sizeof id);
+  return ZS_OK;
+}
+
+int zs_comm_init(const void* uid, int ws, int rank, zs_comm** out) {
+  ZS_REQUIRE(uid && out, "zs_comm_init: NULL argument");
+  *out = nullptr;
+  ZS_REQUIRE(ws >= 1 && rank >= 0 && rank < ws, "zs_comm_init: bad ws/rank %d/%d", ws, rank);
+  ncclUniqueId id;
+  std::memcpy(&id, uid, sizeof id);
+  zs_comm* c = new (std::nothrow) zs_comm();
+  if (!c) return zs::fail(ZS_ERR_NOMEM, "zs_comm_init: out of memory");
+  ncclResult_t r = ncclCommInitRank(&c->comm, ws, id, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    return zs::fail(ZS_ERR_RCCL, "ncclCommInitRank(ws=%d, rank=%d) failed: %s", ws, rank,
+                    ncclGetErrorString(r));
+  }
+  c->ws = ws;
+  c->rank = rank;
+  *out = c;
+  return ZS_OK;
+}
+
+int zs_comm_destroy(zs_comm* c) {
+  if (!c) return ZS_OK;
+  ncclResult_t r = c->comm ? ncclCommDestroy(c->comm) : ncclSuccess;
+  delete c;
+  if (r != ncclSuccess)
+    return zs::fail(ZS_ERR_RCCL, "ncclCommDestroy failed: %s", ncclGetErrorString(r));
+  return ZS_OK;
+}
+
+int zs_reduce_scatter(zs_comm* c, const void* send, void* recv, int64_t recv_count, int dtype,
+                      uintptr_t stream) {
+  ZS_REQUIRE(c && c->comm, "zs_reduce_scatter: NULL communicator");
+  ZS_REQUIRE(recv_count >= 0, "zs_reduce_scatter: recv_count < 0");
+  if (recv_count == 0) return ZS_OK;
+  ZS_REQUIRE(send && recv, "zs_reduce_scatter: NULL buffer");
+  ncclDataType_t t;
+  int rc = to_nccl(dtype, &t);
+  if (rc) return rc;
+  ZS_NCCL(ncclReduceScatter(send, recv, size_t(recv_count), t, ncclSum, c->comm,
+                            reinterpret_cast<hipStream_t>(stream)));
+  return ZS_OK;
+}
+
+int zs_all_gather(zs_comm* c, const void* send, void* recv, int64_t send_count, int dtype,
+                  uintptr_t stream) {
+  ZS_REQUIRE(c && c->comm, "zs_all_gather: NULL communicator");
+  ZS_REQUIRE(send_count >= 0, "zs_all_gather: send_count < 0");
+  if (send_count == 0) return ZS_OK;
+  ZS_REQUIRE(send && recv, "zs_all_gather: NULL buffer");
+  ncclDataType_t t;
+  int rc = to_nccl(dtype, &t);
+  if (rc) return rc;
+  ZS_NCCL(ncclAllGather(send, recv, size_t(send_count), t, c->comm,
+                        reinterpret_cast<hipStream_t>(stream)));
+  return ZS_OK;
+}
+
+int zs_all_reduce(zs_comm* c, const void* send, void* recv, int64_t count, int dtype,
+                  uintptr_t stream) {
+  ZS_REQUIRE(c && c->comm, "zs_all_reduce: NULL communicator");
+  ZS_REQUIRE(count >= 0, "zs_all_reduce: count < 0");
+  if (count == 0) return ZS_OK;
+  ZS_REQUIRE(send && recv, "zs_all_reduce: NULL buffer");
+  ncclDataType_t t;
+  int rc = to_nccl(dtype, &t);
+  if (rc) return rc;
+  ZS_NCCL(ncclAllReduce(send, recv, size_t(count), t, ncclSum, c->comm,
+                        reinterpret_cast<hipStream_t>(stream)));
+  return ZS_OK;
+}
+
+int zs_group_start(void) {
+  ZS_NCCL(ncclGroupStart());
+  return ZS_OK;
+}
+
+int zs_group_end(void) {
+  ZS_NCCL(ncclGroupEnd());
+  return ZS_OK;
+}
+
+int zs_rccl_version(int* version) {
+  ZS_REQUIRE(version != nullptr, "zs_rccl_version: NULL argument");
+  ZS_NCCL(ncclGetVersion(version));
+  return ZS_OK;
+}
+
+}  // extern "C"

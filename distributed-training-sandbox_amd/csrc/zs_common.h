@@ -1,0 +1,37 @@
+// Shared helpers for the zero_amd C ABI: thread-local error text and status mapping.
+#pragma once
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "../../include/zero_amd.h"
+
+namespace zs {
+
+void set_error(const char* fmt, ...);
+
+inline int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  set_error("%s", buf);
+  return code;
+}
+
+}  // namespace zs
+
+#define ZS_REQUIRE(cond, ...)                           \
+  do {                                                  \
+    if (!(cond)) return zs::fail(ZS_ERR_INVALID, __VA_ARGS__); \
+  } while (0)
+
+#define ZS_HIP(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return zs::fail(ZS_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                      __FILE__, __LINE__);                                             \
+  } while (0)

@@ -1,0 +1,509 @@
+// CDNA4 (gfx950) kernels of the ZeRO step: segment copy (pack / unpack) and the fused Adam.
+//
+// Both kernels are HBM-bound streaming kernels (no MFMA, no LDS): 64-wide waves, 256-thread
+// workgroups, 16-byte-per-lane coalesced accesses, a grid of ~8 workgroups per CU that strides over
+// fixed-size chunks of a segment table.  A workgroup finds the segment of its chunk with a forward
+// scan from the previous one (chunks are visited in increasing order), so the lookup is a couple of
+// scalar loads, not a per-chunk binary search.
+//
+// Tables (segment pointers + chunk prefix sums) are uploaded once per set and reused every step:
+// the step itself only launches kernels (no host sync), so it can be captured into a hipGraph.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "zs_common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int64_t kCopyChunkBytes = int64_t(kThreads) * 16 * 4;  // 16 KiB per workgroup step
+constexpr int kAdamGroups = 2;                                       // float4 groups per thread
+constexpr int64_t kAdamChunk = int64_t(kThreads) * 4 * kAdamGroups;  // 2048 elements
+
+int grid_cap() {
+  static int cap = 0;
+  if (cap == 0) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+      hipDeviceProp_t prop;
+      if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+        cus = prop.multiProcessorCount;
+    }
+    cap = cus * 8;
+  }
+  return cap;
+}
+
+// Kernel pointers live in the global address space; a plain pointer loaded from a table would
+// lower to flat_load/flat_store (which also count in lgkmcnt and complete out of order).
+#if defined(__HIP_DEVICE_COMPILE__)
+template <typename T>
+using gptr = __attribute__((address_space(1))) T*;
+#else
+template <typename T>
+using gptr = T*;
+#endif
+template <typename T>
+__device__ __forceinline__ gptr<T> glob(T* p) {
+  return (gptr<T>)p;
+}
+
+// ----------------------------------------------------------------------------------------------
+// segment copy
+// ----------------------------------------------------------------------------------------------
+struct CopySeg {
+  const unsigned char* src;  // nullptr = zero fill
+  unsigned char* dst;
+  int64_t nbytes;
+  int64_t vec;  // 1 if src and dst are 16-byte aligned (or src is null and dst aligned)
+};
+
+__global__ __launch_bounds__(kThreads) void copy_segments_kernel(
+    const CopySeg* __restrict__ segs, const int64_t* __restrict__ chunk_prefix, int64_t nseg,
+    int64_t total_chunks) {
+  int64_t seg = 0;
+  for (int64_t c = blockIdx.x; c < total_chunks; c += gridDim.x) {
+    while (chunk_prefix[seg + 1] <= c) ++seg;  // uniform forward scan
+    const CopySeg s = segs[seg];
+    const int64_t b0 = (c - chunk_prefix[seg]) * kCopyChunkBytes;
+    const int64_t b1 = min(b0 + kCopyChunkBytes, s.nbytes);
+    const gptr<const unsigned char> src = glob(s.src);
+    const gptr<unsigned char> dst = glob(s.dst);
+    if (s.vec) {
+      uint4 val[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // all loads first: 4 x 16 B in flight per lane
+        const int64_t off = b0 + (int64_t(u) * kThreads + threadIdx.x) * 16;
+        val[u] = make_uint4(0, 0, 0, 0);
+        if (src && off + 16 <= b1) val[u] = *reinterpret_cast<gptr<const uint4>>(src + off);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t off = b0 + (int64_t(u) * kThreads + threadIdx.x) * 16;
+        if (off + 16 <= b1) {
+          *reinterpret_cast<gptr<uint4>>(dst + off) = val[u];
+        } else if (off < b1) {
+          for (int64_t b = off; b < b1; ++b) dst[b] = src ? src[b] : 0;
+        }
+      }
+    } else {
+      for (int64_t b = b0 + threadIdx.x; b < b1; b += kThreads) dst[b] = src ? src[b] : 0;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------------
+// fused Adam
+// ----------------------------------------------------------------------------------------------
+struct AdamSeg {
+  const void* g;
+  const float* master;
+  float* master_out;
+  unsigned short* p_out;
+  float* m;
+  float* v;
+  float* vmax;
+  float* carry;
+  int64_t n;
+  int64_t vec;
+};
+
+struct HP {
+  float omb1, beta2, omb2, neg_step, bc2_sqrt, eps, wd, decay_mul, grad_div, inv_div, carry_mul;
+  int div_pow2, maximize;
+};
+
+__device__ __forceinline__ float bf16_to_f32(unsigned short h) {
+  return __uint_as_float(uint32_t(h) << 16);
+}
+
+__device__ __forceinline__ unsigned short f32_to_bf16(float f) {
+  // round-to-nearest-even; NaN stays NaN (plain cast lowers to v_cvt_pk_bf16_f32 on gfx950)
+  __bf16 h = static_cast<__bf16>(f);
+  unsigned short r;
+  __builtin_memcpy(&r, &h, 2);
+  return r;
+}
+
+// One element of torch.optim.Adam's single-tensor update (adam.py:394-547), in the rounding order
+// of torch's CPU kernels: lerp = fma(w, end-self, self) (ATen Lerp.h weight<0.5 branch),
+// exp_avg_sq.mul_(b2).addcmul_(g,g,1-b2) = fma((1-b2)*g, g, v*b2), denom = sqrt(v)/bc2_sqrt + eps,
+// param.addcdiv_(m, denom, -step_size) = p + (-step_size*m)/denom.  Only explicit fmaf() fuse;
+// sqrt and '/' are IEEE correctly rounded (-fhip-fp32-correctly-rounded-divide-sqrt).
+template <bool AMS, bool CARRY>
+__device__ __forceinline__ void adam_elem(float gsum, float& p, float& m, float& v, float& vmax,
+                                          float& carry, const HP& hp) {
+#pragma clang fp contract(off)
+  float s = gsum;
+  if constexpr (CARRY) s = s + hp.carry_mul * carry;  // ZeRO-1: Σ G + (ws-1)·A_{t-1}
+  // zero1.py:84 / zero2.py:111 `grad / ws`; a power-of-two divisor is an exact reciprocal multiply
+  float g = hp.div_pow2 ? s * hp.inv_div : s / hp.grad_div;
+  if constexpr (CARRY) carry = g;
+  if (hp.maximize) g = -g;
+  if (hp.wd != 0.0f) g = fmaf(hp.wd, p, g);  // grad.add(param, alpha=wd)
+  p = p * hp.decay_mul;                       // AdamW: param.mul_(1 - lr*wd); 1.0 otherwise
+  m = fmaf(hp.omb1, g - m, m);
+  v = fmaf(hp.omb2 * g, g, v * hp.beta2);
+  float vv = v;
+  if constexpr (AMS) {
+    vmax = fmaxf(vmax, v);
+    vv = vmax;
+  }
+  const float denom = sqrtf(vv) / hp.bc2_sqrt + hp.eps;
+  p = p + (hp.neg_step * m) / denom;
+}
+
+template <typename GT>
+__device__ __forceinline__ float load_g1(const void* g, int64_t i) {
+  if constexpr (sizeof(GT) == 4) return glob(static_cast<const float*>(g))[i];
+  else return bf16_to_f32(glob(static_cast<const unsigned short*>(g))[i]);
+}
+
+template <typename GT, bool AMS, bool CARRY>
+__device__ __attribute__((noinline)) void adam_scalar_range(const AdamSeg& s, int64_t i0, int64_t i1,
+                                                            int64_t stride, const HP& hp) {
+  for (int64_t i = i0; i < i1; i += stride) {
+    float gs = s.g ? load_g1<GT>(s.g, i) : 0.0f;
+    float p = glob(s.master)[i], m = glob(s.m)[i], v = glob(s.v)[i];
+    float vm = AMS ? glob(s.vmax)[i] : 0.0f;
+    float cr = CARRY ? glob(s.carry)[i] : 0.0f;
+    adam_elem<AMS, CARRY>(gs, p, m, v, vm, cr, hp);
+    if (s.master_out) glob(s.master_out)[i] = p;
+    if (s.p_out) glob(s.p_out)[i] = f32_to_bf16(p);
+    glob(s.m)[i] = m;
+    glob(s.v)[i] = v;
+    if constexpr (AMS) glob(s.vmax)[i] = vm;
+    if constexpr (CARRY) glob(s.carry)[i] = cr;
+  }
+}
+
+template <typename GT>
+__device__ __forceinline__ float4 load_g4(const void* g, int64_t i) {
+  if constexpr (sizeof(GT) == 4) {
+    return *reinterpret_cast<gptr<const float4>>(glob(static_cast<const float*>(g)) + i);
+  } else {
+    const uint2 r =
+        *reinterpret_cast<gptr<const uint2>>(glob(static_cast<const unsigned short*>(g)) + i);
+    return make_float4(__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u),
+                       __uint_as_float(r.y << 16), __uint_as_float(r.y & 0xffff0000u));
+  }
+}
+
+__device__ __forceinline__ float4 ld4(const float* p, int64_t i) {
+  return *reinterpret_cast<gptr<const float4>>(glob(p) + i);
+}
+__device__ __forceinline__ void st4(float* p, int64_t i, float4 x) {
+  *reinterpret_cast<gptr<float4>>(glob(p) + i) = x;
+}
+
+template <typename GT, bool AMS, bool CARRY>
+__global__ __launch_bounds__(kThreads) void adam_segments_kernel(
+    const AdamSeg* __restrict__ segs, const int64_t* __restrict__ chunk_prefix, int64_t nseg,
+    int64_t total_chunks, HP hp) {
+  int64_t seg = 0;
+  for (int64_t c = blockIdx.x; c < total_chunks; c += gridDim.x) {
+    while (chunk_prefix[seg + 1] <= c) ++seg;
+    const AdamSeg s = segs[seg];
+    const int64_t e0 = (c - chunk_prefix[seg]) * kAdamChunk;
+    const int64_t e1 = min(e0 + kAdamChunk, s.n);
+    if (!s.vec) {
+      adam_scalar_range<GT, AMS, CARRY>(s, e0 + threadIdx.x, e1, kThreads, hp);
+      continue;
+    }
+    // Vector path: kAdamGroups float4 groups per thread, lane-contiguous (16 B per lane per
+    // access) so every wave instruction touches one contiguous 1 KiB (f32) / 512 B (bf16) run.
+    float4 g4[kAdamGroups], p4[kAdamGroups], m4[kAdamGroups], v4[kAdamGroups];
+    float4 x4[kAdamGroups], c4[kAdamGroups];
+#pragma unroll
+    for (int u = 0; u < kAdamGroups; ++u) {
+      const int64_t i = e0 + (int64_t(u) * kThreads + threadIdx.x) * 4;
+      if (i + 4 <= e1) {
+        g4[u] = s.g ? load_g4<GT>(s.g, i) : make_float4(0.f, 0.f, 0.f, 0.f);
+        p4[u] = ld4(s.master, i);
+        m4[u] = ld4(s.m, i);
+        v4[u] = ld4(s.v, i);
+        if constexpr (AMS) x4[u] = ld4(s.vmax, i);
+        if constexpr (CARRY) c4[u] = ld4(s.carry, i);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kAdamGroups; ++u) {
+      const int64_t i = e0 + (int64_t(u) * kThreads + threadIdx.x) * 4;
+      if (i + 4 <= e1) {
+        float* gp = reinterpret_cast<float*>(&g4[u]);
+        float* pp = reinterpret_cast<float*>(&p4[u]);
+        float* mp = reinterpret_cast<float*>(&m4[u]);
+        float* vp = reinterpret_cast<float*>(&v4[u]);
+        float* xp = reinterpret_cast<float*>(&x4[u]);
+        float* cp = reinterpret_cast<float*>(&c4[u]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float xv = AMS ? xp[j] : 0.0f;
+          float cv = CARRY ? cp[j] : 0.0f;
+          adam_elem<AMS, CARRY>(gp[j], pp[j], mp[j], vp[j], xv, cv, hp);
+          if constexpr (AMS) xp[j] = xv;
+          if constexpr (CARRY) cp[j] = cv;
+        }
+        if (s.master_out) st4(s.master_out, i, p4[u]);
+        if (s.p_out) {
+          uint2 r;
+          r.x = uint32_t(f32_to_bf16(pp[0])) | (uint32_t(f32_to_bf16(pp[1])) << 16);
+          r.y = uint32_t(f32_to_bf16(pp[2])) | (uint32_t(f32_to_bf16(pp[3])) << 16);
+          *reinterpret_cast<gptr<uint2>>(glob(s.p_out) + i) = r;
+        }
+        st4(s.m, i, m4[u]);
+        st4(s.v, i, v4[u]);
+        if constexpr (AMS) st4(s.vmax, i, x4[u]);
+        if constexpr (CARRY) st4(s.carry, i, c4[u]);
+      } else if (i < e1) {
+        adam_scalar_range<GT, AMS, CARRY>(s, i, e1, 1, hp);
+      }
+    }
+  }
+}
+
+inline bool aligned(uint64_t p, uint64_t a) { return p % a == 0; }
+
+}  // namespace
+
+struct zs_copyset {
+  CopySeg* d_segs = nullptr;
+  int64_t* d_prefix = nullptr;
+  int64_t nseg = 0, total_chunks = 0;
+};
+
+struct zs_adamset {
+  AdamSeg* d_segs = nullptr;
+  int64_t* d_prefix = nullptr;
+  int64_t nseg = 0, total_chunks = 0, elems = 0, bytes = 0;
+  int g_dtype = ZS_F32, p_dtype = ZS_BF16, has_carry = 0, has_vmax = 0;
+};
+
+template <typename T>
+static int upload(const std::vector<T>& h, T** d) {
+  *d = nullptr;
+  if (h.empty()) return ZS_OK;
+  ZS_HIP(hipMalloc(reinterpret_cast<void**>(d), h.size() * sizeof(T)));
+  hipError_t e = hipMemcpy(*d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(*d);
+    *d = nullptr;
+    return zs::fail(ZS_ERR_HIP, "table upload failed: %s", hipGetErrorString(e));
+  }
+  return ZS_OK;
+}
+
+extern "C" {
+
+int zs_copyset_create(const uint64_t* src, const uint64_t* dst, const int64_t* nbytes, int64_t n,
+                      zs_copyset** out) {
+  ZS_REQUIRE(out != nullptr, "zs_copyset_create: out is NULL");
+  *out = nullptr;
+  ZS_REQUIRE(n >= 0, "zs_copyset_create: n < 0");
+  ZS_REQUIRE(n == 0 || (src && dst && nbytes), "zs_copyset_create: NULL table");
+  std::vector<CopySeg> segs;
+  std::vector<int64_t> prefix(1, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    ZS_REQUIRE(nbytes[i] >= 0, "zs_copyset_create: nbytes[%lld] < 0", (long long)i);
+    if (nbytes[i] == 0) continue;
+    ZS_REQUIRE(dst[i] != 0, "zs_copyset_create: dst[%lld] is NULL", (long long)i);
+    CopySeg s;
+    s.src = reinterpret_cast<const unsigned char*>(src[i]);
+    s.dst = reinterpret_cast<unsigned char*>(dst[i]);
+    s.nbytes = nbytes[i];
+    s.vec = aligned(src[i], 16) && aligned(dst[i], 16) ? 1 : 0;
+    segs.push_back(s);
+    prefix.push_back(prefix.back() + (nbytes[i] + kCopyChunkBytes - 1) / kCopyChunkBytes);
+  }
+  zs_copyset* cs = new (std::nothrow) zs_copyset();
+  if (!cs) return zs::fail(ZS_ERR_NOMEM, "zs_copyset_create: out of memory");
+  cs->nseg = int64_t(segs.size());
+  cs->total_chunks = prefix.back();
+  int rc = upload(segs, &cs->d_segs);
+  if (rc == ZS_OK) rc = upload(prefix, &cs->d_prefix);
+  if (rc != ZS_OK) {
+    zs_copyset_destroy(cs);
+    return rc;
+  }
+  *out = cs;
+  return ZS_OK;
+}
+
+int zs_copyset_run(const zs_copyset* cs, uintptr_t stream) {
+  ZS_REQUIRE(cs != nullptr, "zs_copyset_run: NULL set");
+  if (cs->total_chunks == 0) return ZS_OK;
+  const int grid = int(std::min<int64_t>(cs->total_chunks, grid_cap()));
+  hipLaunchKernelGGL(copy_segments_kernel, dim3(grid), dim3(kThreads), 0,
+                     reinterpret_cast<hipStream_t>(stream), cs->d_segs, cs->d_prefix, cs->nseg,
+                     cs->total_chunks);
+  ZS_HIP(hipGetLastError());
+  return ZS_OK;
+}
+
+int zs_copyset_destroy(zs_copyset* cs) {
+  if (!cs) return ZS_OK;
+  if (cs->d_segs) (void)hipFree(cs->d_segs);
+  if (cs->d_prefix) (void)hipFree(cs->d_prefix);
+  delete cs;
+  return ZS_OK;
+}
+
+int zs_adam_hparams_init(double lr, double beta1, double beta2, double eps, double weight_decay,
+                         int decoupled, int amsgrad, int maximize, int64_t step, double grad_div,
+                         double carry_mul, zs_adam_hparams* hp) {
+  ZS_REQUIRE(hp != nullptr, "zs_adam_hparams_init: hp is NULL");
+  ZS_REQUIRE(step >= 1, "zs_adam_hparams_init: step must be >= 1");
+  ZS_REQUIRE(grad_div > 0.0, "zs_adam_hparams_init: grad_div must be > 0");
+  // adam.py:508-515 (non-capturable): Python-float (double) scalars.
+  const double t = double(step);
+  const double bc1 = 1.0 - std::pow(beta1, t);
+  const double bc2 = 1.0 - std::pow(beta2, t);
+  hp->one_minus_beta1 = float(1.0 - beta1);
+  hp->beta2 = float(beta2);
+  hp->one_minus_beta2 = float(1.0 - beta2);
+  hp->neg_step_size = float(-(lr / bc1));
+  hp->bc2_sqrt = float(std::pow(bc2, 0.5));
+  hp->eps = float(eps);
+  hp->weight_decay = decoupled ? 0.0f : float(weight_decay);
+  hp->decay_mul = decoupled ? float(1.0 - lr * weight_decay) : 1.0f;
+  hp->grad_div = float(grad_div);
+  hp->carry_mul = float(carry_mul);
+  hp->amsgrad = amsgrad ? 1 : 0;
+  hp->maximize = maximize ? 1 : 0;
+  return ZS_OK;
+}
+
+int zs_adamset_create(const zs_adam_seg* in, int64_t n, int g_dtype, int p_dtype,
+                      zs_adamset** out) {
+  ZS_REQUIRE(out != nullptr, "zs_adamset_create: out is NULL");
+  *out = nullptr;
+  ZS_REQUIRE(n >= 0 && (n == 0 || in), "zs_adamset_create: bad table");
+  ZS_REQUIRE(g_dtype == ZS_F32 || g_dtype == ZS_BF16, "zs_adamset_create: bad g_dtype %d", g_dtype);
+  ZS_REQUIRE(p_dtype == ZS_BF16, "zs_adamset_create: p_out must be bf16 (got %d)", p_dtype);
+  const uint64_t ga = g_dtype == ZS_F32 ? 16 : 8;
+  std::vector<AdamSeg> segs;
+  std::vector<int64_t> prefix(1, 0);
+  int carry_state = -1, vmax_state = -1;
+  int64_t elems = 0, bytes = 0;
+  const int64_t gsz = g_dtype == ZS_F32 ? 4 : 2;
+  for (int64_t i = 0; i < n; ++i) {
+    const zs_adam_seg& s = in[i];
+    ZS_REQUIRE(s.n >= 0, "zs_adamset_create: seg %lld n < 0", (long long)i);
+    if (s.n == 0) continue;
+    ZS_REQUIRE(s.master && s.m && s.v, "zs_adamset_create: seg %lld missing master/m/v",
+               (long long)i);
+    const int c = s.carry ? 1 : 0;
+    ZS_REQUIRE(carry_state < 0 || carry_state == c,
+               "zs_adamset_create: carry must be set on all segments or none");
+    carry_state = c;
+    const int x = s.vmax ? 1 : 0;
+    ZS_REQUIRE(vmax_state < 0 || vmax_state == x,
+               "zs_adamset_create: vmax must be set on all segments or none");
+    vmax_state = x;
+    AdamSeg d;
+    d.g = reinterpret_cast<const void*>(s.g);
+    d.master = reinterpret_cast<const float*>(s.master);
+    d.master_out = reinterpret_cast<float*>(s.master_out);
+    d.p_out = reinterpret_cast<unsigned short*>(s.p_out);
+    d.m = reinterpret_cast<float*>(s.m);
+    d.v = reinterpret_cast<float*>(s.v);
+    d.vmax = reinterpret_cast<float*>(s.vmax);
+    d.carry = reinterpret_cast<float*>(s.carry);
+    d.n = s.n;
+    d.vec = aligned(s.g, ga) && aligned(s.master, 16) && aligned(s.master_out, 16) &&
+                    aligned(s.p_out, 8) && aligned(s.m, 16) && aligned(s.v, 16) &&
+                    aligned(s.vmax, 16) && aligned(s.carry, 16)
+                ? 1
+                : 0;
+    segs.push_back(d);
+    prefix.push_back(prefix.back() + (s.n + kAdamChunk - 1) / kAdamChunk);
+    elems += s.n;
+    int64_t b = (s.g ? gsz : 0) + 4 /*master*/ + 8 /*m*/ + 8 /*v*/;
+    if (s.master_out) b += 4;
+    if (s.p_out) b += 2;
+    if (s.vmax) b += 8;
+    if (s.carry) b += 8;
+    bytes += b * s.n;
+  }
+  zs_adamset* as = new (std::nothrow) zs_adamset();
+  if (!as) return zs::fail(ZS_ERR_NOMEM, "zs_adamset_create: out of memory");
+  as->nseg = int64_t(segs.size());
+  as->total_chunks = prefix.back();
+  as->elems = elems;
+  as->bytes = bytes;
+  as->g_dtype = g_dtype;
+  as->p_dtype = p_dtype;
+  as->has_carry = carry_state > 0 ? 1 : 0;
+  as->has_vmax = vmax_state > 0 ? 1 : 0;
+  int rc = upload(segs, &as->d_segs);
+  if (rc == ZS_OK) rc = upload(prefix, &as->d_prefix);
+  if (rc != ZS_OK) {
+    zs_adamset_destroy(as);
+    return rc;
+  }
+  *out = as;
+  return ZS_OK;
+}
+
+int zs_adamset_run(const zs_adamset* as, const zs_adam_hparams* h, uintptr_t stream) {
+  ZS_REQUIRE(as && h, "zs_adamset_run: NULL argument");
+  if (as->total_chunks == 0) return ZS_OK;
+  HP hp;
+  hp.omb1 = h->one_minus_beta1;
+  hp.beta2 = h->beta2;
+  hp.omb2 = h->one_minus_beta2;
+  hp.neg_step = h->neg_step_size;
+  hp.bc2_sqrt = h->bc2_sqrt;
+  hp.eps = h->eps;
+  hp.wd = h->weight_decay;
+  hp.decay_mul = h->decay_mul;
+  hp.grad_div = h->grad_div;
+  hp.carry_mul = h->carry_mul;
+  int exp2 = 0;
+  hp.div_pow2 = std::frexp(double(h->grad_div), &exp2) == 0.5 ? 1 : 0;
+  hp.inv_div = float(1.0 / double(h->grad_div));
+  hp.maximize = h->maximize;
+  const bool ams = h->amsgrad != 0, carry = as->has_carry != 0;
+  ZS_REQUIRE(!ams || as->has_vmax || as->nseg == 0, "zs_adamset_run: amsgrad needs vmax segments");
+  const int grid = int(std::min<int64_t>(as->total_chunks, grid_cap()));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define ZS_LAUNCH_ADAM(GT, A, C)                                                          \
+  hipLaunchKernelGGL((adam_segments_kernel<GT, A, C>), dim3(grid), dim3(kThreads), 0, st, \
+                     as->d_segs, as->d_prefix, as->nseg, as->total_chunks, hp)
+  if (as->g_dtype == ZS_F32) {
+    if (ams && carry) ZS_LAUNCH_ADAM(float, true, true);
+    else if (ams) ZS_LAUNCH_ADAM(float, true, false);
+    else if (carry) ZS_LAUNCH_ADAM(float, false, true);
+    else ZS_LAUNCH_ADAM(float, false, false);
+  } else {
+    if (ams && carry) ZS_LAUNCH_ADAM(unsigned short, true, true);
+    else if (ams) ZS_LAUNCH_ADAM(unsigned short, true, false);
+    else if (carry) ZS_LAUNCH_ADAM(unsigned short, false, true);
+    else ZS_LAUNCH_ADAM(unsigned short, false, false);
+  }
+#undef ZS_LAUNCH_ADAM
+  ZS_HIP(hipGetLastError());
+  return ZS_OK;
+}
+
+int zs_adamset_destroy(zs_adamset* as) {
+  if (!as) return ZS_OK;
+  if (as->d_segs) (void)hipFree(as->d_segs);
+  if (as->d_prefix) (void)hipFree(as->d_prefix);
+  delete as;
+  return ZS_OK;
+}
+
+int zs_adamset_stats(const zs_adamset* as, int64_t* elems, int64_t* bytes) {
+  ZS_REQUIRE(as && elems && bytes, "zs_adamset_stats: NULL argument");
+  *elems = as->elems;
+  *bytes = as->bytes;
+  return ZS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,239 @@
+// Layout planner: parameter ownership, per-rank optimizer-shard streams and bucket segments.
+//
+// Host-only (no HIP calls), so it runs in the CPU test suite.  Ownership follows the reference's
+// ShardedOptimizer.__init__ exactly (zero1.py:55-62, zero2.py:51-58, zero3.py:93-100):
+//     ppr = n // ws, rem = n % ws
+//     start_r = r*ppr + min(r, rem), end_r = start_r + ppr + (r < rem)
+// and the broadcast owner of index i (zero1.py:95-100, zero2.py:126-131):
+//     i < (ppr+1)*rem ? i // (ppr+1) : (i - rem) // ppr
+//
+// A rank's *stream* is the ordered list of pieces whose optimizer state it owns; pieces start at
+// multiples of align_elems so that every device access can be 16-byte vectorised.  A bucket k
+// concatenates, rank-major, the window [kW, (k+1)W) of every rank's stream, which is exactly the
+// buffer one equal-count reduce-scatter / all-gather moves (Layout R / Layout Z).
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "zs_common.h"
+
+namespace {
+
+struct Piece {
+  int64_t param, param_off, stream_off, len;
+};
+struct Seg {
+  int64_t param, rank, param_off, buf_off, len;
+};
+
+inline int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+struct zs_plan {
+  int64_t n = 0;
+  int ws = 1, rank = 0, layout = 0;
+  int64_t align = 1, W = 0, K = 0, M = 0;
+  std::vector<int64_t> numel;
+  std::vector<std::vector<Piece>> pieces;  // per rank
+  std::vector<int64_t> stream_len;         // per rank
+  std::vector<std::vector<Seg>> segs;      // per bucket
+};
+
+static void owner_range(int64_t n, int ws, int r, int64_t* s, int64_t* e) {
+  const int64_t ppr = n / ws, rem = n % ws;
+  *s = r * ppr + std::min<int64_t>(r, rem);
+  *e = *s + ppr + (r < rem ? 1 : 0);
+}
+
+static int owner_of(int64_t n, int ws, int64_t i) {
+  const int64_t ppr = n / ws, rem = n % ws;
+  if (i < (ppr + 1) * rem) return int(i / (ppr + 1));
+  return int((i - rem) / ppr);
+}
+
+extern "C" {
+
+int zs_plan_create(int64_t n_params, const int64_t* numels, const int64_t* dim0, int ws, int rank,
+                   int layout, int64_t align_elems, int64_t window_elems, zs_plan** out) {
+  ZS_REQUIRE(out != nullptr, "zs_plan_create: out is NULL");
+  *out = nullptr;
+  ZS_REQUIRE(n_params >= 0, "zs_plan_create: n_params < 0");
+  ZS_REQUIRE(n_params == 0 || numels != nullptr, "zs_plan_create: numels is NULL");
+  ZS_REQUIRE(ws >= 1, "zs_plan_create: ws must be >= 1 (got %d)", ws);
+  ZS_REQUIRE(rank >= 0 && rank < ws, "zs_plan_create: rank %d out of [0,%d)", rank, ws);
+  ZS_REQUIRE(layout == ZS_LAYOUT_R || layout == ZS_LAYOUT_Z || layout == ZS_LAYOUT_F,
+             "zs_plan_create: unknown layout %d", layout);
+  ZS_REQUIRE(align_elems >= 1, "zs_plan_create: align_elems must be >= 1");
+  ZS_REQUIRE(window_elems >= 0, "zs_plan_create: window_elems < 0");
+  ZS_REQUIRE(layout != ZS_LAYOUT_Z || dim0 != nullptr, "zs_plan_create: layout Z needs dim0");
+  for (int64_t i = 0; i < n_params; ++i) {
+    ZS_REQUIRE(numels[i] >= 0, "zs_plan_create: numel[%lld] < 0", (long long)i);
+    if (layout == ZS_LAYOUT_Z) {
+      ZS_REQUIRE((dim0[i] == 0 && numels[i] == 0) || (dim0[i] >= 1 && numels[i] % dim0[i] == 0),
+                 "zs_plan_create: param %lld numel %lld not divisible by dim0 %lld", (long long)i,
+                 (long long)numels[i], (long long)dim0[i]);
+    }
+  }
+
+  zs_plan* p = new (std::nothrow) zs_plan();
+  if (!p) return zs::fail(ZS_ERR_NOMEM, "zs_plan_create: out of memory");
+  p->n = n_params;
+  p->ws = ws;
+  p->rank = rank;
+  p->layout = layout;
+  p->align = align_elems;
+  p->numel.assign(numels, numels + n_params);
+  p->pieces.assign(ws, {});
+  p->stream_len.assign(ws, 0);
+
+  if (layout == ZS_LAYOUT_R) {
+    for (int r = 0; r < ws; ++r) {
+      int64_t s, e, off = 0;
+      owner_range(n_params, ws, r, &s, &e);
+      for (int64_t i = s; i < e; ++i) {
+        p->pieces[r].push_back({i, 0, off, numels[i]});
+        off = round_up(off + numels[i], align_elems);
+      }
+      p->stream_len[r] = off;
+    }
+  } else if (layout == ZS_LAYOUT_Z) {
+    std::vector<int64_t> off(ws, 0);
+    for (int64_t i = 0; i < n_params; ++i) {
+      const int64_t d0 = dim0[i], row = d0 ? numels[i] / d0 : 0;
+      const int64_t cs = (d0 + ws - 1) / ws;  // torch.chunk: ceil(d0/ws) rows per chunk
+      for (int r = 0; r < ws; ++r) {
+        const int64_t r0 = std::min<int64_t>(int64_t(r) * cs, d0);
+        const int64_t r1 = std::min<int64_t>(int64_t(r + 1) * cs, d0);
+        const int64_t len = (r1 - r0) * row;
+        p->pieces[r].push_back({i, r0 * row, off[r], len});  // zero-length kept: index = param
+        off[r] = round_up(off[r] + len, align_elems);
+      }
+    }
+    for (int r = 0; r < ws; ++r) p->stream_len[r] = off[r];
+  } else {  // ZS_LAYOUT_F: balanced contiguous slices of the aligned concatenation
+    std::vector<int64_t> goff(n_params);
+    int64_t T = 0;
+    for (int64_t i = 0; i < n_params; ++i) {
+      goff[i] = T;
+      T = round_up(T + numels[i], align_elems);
+    }
+    const int64_t S = round_up((T + ws - 1) / ws, align_elems);
+    for (int r = 0; r < ws; ++r) {
+      const int64_t lo = int64_t(r) * S, hi = lo + S;
+      for (int64_t i = 0; i < n_params; ++i) {
+        const int64_t a = std::max(lo, goff[i]), b = std::min(hi, goff[i] + numels[i]);
+        if (a < b) p->pieces[r].push_back({i, a - goff[i], a - lo, b - a});
+      }
+      p->stream_len[r] = S;
+    }
+  }
+
+  p->M = 0;
+  for (int r = 0; r < ws; ++r) p->M = std::max(p->M, p->stream_len[r]);
+  int64_t W = window_elems == 0 ? p->M : round_up(window_elems, align_elems);
+  if (W > p->M) W = p->M;
+  p->W = W;
+  p->K = (W == 0) ? 0 : (p->M + W - 1) / W;
+  p->segs.assign(p->K, {});
+  for (int r = 0; r < ws; ++r) {
+    for (const Piece& pc : p->pieces[r]) {
+      if (pc.len == 0) continue;
+      const int64_t k0 = pc.stream_off / W, k1 = (pc.stream_off + pc.len - 1) / W;
+      for (int64_t k = k0; k <= k1; ++k) {
+        const int64_t lo = std::max(pc.stream_off, k * W);
+        const int64_t hi = std::min(pc.stream_off + pc.len, (k + 1) * W);
+        p->segs[k].push_back({pc.param, r, pc.param_off + (lo - pc.stream_off),
+                              int64_t(r) * W + (lo - k * W), hi - lo});
+      }
+    }
+  }
+  *out = p;
+  return ZS_OK;
+}
+
+int zs_plan_destroy(zs_plan* plan) {
+  delete plan;
+  return ZS_OK;
+}
+
+int zs_plan_info(const zs_plan* p, int64_t* info) {
+  ZS_REQUIRE(p && info, "zs_plan_info: NULL argument");
+  info[0] = p->n;
+  info[1] = p->ws;
+  info[2] = p->rank;
+  info[3] = p->layout;
+  info[4] = p->W;
+  info[5] = p->K;
+  info[6] = p->M;
+  return ZS_OK;
+}
+
+int zs_plan_owner_range(const zs_plan* p, int rank, int64_t* start, int64_t* end) {
+  ZS_REQUIRE(p && start && end, "zs_plan_owner_range: NULL argument");
+  ZS_REQUIRE(rank >= 0 && rank < p->ws, "zs_plan_owner_range: rank %d out of range", rank);
+  owner_range(p->n, p->ws, rank, start, end);
+  return ZS_OK;
+}
+
+int zs_plan_owner_of(const zs_plan* p, int64_t i, int* owner) {
+  ZS_REQUIRE(p && owner, "zs_plan_owner_of: NULL argument");
+  ZS_REQUIRE(i >= 0 && i < p->n, "zs_plan_owner_of: index %lld out of range", (long long)i);
+  *owner = owner_of(p->n, p->ws, i);
+  return ZS_OK;
+}
+
+int zs_plan_stream_len(const zs_plan* p, int rank, int64_t* len) {
+  ZS_REQUIRE(p && len, "zs_plan_stream_len: NULL argument");
+  ZS_REQUIRE(rank >= 0 && rank < p->ws, "zs_plan_stream_len: rank %d out of range", rank);
+  *len = p->stream_len[rank];
+  return ZS_OK;
+}
+
+int zs_plan_num_pieces(const zs_plan* p, int rank, int64_t* n) {
+  ZS_REQUIRE(p && n, "zs_plan_num_pieces: NULL argument");
+  ZS_REQUIRE(rank >= 0 && rank < p->ws, "zs_plan_num_pieces: rank %d out of range", rank);
+  *n = int64_t(p->pieces[rank].size());
+  return ZS_OK;
+}
+
+int zs_plan_pieces(const zs_plan* p, int rank, int64_t* param, int64_t* param_off,
+                   int64_t* stream_off, int64_t* len) {
+  ZS_REQUIRE(p && param && param_off && stream_off && len, "zs_plan_pieces: NULL argument");
+  ZS_REQUIRE(rank >= 0 && rank < p->ws, "zs_plan_pieces: rank %d out of range", rank);
+  const auto& v = p->pieces[rank];
+  for (size_t j = 0; j < v.size(); ++j) {
+    param[j] = v[j].param;
+    param_off[j] = v[j].param_off;
+    stream_off[j] = v[j].stream_off;
+    len[j] = v[j].len;
+  }
+  return ZS_OK;
+}
+
+int zs_plan_num_segments(const zs_plan* p, int64_t bucket, int64_t* n) {
+  ZS_REQUIRE(p && n, "zs_plan_num_segments: NULL argument");
+  ZS_REQUIRE(bucket >= 0 && bucket < p->K, "zs_plan_num_segments: bucket %lld out of range",
+             (long long)bucket);
+  *n = int64_t(p->segs[bucket].size());
+  return ZS_OK;
+}
+
+int zs_plan_segments(const zs_plan* p, int64_t bucket, int64_t* param, int64_t* rank,
+                     int64_t* param_off, int64_t* buf_off, int64_t* len) {
+  ZS_REQUIRE(p && param && rank && param_off && buf_off && len, "zs_plan_segments: NULL argument");
+  ZS_REQUIRE(bucket >= 0 && bucket < p->K, "zs_plan_segments: bucket %lld out of range",
+             (long long)bucket);
+  const auto& v = p->segs[bucket];
+  for (size_t j = 0; j < v.size(); ++j) {
+    param[j] = v[j].param;
+    rank[j] = v[j].rank;
+    param_off[j] = v[j].param_off;
+    buf_off[j] = v[j].buf_off;
+    len[j] = v[j].len;
+  }
+  return ZS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,181 @@
+"""Shared body of the ZeRO-1 / ZeRO-2 ``ShardedOptimizer`` drop-ins.
+
+The public surface is the reference's: ``ShardedOptimizer(optimizer)``,
+``.step(closure=None)``, ``.zero_grad()``, attributes ``optimizer``, ``original_param_groups``,
+``params``, ``local_param_indices``, ``local_params``, ``step_time``, ``communication_time``,
+``broadcast_count``; the inner optimizer's ``param_groups`` are filtered to the owned parameters
+(zero1.py:71-74) and ``optimizer.state[p]`` holds ``step`` / ``exp_avg`` / ``exp_avg_sq`` for
+every owned parameter (read by memory.py:15-24).  Everything below ``step()`` is the native
+engine (engine.py → libzero_amd.so); the inner torch optimizer's own ``step`` is never called.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+import torch.distributed as dist
+from torch.optim import Optimizer
+
+from .engine import ShardEngine
+from .training_utils.utils import get
+
+
+def adam_group_hparams(group: dict, optimizer: Optimizer) -> dict:
+    """Hyper-parameters of one torch.optim.Adam / AdamW param group (adam.py:38-90)."""
+    lr = group["lr"]
+    lr = float(lr.item()) if torch.is_tensor(lr) else float(lr)
+    beta1, beta2 = group["betas"]
+    decoupled = bool(group.get("decoupled_weight_decay", False)) or isinstance(
+        optimizer, torch.optim.AdamW)
+    return dict(lr=lr, beta1=float(beta1), beta2=float(beta2), eps=float(group["eps"]),
+                weight_decay=float(group["weight_decay"]), amsgrad=bool(group.get("amsgrad", False)),
+                maximize=bool(group.get("maximize", False)), decoupled=decoupled)
+
+
+class ShardedOptimizerBase:
+    """ZeRO-1/2 wrapper; subclasses set ``_carry`` (ZeRO-1 gradient carry) and ``_variant``."""
+
+    _carry = False
+    _variant = 2
+
+    def __init__(self, optimizer: Optimizer, *, layout: str = "reference",
+                 bucket_mb: float = 256.0, comm=None, sync: bool = True):
+        if not isinstance(optimizer, torch.optim.Adam):
+            raise TypeError("zero_amd ShardedOptimizer wraps torch.optim.Adam / AdamW "
+                            f"(got {type(optimizer).__name__})")
+        self.optimizer = optimizer
+        self.original_param_groups = optimizer.param_groups
+        self.params = [p for group in self.original_param_groups for p in group["params"]]
+        self._group_of = [gi for gi, group in enumerate(self.original_param_groups)
+                          for _ in group["params"]]
+        # references to the unfiltered groups' hyper-parameter dicts (lr schedulers mutate these)
+        self._groups = list(self.original_param_groups)
+
+        world_size = get("ws")
+        rank = get("rank")
+        # zero1.py:55-62 / zero2.py:51-58 (the planner computes the same ranges natively)
+        params_per_rank = len(self.params) // world_size
+        remainder = len(self.params) % world_size
+        start_idx = rank * params_per_rank + min(rank, remainder)
+        end_idx = start_idx + params_per_rank + (1 if rank < remainder else 0)
+        self.local_param_indices = list(range(start_idx, end_idx))
+        self.local_params = set(self.params[i] for i in self.local_param_indices)
+        self._shard_optimizer_params()
+
+        self.broadcast_count = 0
+        self.communication_time = 0.0
+        self.step_time = 0.0
+        self.world_size, self.rank = world_size, rank
+        self._layout = layout
+        self._bucket_bytes = int(bucket_mb * (1 << 20))
+        self._comm = comm
+        self._sync = sync
+        self.engine: ShardEngine | None = None
+        self._step_tensors = {}
+
+    def _shard_optimizer_params(self):
+        """zero1.py:71-74: drop non-owned params from the inner optimizer's groups."""
+        for group in self.optimizer.param_groups:
+            group["params"] = [p for p in group["params"] if p in self.local_params]
+
+    # ------------------------------------------------------------------------------------------
+    def _build_engine(self):
+        comm = self._comm
+        if self.world_size > 1 and comm is None:
+            from .comm import RcclComm
+            comm = RcclComm()
+            self._comm = comm
+        self.engine = ShardEngine(self.params, self._group_of, self.world_size, self.rank,
+                                  layout=self._layout, carry=self._carry, comm=comm,
+                                  bucket_bytes=self._bucket_bytes)
+        if self.engine.plan.layout != 0:
+            return
+        self._expose_state()
+
+    def _expose_state(self):
+        """optimizer.state[p] = {'step', 'exp_avg', 'exp_avg_sq'} as views of the flat shard."""
+        eng = self.engine
+        for i in eng.owned_param_indices():
+            p = self.params[i]
+            views = eng.state_views(i)
+            if views is None:
+                continue
+            st = self.optimizer.state[p]
+            st.update(views)
+            if eng.vmax is not None:
+                so = int(eng.pieces.stream_off[eng.pieces.param == i][0])
+                st["max_exp_avg_sq"] = eng.vmax[so:so + p.numel()].view(p.shape)
+
+    def _hparams_of(self, gi: int) -> dict:
+        return adam_group_hparams(self._groups[gi], self.optimizer)
+
+    def _update_step_state(self):
+        eng = self.engine
+        for i in eng.owned_param_indices():
+            s = int(eng.steps[i])
+            if s == 0:
+                continue
+            t = self._step_tensors.get(s)
+            if t is None:
+                self._step_tensors.clear()
+                t = self._step_tensors[s] = torch.tensor(float(s), dtype=torch.float32)
+            st = self.optimizer.state[self.params[i]]
+            if st.get("step") is not t:
+                st["step"] = t
+
+    # ------------------------------------------------------------------------------------------
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        step_start = time.perf_counter()
+        if self.engine is None:
+            self._build_engine()
+        had_vmax = self.engine.vmax is not None
+        grads = [p.grad for p in self.params]
+        for g, p in zip(grads, self.params):
+            if g is not None and (g.dtype != p.dtype or g.shape != p.shape or not g.is_contiguous()):
+                raise ValueError("zero_amd: grads must be contiguous and match their param's "
+                                 "dtype and shape")
+        with torch.no_grad():
+            self.engine.step(grads, self._hparams_of)
+        if not had_vmax and self.engine.vmax is not None:
+            self._expose_state()
+        self._update_step_state()
+        self._release_grads()
+        if self._sync:
+            torch.cuda.synchronize(self.engine.device)
+            self.communication_time += self.engine.comm_time_s()
+        self.step_time += time.perf_counter() - step_start
+        return loss
+
+    def _release_grads(self):
+        # zero2.py:113 frees non-owned grads; the reduced grads live in the bucket arena, so
+        # every grad is released (the next backward allocates fresh ones).
+        for p in self.params:
+            p.grad = None
+
+    def zero_grad(self, set_to_none: bool = True):
+        for p in self.params:
+            if p.grad is not None:
+                if set_to_none:
+                    p.grad = None
+                else:
+                    p.grad.zero_()
+
+    # convenience --------------------------------------------------------------------------------
+    @property
+    def param_groups(self):
+        return self.optimizer.param_groups
+
+    def state_dict(self):
+        return self.optimizer.state_dict()
+
+    def __repr__(self):
+        return (f"{type(self).__name__}(zero={self._variant}, ws={self.world_size}, rank={self.rank}, "
+                f"owned={self.local_param_indices[:1]}..{self.local_param_indices[-1:]})")
+
+
+def is_initialized() -> bool:
+    return dist.is_available() and dist.is_initialized()

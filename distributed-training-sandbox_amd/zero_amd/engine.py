@@ -1,0 +1,280 @@
+"""The bucketed ZeRO step: pack → reduce-scatter → fused Adam → all-gather → unpack.
+
+One ``ShardEngine`` per ``ShardedOptimizer``.  It owns, for this rank's optimizer shard (the
+*stream* the planner assigns it), flat fp32 buffers for exp_avg / exp_avg_sq (+ max_exp_avg_sq,
+the fp32 master of bf16 params, and the ZeRO-1 gradient carry), and one persistent *arena* of
+bucket buffers in the parameter dtype.  A bucket buffer is ws windows of W elements, rank-major,
+so a single in-place RCCL reduce-scatter hands every rank the summed gradient of its own window
+and a single in-place all-gather hands every rank all updated windows.
+
+Per step and bucket k (reference loop it replaces in brackets):
+  compute stream: pack(k)  — gfx950 gather of every param's grad slice into bucket k
+                              [zero2.py:99-104 flatten + cat×ws; zero1.py has no copy]
+  comm stream:    RS(k)     — RCCL reduce-scatter, in place    [zero1.py:81-84 / zero2.py:107]
+  compute stream: adam(k)  — fused Adam on this rank's window, grad /ws folded in, writes the
+                              updated param into its bucket slot [zero1.py:88 / zero2.py:111,120]
+  comm stream:    AG(k)     — RCCL all-gather, in place          [zero1.py:95-102 / zero2.py:126-133]
+  compute stream: unpack(k) — gfx950 scatter of bucket k back into module storage
+Streams are ordered by events only; adam(k) overlaps RS(k+1), unpack(k) overlaps AG(k+1).
+With ws == 1 there is nothing to exchange and the step is one fused-Adam launch that reads
+every grad and writes every param in place.
+
+Segment tables are uploaded once and reused while the tensors' addresses stay the same.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from .comm import zs_dtype
+from .kernels import AdamSet, CopySet, adam_hparams
+from .plan import Plan
+
+ALIGN_ELEMS = 64  # every stream piece starts 256 B (f32) / 128 B (bf16) aligned
+
+
+def _ptr(t: torch.Tensor | None) -> int:
+    return 0 if t is None else int(t.data_ptr())
+
+
+class ShardEngine:
+    def __init__(self, params, group_of, ws: int, rank: int, *, layout="reference", carry=False,
+                 comm=None, bucket_bytes: int = 256 << 20, align: int = ALIGN_ELEMS):
+        if not params:
+            raise ValueError("ShardEngine: no parameters")
+        dev = params[0].device
+        if dev.type != "cuda":
+            raise RuntimeError(f"zero_amd: parameters must live on a GPU (got {dev}); "
+                               "there is no CPU path")
+        dtype = params[0].dtype
+        for p in params:
+            if p.device != dev or p.dtype != dtype:
+                raise TypeError("zero_amd: all parameters must share one device and dtype")
+            if not p.is_contiguous():
+                raise ValueError("zero_amd: parameters must be contiguous")
+        self.zdtype = zs_dtype(dtype)
+        self.params = list(params)
+        self.group_of = list(group_of)
+        self.ws, self.rank = ws, rank
+        self.device, self.dtype = dev, dtype
+        self.es = params[0].element_size()
+        self.mixed = dtype == torch.bfloat16  # bf16 params → fp32 master in the shard
+        self.has_carry = bool(carry)
+        self.comm = comm
+        if ws > 1 and comm is None:
+            raise ValueError("ShardEngine: ws > 1 needs a communicator")
+
+        numels = [p.numel() for p in params]
+        dim0 = [p.shape[0] if p.dim() > 0 else 1 for p in params]
+        window = 0 if ws == 1 else max(align, int(bucket_bytes) // (ws * self.es))
+        self.plan = Plan(numels, ws, rank, layout, dim0=dim0, align_elems=align, window_elems=window)
+        self.W, self.K = self.plan.window, self.plan.num_buckets
+        self.L = self.plan.stream_len(rank)
+        self.pieces = self.plan.pieces(rank)
+
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.m = torch.zeros(self.L, **f32)
+        self.v = torch.zeros(self.L, **f32)
+        self.vmax = None
+        self.carry = torch.zeros(self.L, **f32) if carry else None
+        self.master = None
+        if self.mixed:
+            self.master = torch.zeros(self.L, **f32)
+            for i, po, so, n in zip(*self._piece_cols()):
+                self.master[so:so + n].copy_(params[i].detach().reshape(-1)[po:po + n])
+        self.arena = None
+        if ws > 1:
+            self.arena = torch.zeros(self.K * self.plan.bucket_elems, dtype=dtype, device=dev)
+            self.segs = [self.plan.segments(k) for k in range(self.K)]
+            self.comm_stream = torch.cuda.Stream(device=dev)
+            mk = lambda: [torch.cuda.Event() for _ in range(self.K)]  # noqa: E731
+            self.ev_pack, self.ev_rs, self.ev_adam, self.ev_ag = mk(), mk(), mk(), mk()
+        self.ev_c0 = torch.cuda.Event(enable_timing=True)
+        self.ev_c1 = torch.cuda.Event(enable_timing=True)
+        self.steps = np.zeros(len(params), np.int64)  # torch's per-param state['step']
+        self._cache = {}
+        self.timing_events = None  # optional list of (start, end) events around each Adam launch
+        self.last_adam_bytes = 0
+
+    # ------------------------------------------------------------------------------------------
+    def _piece_cols(self):
+        pc = self.pieces
+        return pc.param.tolist(), pc.param_off.tolist(), pc.stream_off.tolist(), pc.length.tolist()
+
+    def owned_param_indices(self):
+        return sorted(set(int(i) for i, n in zip(self.pieces.param, self.pieces.length) if n > 0))
+
+    def state_views(self, i: int):
+        """exp_avg / exp_avg_sq views of param i's shard (Layout R: the whole param)."""
+        sel = np.nonzero(self.pieces.param == i)[0]
+        if len(sel) != 1:
+            return None
+        j = int(sel[0])
+        so, n = int(self.pieces.stream_off[j]), int(self.pieces.length[j])
+        po = int(self.pieces.param_off[j])
+        p = self.params[i]
+        shape = p.shape if (po == 0 and n == p.numel()) else (n,)
+        views = {"exp_avg": self.m[so:so + n].view(shape), "exp_avg_sq": self.v[so:so + n].view(shape)}
+        if self.master is not None:
+            views["master_param"] = self.master[so:so + n].view(shape)
+        return views
+
+    def ensure_vmax(self):
+        if self.vmax is None:
+            self.vmax = torch.zeros(self.L, dtype=torch.float32, device=self.device)
+        return self.vmax
+
+    def _cached(self, key, sig: bytes, build):
+        hit = self._cache.get(key)
+        if hit is not None and hit[0] == sig:
+            return hit[1]
+        obj = build()
+        self._cache[key] = (sig, obj)
+        return obj
+
+    # ------------------------------------------------------------------------------------------
+    def _adam_rows(self, idx, g_ptr, mst, mst_out, p_out, so, n):
+        """Vectorised zs_adam_seg rows (numpy uint64 (n, 9))."""
+        rows = np.zeros((len(idx), 9), np.uint64)
+        so = so.astype(np.uint64)
+        rows[:, 0] = g_ptr
+        rows[:, 1] = mst
+        rows[:, 2] = mst_out
+        rows[:, 3] = p_out
+        rows[:, 4] = np.uint64(self.m.data_ptr()) + so * np.uint64(4)
+        rows[:, 5] = np.uint64(self.v.data_ptr()) + so * np.uint64(4)
+        if self.vmax is not None:
+            rows[:, 6] = np.uint64(self.vmax.data_ptr()) + so * np.uint64(4)
+        if self.carry is not None:
+            rows[:, 7] = np.uint64(self.carry.data_ptr()) + so * np.uint64(4)
+        rows[:, 8] = n.astype(np.uint64)
+        return rows
+
+    def _run_adam(self, tag, rows, param_idx, hparams_of, stream):
+        """Partition rows by (group, step) — torch's bias correction is per param — and launch."""
+        if len(rows) == 0:
+            return
+        keys = np.stack([np.asarray(self.group_of)[param_idx], self.steps[param_idx]], axis=1)
+        for key in np.unique(keys, axis=0):
+            sel = np.nonzero((keys == key).all(axis=1))[0]
+            sub = np.ascontiguousarray(rows[sel])
+            gidx, step = int(key[0]), int(key[1])
+            aset = self._cached(("adam", tag, gidx, len(sel), int(sel[0])), sub.tobytes(),
+                                lambda: AdamSet(sub, self.zdtype))
+            hpd = hparams_of(gidx)
+            if hpd["amsgrad"] and self.vmax is None:
+                raise RuntimeError("amsgrad state buffer missing")
+            hp = adam_hparams(hpd["lr"], hpd["beta1"], hpd["beta2"], hpd["eps"],
+                              hpd["weight_decay"], step, decoupled=hpd["decoupled"],
+                              amsgrad=hpd["amsgrad"], maximize=hpd["maximize"],
+                              grad_div=float(self.ws),
+                              carry_mul=float(self.ws - 1) if self.carry is not None else 0.0)
+            if self.timing_events is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                aset.run(hp, stream)
+                e1.record(stream)
+                self.timing_events.append((e0, e1, aset.bytes))
+            else:
+                aset.run(hp, stream)
+            self.last_adam_bytes += aset.bytes
+
+    # ------------------------------------------------------------------------------------------
+    def step(self, grads, hparams_of, stream=None):
+        """One optimizer step.  ``grads[i]`` is param i's local gradient (or None);
+        ``hparams_of(group_index)`` returns that group's Adam hyper-parameters."""
+        stream = torch.cuda.current_stream(self.device) if stream is None else stream
+        n = len(self.params)
+        has = np.fromiter((g is not None for g in grads), bool, n)
+        gptr = np.fromiter((_ptr(g) for g in grads), np.uint64, n)
+        if any(hparams_of(g)["amsgrad"] for g in set(self.group_of)):
+            self.ensure_vmax()
+        owned = np.zeros(n, bool)
+        owned[self.owned_param_indices()] = True
+        self.steps[owned & has] += 1
+        self.last_adam_bytes = 0
+        if self.ws == 1:
+            self._step_local(gptr, has, hparams_of, stream)
+        else:
+            self._step_buckets(gptr, has, hparams_of, stream)
+
+    def _step_local(self, gptr, has, hparams_of, stream):
+        pc = self.pieces
+        sel = np.nonzero(has[pc.param] & (pc.length > 0))[0]
+        idx, po, so, n = pc.param[sel], pc.param_off[sel], pc.stream_off[sel], pc.length[sel]
+        pptr = np.fromiter((_ptr(self.params[i]) for i in idx), np.uint64, len(idx))
+        es = np.uint64(self.es)
+        g = gptr[idx] + po.astype(np.uint64) * es
+        if self.mixed:
+            mst = np.uint64(self.master.data_ptr()) + so.astype(np.uint64) * np.uint64(4)
+            rows = self._adam_rows(idx, g, mst, mst, pptr + po.astype(np.uint64) * es, so, n)
+        else:
+            p = pptr + po.astype(np.uint64) * np.uint64(4)
+            rows = self._adam_rows(idx, g, p, p, 0, so, n)
+        self._run_adam("local", rows, idx, hparams_of, stream)
+
+    def _step_buckets(self, gptr, has, hparams_of, stream):
+        es = np.uint64(self.es)
+        pptr = np.fromiter((_ptr(p) for p in self.params), np.uint64, len(self.params))
+        base = np.uint64(self.arena.data_ptr())
+        BE, W, r = self.plan.bucket_elems, self.W, self.rank
+        cs = self.comm_stream
+        self.ev_c0.record(cs)
+        for k in range(self.K):  # pack every bucket on the compute stream
+            s = self.segs[k]
+            src = np.where(has[s.param], gptr[s.param] + s.param_off.astype(np.uint64) * es, 0)
+            dst = base + np.uint64(k * BE) * es + s.buf_off.astype(np.uint64) * es
+            nb = s.length * self.es
+            sig = src.tobytes() + dst.tobytes()
+            self._cached(("pack", k), sig, lambda: CopySet(src, dst, nb)).run(stream)
+            self.ev_pack[k].record(stream)
+        for k in range(self.K):  # in-place reduce-scatter of each bucket
+            cs.wait_event(self.ev_pack[k])
+            buf = self.arena[k * BE:(k + 1) * BE]
+            self.comm.reduce_scatter(buf, buf[r * W:(r + 1) * W], cs)
+            self.ev_rs[k].record(cs)
+        for k in range(self.K):  # fused Adam on this rank's window
+            stream.wait_event(self.ev_rs[k])
+            s = self.segs[k]
+            own = np.nonzero(s.rank == r)[0]
+            idx = s.param[own]
+            slot = base + np.uint64(k * BE) * es + s.buf_off[own].astype(np.uint64) * es
+            so = (s.buf_off[own] - r * W) + k * W
+            ln = s.length[own]
+            po = s.param_off[own].astype(np.uint64)
+            live = has[idx]
+            if self.mixed:
+                mst = np.uint64(self.master.data_ptr()) + so.astype(np.uint64) * np.uint64(4)
+                rows = self._adam_rows(idx, slot, mst, mst, slot, so, ln)
+            else:
+                p = pptr[idx] + po * np.uint64(4)
+                rows = self._adam_rows(idx, slot, p, slot, 0, so, ln)
+            self._run_adam(("bucket", k), rows[live], idx[live], hparams_of, stream)
+            if not live.all():  # params without a grad keep their value: copy it into the slot
+                dead = np.nonzero(~live)[0]
+                src = pptr[idx[dead]] + po[dead] * es
+                nb = ln[dead] * self.es
+                self._cached(("pass", k), src.tobytes() + slot[dead].tobytes(),
+                             lambda: CopySet(src, slot[dead], nb)).run(stream)
+            self.ev_adam[k].record(stream)
+        for k in range(self.K):  # in-place all-gather of the updated windows
+            cs.wait_event(self.ev_adam[k])
+            buf = self.arena[k * BE:(k + 1) * BE]
+            self.comm.all_gather(buf[r * W:(r + 1) * W], buf, cs)
+            self.ev_ag[k].record(cs)
+        self.ev_c1.record(cs)
+        for k in range(self.K):  # scatter every bucket back into module storage
+            stream.wait_event(self.ev_ag[k])
+            s = self.segs[k]
+            src = base + np.uint64(k * BE) * es + s.buf_off.astype(np.uint64) * es
+            dst = pptr[s.param] + s.param_off.astype(np.uint64) * es
+            self._cached(("unpack", k), dst.tobytes(),
+                         lambda: CopySet(src, dst, s.length * self.es)).run(stream)
+
+    def comm_time_s(self) -> float:
+        """Seconds between the first reduce-scatter and the last all-gather of the last step
+        (valid after a synchronize)."""
+        if self.ws == 1:
+            return 0.0
+        return self.ev_c0.elapsed_time(self.ev_c1) / 1e3

@@ -1,0 +1,91 @@
+"""Python handles for the gfx950 kernels behind the C ABI (csrc/zs_kernels.hip).
+
+``CopySet``  — one launch of the descriptor-driven gather/scatter copy (pack / unpack).
+``AdamSet``  — one launch of the fused Adam/AdamW update over a list of segments.
+
+Both upload their segment table once; ``run(stream)`` only enqueues a kernel on ``stream``.
+They raise ``ZeroAmdError`` on any failure; there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import AdamHParams, AdamSeg
+
+_PU64 = ctypes.POINTER(ctypes.c_uint64)
+_PI64 = ctypes.POINTER(ctypes.c_int64)
+
+
+def stream_handle(stream) -> int:
+    """uintptr_t for a torch.cuda.Stream (or an int handle)."""
+    return int(stream) if isinstance(stream, int) else int(stream.cuda_stream)
+
+
+class CopySet:
+    """Copy ``nbytes[i]`` bytes from ``src[i]`` to ``dst[i]`` (src 0 = zero fill)."""
+
+    def __init__(self, src, dst, nbytes):
+        src = np.ascontiguousarray(np.asarray(src, dtype=np.uint64))
+        dst = np.ascontiguousarray(np.asarray(dst, dtype=np.uint64))
+        nb = np.ascontiguousarray(np.asarray(nbytes, dtype=np.int64))
+        assert src.shape == dst.shape == nb.shape
+        self.nbytes = int(nb.sum()) if nb.size else 0
+        self.nseg = int(nb.size)
+        h = ctypes.c_void_p()
+        _lib.call("zs_copyset_create", src.ctypes.data_as(_PU64), dst.ctypes.data_as(_PU64),
+                  nb.ctypes.data_as(_PI64), int(nb.size), ctypes.byref(h))
+        self._h = h
+
+    def run(self, stream) -> None:
+        _lib.call("zs_copyset_run", self._h, stream_handle(stream))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib is not None:
+            try:
+                _lib.lib.zs_copyset_destroy(h)
+            except Exception:  # interpreter teardown
+                pass
+            self._h = None
+
+
+def adam_hparams(lr, beta1, beta2, eps, weight_decay, step, *, decoupled=False, amsgrad=False,
+                 maximize=False, grad_div=1.0, carry_mul=0.0) -> AdamHParams:
+    hp = AdamHParams()
+    _lib.call("zs_adam_hparams_init", float(lr), float(beta1), float(beta2), float(eps),
+              float(weight_decay), int(bool(decoupled)), int(bool(amsgrad)), int(bool(maximize)),
+              int(step), float(grad_div), float(carry_mul), ctypes.byref(hp))
+    return hp
+
+
+class AdamSet:
+    """Fused Adam over segments; ``segs`` is an (n, 9) int64/uint64 array in zs_adam_seg order:
+    g, master, master_out, p_out, m, v, vmax, carry, n."""
+
+    FIELDS = ("g", "master", "master_out", "p_out", "m", "v", "vmax", "carry", "n")
+
+    def __init__(self, segs: np.ndarray, g_dtype: int, p_dtype: int = _lib.ZS_BF16):
+        segs = np.ascontiguousarray(np.asarray(segs, dtype=np.uint64).reshape(-1, 9))
+        arr = (AdamSeg * max(len(segs), 1))()
+        ctypes.memmove(arr, segs.ctypes.data, segs.nbytes)
+        h = ctypes.c_void_p()
+        _lib.call("zs_adamset_create", arr, len(segs), int(g_dtype), int(p_dtype), ctypes.byref(h))
+        self._h = h
+        e, b = ctypes.c_int64(), ctypes.c_int64()
+        _lib.call("zs_adamset_stats", self._h, ctypes.byref(e), ctypes.byref(b))
+        self.elems, self.bytes = e.value, b.value
+
+    def run(self, hp: AdamHParams, stream) -> None:
+        _lib.call("zs_adamset_run", self._h, ctypes.byref(hp), stream_handle(stream))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib is not None:
+            try:
+                _lib.lib.zs_adamset_destroy(h)
+            except Exception:  # interpreter teardown
+                pass
+            self._h = None

@@ -1,0 +1,177 @@
+/*
+ * zero_amd.h — C ABI of the MI355X-native ZeRO sharded-optimizer step.
+ *
+ * The reference (xo-toybox/distributed-training-sandbox, zero/zero{1,2,3}.py) has no native code:
+ * its hot path is Python calling c10d collectives and torch.optim.Adam.  This library is what the
+ * drop-in ShardedOptimizer (distributed-training-sandbox_amd/zero_amd/zero{1,2,3}.py) binds with
+ * ctypes.  Every entry point below names the reference interface it replaces.
+ *
+ * Conventions
+ *  - plain C types only: no torch types cross this boundary; device buffers are raw pointers
+ *    (uint64_t / void*) owned by the caller (torch tensors); the library never frees caller memory.
+ *  - every launch takes a hipStream_t passed as uintptr_t (torch.cuda.Stream.cuda_stream);
+ *    nothing synchronises the host except *_create (table upload) and zs_comm_init.
+ *  - every function returns int status: ZS_OK (0) or a ZS_ERR_* code; zs_last_error() returns a
+ *    thread-local message for the most recent failure on the calling thread.
+ *  - element counts are int64_t elements; byte counts say "bytes".
+ */
+#ifndef ZERO_AMD_H
+#define ZERO_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZS_ABI_VERSION 1
+
+enum zs_status {
+  ZS_OK = 0,
+  ZS_ERR_INVALID = 1,   /* bad argument / shape mismatch */
+  ZS_ERR_HIP = 2,       /* hipError_t from the runtime */
+  ZS_ERR_RCCL = 3,      /* ncclResult_t from RCCL */
+  ZS_ERR_NOMEM = 4
+};
+
+enum zs_dtype { ZS_F32 = 0, ZS_BF16 = 1 };
+
+/* Shard layouts (SURVEY.md §7 "Two shard layouts"). */
+enum zs_layout {
+  ZS_LAYOUT_R = 0,  /* reference owner-by-parameter-index (zero1.py:55-62, zero2.py:51-58) */
+  ZS_LAYOUT_Z = 1,  /* dim-0 chunk of every parameter, torch.chunk semantics (zero3.py:105-110) */
+  ZS_LAYOUT_F = 2   /* flat: one balanced contiguous 1/ws slice of the concatenated params */
+};
+
+int zs_abi_version(void);
+const char* zs_last_error(void);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Layout planner (host only; callable without a GPU).                                         */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct zs_plan zs_plan;
+
+/* Replaces ShardedOptimizer.__init__'s ownership computation (zero1.py:44-62, zero2.py:39-58,
+ * zero3.py:82-110).  numels[i] = params[i].numel(); dim0[i] = params[i].shape[0] (1 for 0-d;
+ * only read for ZS_LAYOUT_Z, may be NULL otherwise).  align_elems: every piece starts at a
+ * multiple of this in its rank's stream (>=1).  window_elems: per-rank elements per bucket
+ * (0 = one bucket holding the whole longest stream). */
+int zs_plan_create(int64_t n_params, const int64_t* numels, const int64_t* dim0, int ws, int rank,
+                   int layout, int64_t align_elems, int64_t window_elems, zs_plan** out);
+int zs_plan_destroy(zs_plan* plan);
+
+/* info[0..6] = {n_params, ws, rank, layout, window_elems W, num_buckets K, max_stream_len M} */
+int zs_plan_info(const zs_plan* plan, int64_t* info7);
+
+/* Parameter-index ownership [start,end) of `rank` (zero1.py:55-62).  Same formula for every
+ * layout: it is what the reference uses to filter the inner optimizer's param_groups. */
+int zs_plan_owner_range(const zs_plan* plan, int rank, int64_t* start, int64_t* end);
+
+/* Broadcast-source rank of parameter i (zero1.py:95-100, zero2.py:126-131). */
+int zs_plan_owner_of(const zs_plan* plan, int64_t i, int* owner);
+
+/* Length (elements, padded to align) of rank r's stream = its optimizer shard. */
+int zs_plan_stream_len(const zs_plan* plan, int rank, int64_t* len);
+
+/* Pieces of rank r's stream: param index, element offset inside the (flattened) param,
+ * element offset inside the stream, length.  Arrays sized by zs_plan_num_pieces. */
+int zs_plan_num_pieces(const zs_plan* plan, int rank, int64_t* n);
+int zs_plan_pieces(const zs_plan* plan, int rank, int64_t* param, int64_t* param_off,
+                   int64_t* stream_off, int64_t* len);
+
+/* Segments of bucket k (all ranks): bucket buffer = ws windows of W elements, rank-major.
+ * buf_off is the element offset inside the bucket buffer (rank*W + offset in window). */
+int zs_plan_num_segments(const zs_plan* plan, int64_t bucket, int64_t* n);
+int zs_plan_segments(const zs_plan* plan, int64_t bucket, int64_t* param, int64_t* rank,
+                     int64_t* param_off, int64_t* buf_off, int64_t* len);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Segment copy (pack / unpack).  Replaces the flatten + torch.cat([g]*ws) copies of            */
+/* zero2.py:99-104, the chunk().contiguous() copies of zero3.py:44-51,107-108,142-143 and the   */
+/* torch.cat of gathered shards (zero3.py:40).                                                  */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct zs_copyset zs_copyset;
+
+/* src[i]==0 means "write nbytes[i] zero bytes to dst[i]".  The table is uploaded once. */
+int zs_copyset_create(const uint64_t* src, const uint64_t* dst, const int64_t* nbytes, int64_t n,
+                      zs_copyset** out);
+int zs_copyset_run(const zs_copyset* cs, uintptr_t stream);
+int zs_copyset_destroy(zs_copyset* cs);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Fused Adam / AdamW.  Replaces torch.optim.Adam.step on the owned shard (zero1.py:88,          */
+/* zero2.py:120, zero3.py:161; math of torch/optim/adam.py:457-547) plus the grad averaging     */
+/* (zero1.py:84 `p.grad /= ws`, zero2.py:111 `output / ws`, zero3.py:147).                      */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+  uint64_t g;          /* gradient (reduced SUM over ranks), dtype g_dtype; 0 = zero gradient */
+  uint64_t master;     /* fp32 master / param read by the update */
+  uint64_t master_out; /* fp32 destination of the updated master (may equal master, may be a
+                          bucket slot; 0 = not written) */
+  uint64_t p_out;      /* optional copy of the updated param in p_dtype (bf16); 0 = none */
+  uint64_t m;          /* fp32 exp_avg, updated in place */
+  uint64_t v;          /* fp32 exp_avg_sq, updated in place */
+  uint64_t vmax;       /* fp32 max_exp_avg_sq (amsgrad) or 0 */
+  uint64_t carry;      /* fp32 ZeRO-1 carried average A_{t-1}, rewritten with A_t; or 0 */
+  int64_t n;           /* elements */
+} zs_adam_seg;
+
+typedef struct {
+  /* scalars exactly as torch computes them (double on host, rounded to f32 once) */
+  float one_minus_beta1;  /* lerp weight 1-beta1 */
+  float beta2;
+  float one_minus_beta2;
+  float neg_step_size;    /* -(lr / (1 - beta1^t)) */
+  float bc2_sqrt;         /* sqrt(1 - beta2^t) */
+  float eps;
+  float weight_decay;     /* L2 (Adam) coefficient; 0 = off */
+  float decay_mul;        /* AdamW: 1 - lr*wd; 1 = off */
+  float grad_div;         /* divide the reduced sum by this (world size) */
+  float carry_mul;        /* ZeRO-1: sum += carry_mul * carry (ws-1) */
+  int32_t amsgrad;
+  int32_t maximize;
+} zs_adam_hparams;
+
+/* Fill hp the way torch.optim.Adam/AdamW (non-capturable path) derives its scalars at step t. */
+int zs_adam_hparams_init(double lr, double beta1, double beta2, double eps, double weight_decay,
+                         int decoupled, int amsgrad, int maximize, int64_t step, double grad_div,
+                         double carry_mul, zs_adam_hparams* hp);
+
+typedef struct zs_adamset zs_adamset;
+/* g_dtype: dtype of every seg's g; p_dtype: dtype of every non-null p_out (ZS_BF16). All
+ * fp32 pointers of a seg must be 16-byte aligned and bf16 pointers 8-byte aligned for the
+ * vector path; other segments take a scalar path. */
+int zs_adamset_create(const zs_adam_seg* segs, int64_t n, int g_dtype, int p_dtype,
+                      zs_adamset** out);
+int zs_adamset_run(const zs_adamset* as, const zs_adam_hparams* hp, uintptr_t stream);
+int zs_adamset_destroy(zs_adamset* as);
+/* total elements covered by the set and algorithmic HBM bytes one run moves */
+int zs_adamset_stats(const zs_adamset* as, int64_t* elems, int64_t* bytes);
+
+/* ------------------------------------------------------------------------------------------ */
+/* RCCL over xGMI.  Replaces the per-tensor dist.all_reduce (zero1.py:83, zero3.py:146),        */
+/* dist.reduce_scatter_tensor (zero2.py:107), dist.broadcast (zero1.py:102, zero2.py:133) and   */
+/* dist.all_gather (zero3.py:39) with bucketed collectives on a caller stream.                  */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct zs_comm zs_comm;
+#define ZS_UNIQUE_ID_BYTES 128
+int zs_comm_unique_id(void* out128);
+int zs_comm_init(const void* unique_id128, int ws, int rank, zs_comm** out);
+int zs_comm_destroy(zs_comm* comm);
+/* recv_count / send_count are elements per rank (NCCL convention). In-place is allowed:
+ * recv == send + rank*recv_count (reduce-scatter), send == recv + rank*send_count (all-gather). */
+int zs_reduce_scatter(zs_comm* comm, const void* send, void* recv, int64_t recv_count, int dtype,
+                      uintptr_t stream);
+int zs_all_gather(zs_comm* comm, const void* send, void* recv, int64_t send_count, int dtype,
+                  uintptr_t stream);
+int zs_all_reduce(zs_comm* comm, const void* send, void* recv, int64_t count, int dtype,
+                  uintptr_t stream);
+int zs_group_start(void);
+int zs_group_end(void);
+/* RCCL version the library is bound to at run time (e.g. 22606). */
+int zs_rccl_version(int* version);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZERO_AMD_H */

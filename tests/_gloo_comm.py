@@ -1,0 +1,48 @@
+"""TEST-ONLY communicator: GPU buffers staged through host memory and the gloo process group.
+
+RCCL refuses two ranks of one communicator on the same GPU ("Using the same HIP device for multiple
+ranks of the same Communicator is not supported", rccl.h:174-176), and the GPU box has one GPU.  To
+exercise the engine's multi-rank orchestration (Layout R buckets, in-place reduce-scatter /
+all-gather slices, ZeRO-1 carry, per-rank Adam windows) with the real HIP pack / Adam / unpack
+kernels, ws processes share cuda:0 and exchange through this class.  Sums are done in fp32.
+"""
+import torch
+import torch.distributed as dist
+
+
+class GlooStagedComm:
+    def __init__(self, group=None):
+        self.group = group
+        self.ws = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.calls = []
+
+    def reduce_scatter(self, send, recv, stream):
+        stream.synchronize()
+        h = send.detach().to("cpu", torch.float32)
+        out = torch.empty(recv.numel(), dtype=torch.float32)
+        dist.reduce_scatter_tensor(out, h, group=self.group)
+        with torch.cuda.stream(stream):
+            recv.copy_(out.to(recv.device).to(recv.dtype))
+        self.calls.append(("rs", send.numel()))
+
+    def all_gather(self, send, recv, stream):
+        stream.synchronize()
+        h = send.detach().to("cpu")
+        if h.dtype == torch.bfloat16:
+            h = h.view(torch.int16)
+        out = torch.empty(recv.numel(), dtype=h.dtype)
+        dist.all_gather_into_tensor(out, h, group=self.group)
+        if recv.dtype == torch.bfloat16:
+            out = out.view(torch.bfloat16)
+        with torch.cuda.stream(stream):
+            recv.copy_(out.to(recv.device))
+        self.calls.append(("ag", recv.numel()))
+
+    def all_reduce(self, t, stream):
+        stream.synchronize()
+        h = t.detach().to("cpu", torch.float32)
+        dist.all_reduce(h, group=self.group)
+        with torch.cuda.stream(stream):
+            t.copy_(h.to(t.device).to(t.dtype))
+        self.calls.append(("ar", t.numel()))

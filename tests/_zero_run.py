@@ -1,0 +1,68 @@
+"""Drive the zero_amd ShardedOptimizer with a golden trajectory's exact step inputs.
+
+Shared by the single-process GPU parity tests and the spawned multi-rank ones.  The reference's
+local gradients per rank and step (tests/golden/traj_*.npz, ``r{rank}_t{t}_lg{i}``) are written into
+``p.grad`` and ``step()`` runs; the returned params are compared with the reference's own.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+def init_pg(rank: int, ws: int, port: int):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+
+
+def module_for(variant: int):
+    if variant == 1:
+        from zero_amd import zero1 as mod
+    elif variant == 2:
+        from zero_amd import zero2 as mod
+    else:
+        from zero_amd import zero3 as mod
+    return mod
+
+
+def run_injected(z, variant: int, rank: int, ws: int, device, comm=None, window_elems=64, tol=1e-6):
+    """Replay the fixture's grads through ShardedOptimizer; assert params match every step."""
+    mod = module_for(variant)
+    steps = int(z["steps"])
+    params = [torch.nn.Parameter(torch.from_numpy(z[f"init_{i}"].copy()).to(device)) for i in range(12)]
+    kw = dict(bucket_mb=ws * window_elems * 4 / (1 << 20))
+    if comm is not None:
+        kw["comm"] = comm
+    opt = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), **kw)
+    worst = 0.0
+    for t in range(steps):
+        opt.zero_grad()
+        for i, p in enumerate(params):
+            p.grad = torch.from_numpy(z[f"r{rank}_t{t}_lg{i}"].copy()).to(device)
+        opt.step()
+        key0 = f"r{rank}_t{t}_p0"
+        if key0 in z.files:
+            for i, p in enumerate(params):
+                e = rel(p.detach().cpu().numpy(), z[f"r{rank}_t{t}_p{i}"])
+                worst = max(worst, e)
+                assert e <= tol, (variant, ws, rank, t, i, e)
+    # Adam state exposed through optimizer.state (memory.py:15-24 reads it)
+    for i, p in enumerate(params):
+        key = f"r{rank}_state_{i}_exp_avg"
+        if key in z.files:
+            st = opt.optimizer.state[p]
+            assert int(st["step"].item()) == int(z[f"r{rank}_state_{i}_step"])
+            assert rel(st["exp_avg"].cpu().numpy(), z[key]) <= tol
+            assert rel(st["exp_avg_sq"].cpu().numpy(), z[f"r{rank}_state_{i}_exp_avg_sq"]) <= tol
+    assert opt.local_param_indices == z[f"r{rank}_local"].tolist()
+    return worst

@@ -1,0 +1,69 @@
+"""The C-ABI library loads and exports exactly what include/zero_amd.h declares (no GPU needed)."""
+import ctypes
+import math
+import re
+
+import pytest
+
+from conftest import REPO
+
+
+def _declared():
+    text = (REPO / "include" / "zero_amd.h").read_text()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(zs_\w+)\s*\(", text, re.M)))
+
+
+def test_header_and_library_agree():
+    from zero_amd import _lib
+
+    declared = _declared()
+    assert declared, "no declarations parsed"
+    assert sorted(_lib.EXPORTED) == declared
+    raw = ctypes.CDLL(str(_lib.LIB_PATH))
+    for name in declared:
+        assert hasattr(raw, name), name
+
+
+def test_library_is_gfx950_code_object():
+    from zero_amd import _lib
+
+    data = _lib.LIB_PATH.read_bytes()
+    assert b"gfx950" in data
+    assert b"adam_segments_kernel" in data and b"copy_segments_kernel" in data
+
+
+def test_abi_version_and_error_text():
+    from zero_amd import _lib
+
+    assert _lib.lib.zs_abi_version() == 1
+    h = ctypes.c_void_p()
+    rc = _lib.lib.zs_plan_create(0, None, None, 0, 0, 0, 64, 0, ctypes.byref(h))
+    assert rc == _lib.ZS_ERR_INVALID
+    assert b"ws must be >= 1" in _lib.lib.zs_last_error()
+
+
+def test_hparams_match_torch_scalars():
+    """zs_adam_hparams_init derives the scalars as adam.py:508-537 does (python doubles)."""
+    import numpy as np
+    from zero_amd.kernels import adam_hparams
+
+    for step in (1, 2, 10, 1000):
+        lr, b1, b2, eps = 1e-3, 0.9, 0.999, 1e-8
+        hp = adam_hparams(lr, b1, b2, eps, 0.0, step, grad_div=4.0, carry_mul=3.0)
+        assert hp.neg_step_size == np.float32(-(lr / (1 - b1 ** step)))
+        assert hp.bc2_sqrt == np.float32((1 - b2 ** step) ** 0.5)
+        assert hp.one_minus_beta1 == np.float32(1 - b1)
+        assert hp.one_minus_beta2 == np.float32(1 - b2)
+        assert hp.grad_div == 4.0 and hp.carry_mul == 3.0 and hp.decay_mul == 1.0
+    hp = adam_hparams(1e-3, 0.9, 0.999, 1e-8, 1e-2, 1, decoupled=True)
+    assert hp.weight_decay == 0.0 and hp.decay_mul == np.float32(1 - 1e-3 * 1e-2)
+    hp = adam_hparams(1e-3, 0.9, 0.999, 1e-8, 1e-2, 1)
+    assert math.isclose(hp.weight_decay, 1e-2, rel_tol=1e-7) and hp.decay_mul == 1.0
+
+
+def test_invalid_step_rejected():
+    from zero_amd._lib import ZeroAmdError
+    from zero_amd.kernels import adam_hparams
+
+    with pytest.raises(ZeroAmdError):
+        adam_hparams(1e-3, 0.9, 0.999, 1e-8, 0.0, 0)

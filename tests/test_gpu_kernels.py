@@ -1,0 +1,196 @@
+"""gfx950 kernels through the C ABI: segment copy (bit-exact) and fused Adam (vs the C oracle
+bit-exact, vs torch.optim.Adam's known answers within 1e-6)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import c_oracle
+from oracle import zero_oracle as zo
+
+pytestmark = pytest.mark.gpu
+
+
+def _seed(n):
+    return np.random.default_rng(n)
+
+
+def test_copy_segments_bit_exact(gpu):
+    from zero_amd.kernels import CopySet
+
+    rng = _seed(1)
+    src = torch.randint(0, 256, (1 << 20,), dtype=torch.uint8, device=gpu)
+    dst = torch.zeros(1 << 21, dtype=torch.uint8, device=gpu)
+    want = torch.zeros_like(dst).cpu()
+    s_cpu = src.cpu()
+    srcs, dsts, nbs = [], [], []
+    doff = 0
+    lens = [0, 1, 2, 15, 16, 17, 31, 64, 1000, 16384, 16385, 100_000, 65536 * 3 + 7]
+    for k, ln in enumerate(lens * 2):
+        align = k % 2 == 0
+        so = int(rng.integers(0, 1000)) * (16 if align else 1)
+        doff = (doff + 15) // 16 * 16 if align else doff + 3
+        zero = (k % 7) == 3
+        srcs.append(0 if zero else src.data_ptr() + so)
+        dsts.append(dst.data_ptr() + doff)
+        nbs.append(ln)
+        want[doff:doff + ln] = 0 if zero else s_cpu[so:so + ln]
+        doff += ln
+    dst.fill_(0)
+    CopySet(srcs, dsts, nbs).run(torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dst.cpu(), want)
+
+
+def test_copy_zero_fill_overwrites(gpu):
+    from zero_amd.kernels import CopySet
+
+    dst = torch.full((4096,), 7, dtype=torch.float32, device=gpu)
+    CopySet([0], [dst.data_ptr() + 64], [1024]).run(torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    h = dst.cpu()
+    assert (h[16:16 + 256] == 0).all() and (h[:16] == 7).all() and (h[272:] == 7).all()
+
+
+def _adam_rows(g, master, master_out, p_out, m, v, vmax=None, carry=None, n=None):
+    ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+    n = master.numel() if n is None else n
+    return np.array([[ptr(g), ptr(master), ptr(master_out), ptr(p_out), ptr(m), ptr(v),
+                      ptr(vmax), ptr(carry), n]], dtype=np.uint64)
+
+
+CASES = {
+    "default": dict(),
+    "wd": dict(weight_decay=1e-2),
+    "amsgrad": dict(amsgrad=True),
+    "maximize": dict(maximize=True),
+    "adamw": dict(weight_decay=1e-2, decoupled=True),
+    "hyper": dict(lr=1e-2, beta1=0.8, beta2=0.99, eps=1e-6),
+}
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_adam_fp32_vs_torch_kat_and_oracle(gpu, golden, case):
+    from zero_amd._lib import ZS_F32
+    from zero_amd.kernels import AdamSet, adam_hparams
+
+    z = golden("adam_kat.npz")
+    cfg = dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0)
+    cfg.update(CASES[case])
+    flags = {k: cfg.pop(k) for k in ("decoupled", "amsgrad", "maximize") if k in cfg}
+    p0 = z[f"{case}_p0"]
+    p = torch.from_numpy(p0.copy()).to(gpu)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    vmax = torch.zeros_like(p) if flags.get("amsgrad") else None
+    g = torch.empty_like(p)
+    aset = AdamSet(_adam_rows(g, p, p, None, m, v, vmax), ZS_F32)
+    # C oracle in lock-step
+    cp, cm, cv, cx = p0.copy(), np.zeros_like(p0), np.zeros_like(p0), np.zeros_like(p0)
+    for t, gt in enumerate(z[f"{case}_grads"]):
+        g.copy_(torch.from_numpy(gt))
+        aset.run(adam_hparams(cfg["lr"], cfg["beta1"], cfg["beta2"], cfg["eps"], cfg["weight_decay"],
+                              t + 1, **flags), torch.cuda.current_stream())
+        c_oracle.adam_f32(cp, np.ascontiguousarray(gt), cm, cv,
+                          c_oracle.hparams(step=t + 1, **cfg, **flags),
+                          vmax=cx if flags.get("amsgrad") else None)
+    torch.cuda.synchronize()
+    hp_, hm, hv = p.cpu().numpy(), m.cpu().numpy(), v.cpu().numpy()
+    # bit-exact against the C restatement (same rounding order, IEEE sqrt/div on both sides)
+    assert np.array_equal(hp_.view(np.uint32), cp.view(np.uint32))
+    assert np.array_equal(hm.view(np.uint32), cm.view(np.uint32))
+    assert np.array_equal(hv.view(np.uint32), cv.view(np.uint32))
+    # within 1e-6 of torch.optim.Adam itself (north-star tolerance)
+    for a, key in ((hp_, "p"), (hm, "m"), (hv, "v")):
+        ref = z[f"{case}_{key}"]
+        assert np.max(np.abs(a - ref)) / np.max(np.abs(ref)) <= 1e-6
+
+
+@pytest.mark.parametrize("ws,carry", [(1, False), (3, False), (4, False), (3, True), (8, True)])
+def test_adam_bf16_master_and_carry_vs_oracle(gpu, ws, carry):
+    """bf16 grads + fp32 master/m/v + bf16 param out; grad/ws and the ZeRO-1 carry folded in."""
+    from zero_amd._lib import ZS_BF16
+    from zero_amd.kernels import AdamSet, adam_hparams
+
+    rng = _seed(ws)
+    n = 100_003
+    master0 = (rng.standard_normal(n) * 0.02).astype(np.float32)
+    master = torch.from_numpy(master0.copy()).to(gpu)
+    pbf = torch.zeros(n, dtype=torch.bfloat16, device=gpu)
+    m, v = torch.zeros_like(master), torch.zeros_like(master)
+    cr = torch.zeros_like(master) if carry else None
+    g = torch.zeros(n, dtype=torch.bfloat16, device=gpu)
+    aset = AdamSet(_adam_rows(g, master, master, pbf, m, v, carry=cr), ZS_BF16)
+    cm_, cp_, cmm, cvv = master0.copy(), np.zeros(n, np.uint16), np.zeros(n, np.float32), np.zeros(n, np.float32)
+    ccr = np.zeros(n, np.float32) if carry else None
+    for t in range(1, 6):
+        gt = torch.from_numpy((rng.standard_normal(n) * 1e-2).astype(np.float32)).to(torch.bfloat16)
+        g.copy_(gt)
+        kw = dict(grad_div=float(ws), carry_mul=float(ws - 1) if carry else 0.0)
+        aset.run(adam_hparams(1e-3, 0.9, 0.999, 1e-8, 0.0, t, **kw), torch.cuda.current_stream())
+        c_oracle.adam_bf16(cm_, cp_, gt.view(torch.int16).numpy().view(np.uint16).copy(), cmm, cvv,
+                           c_oracle.hparams(step=t, **kw), carry=ccr)
+    torch.cuda.synchronize()
+    assert np.array_equal(master.cpu().numpy().view(np.uint32), cm_.view(np.uint32))
+    assert np.array_equal(pbf.cpu().view(torch.int16).numpy().view(np.uint16), cp_)
+    assert np.array_equal(pbf.cpu().view(torch.int16).numpy().view(np.uint16),
+                          zo.f32_to_bf16_bits(cm_))
+    if carry:
+        assert np.array_equal(cr.cpu().numpy().view(np.uint32), ccr.view(np.uint32))
+
+
+def test_adam_many_segments_unaligned_and_tails(gpu):
+    """Segment table with tails, unaligned (scalar-path) segments, null grads and 1-elem segs."""
+    from zero_amd._lib import ZS_F32
+    from zero_amd.kernels import AdamSet, adam_hparams
+
+    rng = _seed(7)
+    N = 300_000
+    P = torch.from_numpy(rng.standard_normal(N).astype(np.float32)).to(gpu)
+    G = torch.from_numpy(rng.standard_normal(N).astype(np.float32) * 1e-3).to(gpu)
+    M, V = torch.zeros_like(P), torch.zeros_like(P)
+    rows, off = [], 0
+    for k, ln in enumerate([1, 3, 4, 5, 2047, 2048, 2049, 4096 + 13, 70_001, 1, 999]):
+        off += k % 3  # k%3 != 0 → unaligned (scalar path)
+        gp = 0 if k == 4 else G.data_ptr() + 4 * off
+        r = [gp] + [P.data_ptr() + 4 * off] * 2 + [0, M.data_ptr() + 4 * off, V.data_ptr() + 4 * off,
+                                                   0, 0, ln]
+        rows.append(r)
+        off += ln
+    rows = np.array(rows, dtype=np.uint64)
+    p_ref, g_ref = P.cpu().numpy().copy(), G.cpu().numpy().copy()
+    m_ref, v_ref = np.zeros(N, np.float32), np.zeros(N, np.float32)
+    AdamSet(rows, ZS_F32).run(adam_hparams(1e-3, 0.9, 0.999, 1e-8, 0.0, 1), torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    for r in rows:
+        o = (int(r[1]) - P.data_ptr()) // 4
+        ln = int(r[8])
+        gg = np.zeros(ln, np.float32) if int(r[0]) == 0 else g_ref[o:o + ln].copy()
+        pp, mm, vv = p_ref[o:o + ln].copy(), m_ref[o:o + ln].copy(), v_ref[o:o + ln].copy()
+        c_oracle.adam_f32(pp, gg, mm, vv, c_oracle.hparams(step=1))
+        p_ref[o:o + ln], m_ref[o:o + ln], v_ref[o:o + ln] = pp, mm, vv
+    assert np.array_equal(P.cpu().numpy().view(np.uint32), p_ref.view(np.uint32))
+    assert np.array_equal(M.cpu().numpy().view(np.uint32), m_ref.view(np.uint32))
+
+
+def test_pack_unpack_round_trip_c2(gpu):
+    """Size-independent property at C2 scale (100.7M fp32 params): pack every Layout-R bucket at
+    ws=4, unpack into fresh tensors, get the params back bit-for-bit."""
+    from zero_amd.kernels import CopySet
+    from zero_amd.plan import Plan
+    from zero_amd.shapes import mlp_shapes
+
+    shapes = mlp_shapes(4096)
+    ps = [torch.randn(s, device=gpu) for s in shapes]
+    outs = [torch.empty_like(p) for p in ps]
+    plan = Plan([p.numel() for p in ps], 4, 0, "reference", window_elems=4 << 20)
+    buf = torch.zeros(plan.bucket_elems, device=gpu)
+    st = torch.cuda.current_stream()
+    for k in range(plan.num_buckets):
+        s = plan.segments(k)
+        src = [ps[i].data_ptr() + 4 * po for i, po in zip(s.param, s.param_off)]
+        dst = [buf.data_ptr() + 4 * bo for bo in s.buf_off]
+        CopySet(src, dst, s.length * 4).run(st)
+        CopySet(dst, [outs[i].data_ptr() + 4 * po for i, po in zip(s.param, s.param_off)],
+                s.length * 4).run(st)
+    torch.cuda.synchronize()
+    for p, o in zip(ps, outs):
+        assert torch.equal(p, o)

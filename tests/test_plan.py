@@ -1,0 +1,147 @@
+"""Layout planner (zs_plan_*, host-only C++) against the reference's ownership fixtures and the
+structural invariants every pack / reduce-scatter / all-gather / unpack relies on."""
+import numpy as np
+import pytest
+
+from zero_amd.plan import Plan
+from oracle import zero_oracle as zo
+
+
+def test_ownership_matches_reference(golden):
+    """zero1.py:55-62 ranges and zero1.py:95-100 owners, bit-exact, n<=400, ws<=64."""
+    z = golden("ownership.npz")
+    for n in z["ns"]:
+        for ws in z["wss"]:
+            n, ws = int(n), int(ws)
+            start, end, owner = z[f"n{n}_ws{ws}_start"], z[f"n{n}_ws{ws}_end"], z[f"n{n}_ws{ws}_owner"]
+            plan = Plan(np.ones(n, np.int64), ws, 0)
+            for r in range(ws):
+                s, e = plan.owner_range(r)
+                if end[r] > start[r]:
+                    assert (s, e) == (start[r], end[r]), (n, ws, r)
+                else:
+                    assert s == e, (n, ws, r)
+            got = [plan.owner_of(i) for i in range(n)]
+            assert got == owner.tolist(), (n, ws)
+
+
+def test_oracle_ownership_matches_reference(golden):
+    z = golden("ownership.npz")
+    for n in (1, 2, 7, 12, 13, 64, 291, 326, 400):
+        for ws in z["wss"]:
+            ws = int(ws)
+            own = z[f"n{n}_ws{ws}_owner"]
+            assert [zo.owner_of(n, ws, i) for i in range(n)] == own.tolist()
+            for r in range(ws):
+                s, e = zo.owner_range(n, ws, r)
+                if z[f"n{n}_ws{ws}_end"][r] > z[f"n{n}_ws{ws}_start"][r]:
+                    assert (s, e) == (z[f"n{n}_ws{ws}_start"][r], z[f"n{n}_ws{ws}_end"][r])
+
+
+def _coverage(plan, numels):
+    """Every element of every param appears in exactly one rank's pieces and exactly once in the
+    buckets; bucket offsets are in range and disjoint; piece starts are aligned."""
+    ws = plan.ws
+    cover = [np.zeros(n, np.int32) for n in numels]
+    for r in range(ws):
+        pc = plan.pieces(r)
+        L = plan.stream_len(r)
+        used = np.zeros(L, np.int8)
+        for i, po, so, ln in zip(pc.param, pc.param_off, pc.stream_off, pc.length):
+            assert so % 64 == 0
+            assert so + ln <= L
+            cover[i][po:po + ln] += 1
+            assert used[so:so + ln].sum() == 0
+            used[so:so + ln] = 1
+    for c in cover:
+        assert (c == 1).all()
+    seen = [np.zeros(n, np.int32) for n in numels]
+    for k in range(plan.num_buckets):
+        s = plan.segments(k)
+        used = np.zeros(plan.bucket_elems, np.int8)
+        for i, r, po, bo, ln in zip(s.param, s.rank, s.param_off, s.buf_off, s.length):
+            assert r * plan.window <= bo and bo + ln <= (r + 1) * plan.window
+            assert used[bo:bo + ln].sum() == 0
+            used[bo:bo + ln] = 1
+            seen[i][po:po + ln] += 1
+    for c in seen:
+        assert (c == 1).all()
+
+
+@pytest.mark.parametrize("layout", ["reference", "chunk", "flat"])
+@pytest.mark.parametrize("ws", [1, 2, 3, 4, 8])
+def test_layout_invariants(layout, ws):
+    rng = np.random.default_rng(ws)
+    shapes = [(int(rng.integers(1, 40)), int(rng.integers(1, 9))) for _ in range(23)]
+    shapes += [(16, 16), (16,), (1,), (0,), (5, 3)]
+    numels = [int(np.prod(s)) for s in shapes]
+    dim0 = [s[0] for s in shapes]
+    for window in (0, 64, 128, 1000):
+        plan = Plan(numels, ws, 0, layout, dim0=dim0, window_elems=window)
+        _coverage(plan, numels)
+        if window:
+            assert plan.window % 64 == 0
+
+
+@pytest.mark.parametrize("ws", [1, 2, 3, 4, 8])
+def test_chunk_layout_matches_torch_chunk(ws):
+    """Layout Z pieces are torch.chunk(ws, dim=0)[rank] (zero3.py:107-108), incl. uneven d0."""
+    import torch
+
+    shapes = [(16, 4), (10000 // 625, 3), (7, 2), (3,), (2, 5), (1, 1)]
+    numels = [int(np.prod(s)) for s in shapes]
+    plan = Plan(numels, ws, 0, "chunk", dim0=[s[0] for s in shapes])
+    for r in range(ws):
+        pc = plan.pieces(r)
+        for i, s in enumerate(shapes):
+            t = torch.arange(numels[i]).reshape(s)
+            chunks = t.chunk(ws, dim=0)
+            j = np.nonzero(pc.param == i)[0]
+            assert len(j) == 1
+            po, ln = int(pc.param_off[j[0]]), int(pc.length[j[0]])
+            want = chunks[r].reshape(-1) if r < len(chunks) else torch.zeros(0, dtype=t.dtype)
+            assert torch.equal(t.reshape(-1)[po:po + ln], want)
+
+
+def test_flat_layout_balanced():
+    numels = [4096 * 4096, 4096] * 6
+    for ws in (2, 4, 8):
+        plan = Plan(numels, ws, 0, "flat")
+        lens = [plan.stream_len(r) for r in range(ws)]
+        assert len(set(lens)) == 1
+        assert lens[0] * ws - sum(numels) < 64 * ws + 64 * len(numels)
+
+
+def test_reference_layout_padding_smollm3():
+    """Layout R pads to the largest owner (SmolLM3-3B at ws=8 ≈ 1.52×)."""
+    from zero_amd.shapes import smollm3_3b_shapes
+
+    numels = [int(np.prod(s)) for s in smollm3_3b_shapes()]
+    assert sum(numels) == 3_075_098_624 and len(numels) == 326
+    plan = Plan(numels, 8, 0, "reference")
+    ratio = plan.max_stream_len * 8 / sum(numels)
+    assert 1.4 < ratio < 1.6
+
+
+def test_invalid_arguments_raise():
+    from zero_amd._lib import ZeroAmdError
+
+    with pytest.raises(ZeroAmdError):
+        Plan([4, 4], 0, 0)
+    with pytest.raises(ZeroAmdError):
+        Plan([4, 4], 2, 2)
+    with pytest.raises(ZeroAmdError):
+        Plan([6, 4], 2, 0, "chunk", dim0=[4, 4])  # 6 % 4 != 0
+    plan = Plan([4, 4], 2, 0)
+    with pytest.raises(ZeroAmdError):
+        plan.segments(5)
+    with pytest.raises(ZeroAmdError):
+        plan.owner_of(2)
+
+
+def test_empty_and_tiny():
+    plan = Plan([], 4, 1)
+    assert plan.num_buckets == 0 and plan.stream_len() == 0
+    plan = Plan([3], 4, 3)  # ws > n: ranks 1..3 own nothing
+    assert plan.owner_range(3) == (1, 1) and plan.stream_len(3) == 0
+    assert plan.owner_of(0) == 0
