@@ -11,6 +11,7 @@ of one communicator on the same device).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 
 import torch
@@ -63,6 +64,15 @@ class RcclComm:
             self.close()
         except Exception:  # interpreter teardown
             pass
+
+    @contextlib.contextmanager
+    def group(self):
+        """RCCL group: the collectives issued inside launch together at exit."""
+        _lib.call("zs_group_start")
+        try:
+            yield
+        finally:
+            _lib.call("zs_group_end")
 
     def reduce_scatter(self, send: torch.Tensor, recv: torch.Tensor, stream) -> None:
         """SUM-reduce ``send`` (ws*count elements) and leave chunk ``rank`` in ``recv``."""
