@@ -34,7 +34,7 @@ int grid_cap() {
       if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
         cus = prop.multiProcessorCount;
     }
-    cap = cus * 8;
+    cap = cus * 32;  // ~4x the resident workgroups: measured best for these streaming kernels
   }
   return cap;
 }
@@ -110,7 +110,6 @@ struct AdamSeg {
   float* vmax;
   float* carry;
   int64_t n;
-  int64_t vec;
 };
 
 struct HP {
@@ -164,10 +163,17 @@ __device__ __forceinline__ float load_g1(const void* g, int64_t i) {
   else return bf16_to_f32(glob(static_cast<const unsigned short*>(g))[i]);
 }
 
+// Scalar kernel: any alignment, any length (segment tails and unaligned segments; tiny).
 template <typename GT, bool AMS, bool CARRY>
-__device__ __attribute__((noinline)) void adam_scalar_range(const AdamSeg& s, int64_t i0, int64_t i1,
-                                                            int64_t stride, const HP& hp) {
-  for (int64_t i = i0; i < i1; i += stride) {
+__global__ __launch_bounds__(kThreads) void adam_scalar_kernel(
+    const AdamSeg* __restrict__ segs, const int64_t* __restrict__ chunk_prefix, int64_t nseg,
+    int64_t total_chunks, HP hp) {
+  int64_t seg = 0;
+  for (int64_t c = blockIdx.x; c < total_chunks; c += gridDim.x) {
+    while (chunk_prefix[seg + 1] <= c) ++seg;
+    const AdamSeg s = segs[seg];
+    const int64_t i = (c - chunk_prefix[seg]) * kThreads + threadIdx.x;
+    if (i >= s.n) continue;
     float gs = s.g ? load_g1<GT>(s.g, i) : 0.0f;
     float p = glob(s.master)[i], m = glob(s.m)[i], v = glob(s.v)[i];
     float vm = AMS ? glob(s.vmax)[i] : 0.0f;
@@ -201,6 +207,10 @@ __device__ __forceinline__ void st4(float* p, int64_t i, float4 x) {
   *reinterpret_cast<gptr<float4>>(glob(p) + i) = x;
 }
 
+// Vector kernel: every segment 16-B aligned (8-B for bf16 arrays) with n % 4 == 0 (the host
+// splits tails off into the scalar table).  kAdamGroups float4 groups per thread, lane-contiguous
+// (16 B per lane per access), so each wave instruction touches one contiguous 1 KiB (f32) /
+// 512 B (bf16) run; every group's loads are issued before any math.
 template <typename GT, bool AMS, bool CARRY>
 __global__ __launch_bounds__(kThreads) void adam_segments_kernel(
     const AdamSeg* __restrict__ segs, const int64_t* __restrict__ chunk_prefix, int64_t nseg,
@@ -210,19 +220,12 @@ __global__ __launch_bounds__(kThreads) void adam_segments_kernel(
     while (chunk_prefix[seg + 1] <= c) ++seg;
     const AdamSeg s = segs[seg];
     const int64_t e0 = (c - chunk_prefix[seg]) * kAdamChunk;
-    const int64_t e1 = min(e0 + kAdamChunk, s.n);
-    if (!s.vec) {
-      adam_scalar_range<GT, AMS, CARRY>(s, e0 + threadIdx.x, e1, kThreads, hp);
-      continue;
-    }
-    // Vector path: kAdamGroups float4 groups per thread, lane-contiguous (16 B per lane per
-    // access) so every wave instruction touches one contiguous 1 KiB (f32) / 512 B (bf16) run.
     float4 g4[kAdamGroups], p4[kAdamGroups], m4[kAdamGroups], v4[kAdamGroups];
     float4 x4[kAdamGroups], c4[kAdamGroups];
 #pragma unroll
     for (int u = 0; u < kAdamGroups; ++u) {
       const int64_t i = e0 + (int64_t(u) * kThreads + threadIdx.x) * 4;
-      if (i + 4 <= e1) {
+      if (i < s.n) {
         g4[u] = s.g ? load_g4<GT>(s.g, i) : make_float4(0.f, 0.f, 0.f, 0.f);
         p4[u] = ld4(s.master, i);
         m4[u] = ld4(s.m, i);
@@ -234,7 +237,7 @@ __global__ __launch_bounds__(kThreads) void adam_segments_kernel(
 #pragma unroll
     for (int u = 0; u < kAdamGroups; ++u) {
       const int64_t i = e0 + (int64_t(u) * kThreads + threadIdx.x) * 4;
-      if (i + 4 <= e1) {
+      if (i < s.n) {
         float* gp = reinterpret_cast<float*>(&g4[u]);
         float* pp = reinterpret_cast<float*>(&p4[u]);
         float* mp = reinterpret_cast<float*>(&m4[u]);
@@ -260,8 +263,6 @@ __global__ __launch_bounds__(kThreads) void adam_segments_kernel(
         st4(s.v, i, v4[u]);
         if constexpr (AMS) st4(s.vmax, i, x4[u]);
         if constexpr (CARRY) st4(s.carry, i, c4[u]);
-      } else if (i < e1) {
-        adam_scalar_range<GT, AMS, CARRY>(s, i, e1, 1, hp);
       }
     }
   }
@@ -278,9 +279,12 @@ struct zs_copyset {
 };
 
 struct zs_adamset {
-  AdamSeg* d_segs = nullptr;
-  int64_t* d_prefix = nullptr;
-  int64_t nseg = 0, total_chunks = 0, elems = 0, bytes = 0;
+  // vector table (aligned, n % 4 == 0) and scalar table (tails, unaligned segments)
+  AdamSeg* d_vec = nullptr;
+  int64_t* d_vec_prefix = nullptr;
+  AdamSeg* d_sca = nullptr;
+  int64_t* d_sca_prefix = nullptr;
+  int64_t nvec = 0, vec_chunks = 0, nsca = 0, sca_chunks = 0, elems = 0, bytes = 0;
   int g_dtype = ZS_F32, p_dtype = ZS_BF16, has_carry = 0, has_vmax = 0;
 };
 
@@ -385,12 +389,11 @@ int zs_adamset_create(const zs_adam_seg* in, int64_t n, int g_dtype, int p_dtype
   ZS_REQUIRE(n >= 0 && (n == 0 || in), "zs_adamset_create: bad table");
   ZS_REQUIRE(g_dtype == ZS_F32 || g_dtype == ZS_BF16, "zs_adamset_create: bad g_dtype %d", g_dtype);
   ZS_REQUIRE(p_dtype == ZS_BF16, "zs_adamset_create: p_out must be bf16 (got %d)", p_dtype);
-  const uint64_t ga = g_dtype == ZS_F32 ? 16 : 8;
-  std::vector<AdamSeg> segs;
-  std::vector<int64_t> prefix(1, 0);
+  const int64_t gsz = g_dtype == ZS_F32 ? 4 : 2;
+  std::vector<AdamSeg> vec, sca;
+  std::vector<int64_t> vpre(1, 0), spre(1, 0);
   int carry_state = -1, vmax_state = -1;
   int64_t elems = 0, bytes = 0;
-  const int64_t gsz = g_dtype == ZS_F32 ? 4 : 2;
   for (int64_t i = 0; i < n; ++i) {
     const zs_adam_seg& s = in[i];
     ZS_REQUIRE(s.n >= 0, "zs_adamset_create: seg %lld n < 0", (long long)i);
@@ -414,14 +417,33 @@ int zs_adamset_create(const zs_adam_seg* in, int64_t n, int g_dtype, int p_dtype
     d.v = reinterpret_cast<float*>(s.v);
     d.vmax = reinterpret_cast<float*>(s.vmax);
     d.carry = reinterpret_cast<float*>(s.carry);
-    d.n = s.n;
-    d.vec = aligned(s.g, ga) && aligned(s.master, 16) && aligned(s.master_out, 16) &&
-                    aligned(s.p_out, 8) && aligned(s.m, 16) && aligned(s.v, 16) &&
-                    aligned(s.vmax, 16) && aligned(s.carry, 16)
-                ? 1
-                : 0;
-    segs.push_back(d);
-    prefix.push_back(prefix.back() + (s.n + kAdamChunk - 1) / kAdamChunk);
+    const bool ok = aligned(s.g, uint64_t(gsz) * 4) && aligned(s.master, 16) &&
+                    aligned(s.master_out, 16) && aligned(s.p_out, 8) && aligned(s.m, 16) &&
+                    aligned(s.v, 16) && aligned(s.vmax, 16) && aligned(s.carry, 16);
+    const int64_t nv = ok ? (s.n & ~int64_t(3)) : 0;
+    if (nv) {
+      d.n = nv;
+      vec.push_back(d);
+      vpre.push_back(vpre.back() + (nv + kAdamChunk - 1) / kAdamChunk);
+    }
+    if (nv < s.n) {  // tail (or the whole unaligned segment) through the scalar kernel
+      AdamSeg t = d;
+      auto adv = [nv](auto* p, int64_t es) {
+        using P = decltype(p);
+        return p ? reinterpret_cast<P>(reinterpret_cast<uintptr_t>(p) + uintptr_t(nv * es)) : p;
+      };
+      t.g = s.g ? reinterpret_cast<const void*>(s.g + uint64_t(nv * gsz)) : nullptr;
+      t.master = adv(d.master, 4);
+      t.master_out = adv(d.master_out, 4);
+      t.p_out = adv(d.p_out, 2);
+      t.m = adv(d.m, 4);
+      t.v = adv(d.v, 4);
+      t.vmax = adv(d.vmax, 4);
+      t.carry = adv(d.carry, 4);
+      t.n = s.n - nv;
+      sca.push_back(t);
+      spre.push_back(spre.back() + (t.n + kThreads - 1) / kThreads);
+    }
     elems += s.n;
     int64_t b = (s.g ? gsz : 0) + 4 /*master*/ + 8 /*m*/ + 8 /*v*/;
     if (s.master_out) b += 4;
@@ -432,16 +454,25 @@ int zs_adamset_create(const zs_adam_seg* in, int64_t n, int g_dtype, int p_dtype
   }
   zs_adamset* as = new (std::nothrow) zs_adamset();
   if (!as) return zs::fail(ZS_ERR_NOMEM, "zs_adamset_create: out of memory");
-  as->nseg = int64_t(segs.size());
-  as->total_chunks = prefix.back();
+  as->nvec = int64_t(vec.size());
+  as->vec_chunks = vpre.back();
+  as->nsca = int64_t(sca.size());
+  as->sca_chunks = spre.back();
   as->elems = elems;
   as->bytes = bytes;
   as->g_dtype = g_dtype;
   as->p_dtype = p_dtype;
   as->has_carry = carry_state > 0 ? 1 : 0;
   as->has_vmax = vmax_state > 0 ? 1 : 0;
-  int rc = upload(segs, &as->d_segs);
-  if (rc == ZS_OK) rc = upload(prefix, &as->d_prefix);
+  int rc = ZS_OK;
+  if (as->nvec) {
+    rc = upload(vec, &as->d_vec);
+    if (rc == ZS_OK) rc = upload(vpre, &as->d_vec_prefix);
+  }
+  if (rc == ZS_OK && as->nsca) {
+    rc = upload(sca, &as->d_sca);
+    if (rc == ZS_OK) rc = upload(spre, &as->d_sca_prefix);
+  }
   if (rc != ZS_OK) {
     zs_adamset_destroy(as);
     return rc;
@@ -452,7 +483,6 @@ int zs_adamset_create(const zs_adam_seg* in, int64_t n, int g_dtype, int p_dtype
 
 int zs_adamset_run(const zs_adamset* as, const zs_adam_hparams* h, uintptr_t stream) {
   ZS_REQUIRE(as && h, "zs_adamset_run: NULL argument");
-  if (as->total_chunks == 0) return ZS_OK;
   HP hp;
   hp.omb1 = h->one_minus_beta1;
   hp.beta2 = h->beta2;
@@ -469,32 +499,45 @@ int zs_adamset_run(const zs_adamset* as, const zs_adam_hparams* h, uintptr_t str
   hp.inv_div = float(1.0 / double(h->grad_div));
   hp.maximize = h->maximize;
   const bool ams = h->amsgrad != 0, carry = as->has_carry != 0;
-  ZS_REQUIRE(!ams || as->has_vmax || as->nseg == 0, "zs_adamset_run: amsgrad needs vmax segments");
-  const int grid = int(std::min<int64_t>(as->total_chunks, grid_cap()));
+  ZS_REQUIRE(!ams || as->has_vmax || (as->nvec + as->nsca) == 0,
+             "zs_adamset_run: amsgrad needs vmax segments");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-#define ZS_LAUNCH_ADAM(GT, A, C)                                                          \
-  hipLaunchKernelGGL((adam_segments_kernel<GT, A, C>), dim3(grid), dim3(kThreads), 0, st, \
-                     as->d_segs, as->d_prefix, as->nseg, as->total_chunks, hp)
-  if (as->g_dtype == ZS_F32) {
-    if (ams && carry) ZS_LAUNCH_ADAM(float, true, true);
-    else if (ams) ZS_LAUNCH_ADAM(float, true, false);
-    else if (carry) ZS_LAUNCH_ADAM(float, false, true);
-    else ZS_LAUNCH_ADAM(float, false, false);
-  } else {
-    if (ams && carry) ZS_LAUNCH_ADAM(unsigned short, true, true);
-    else if (ams) ZS_LAUNCH_ADAM(unsigned short, true, false);
-    else if (carry) ZS_LAUNCH_ADAM(unsigned short, false, true);
-    else ZS_LAUNCH_ADAM(unsigned short, false, false);
+#define ZS_LAUNCH(KERNEL, GT, A, C, TAB, PRE, NS, NCH)                                        \
+  hipLaunchKernelGGL((KERNEL<GT, A, C>), dim3(int(std::min<int64_t>(NCH, grid_cap()))),      \
+                     dim3(kThreads), 0, st, TAB, PRE, NS, NCH, hp)
+#define ZS_DISPATCH(KERNEL, TAB, PRE, NS, NCH)                                                \
+  do {                                                                                        \
+    if (as->g_dtype == ZS_F32) {                                                              \
+      if (ams && carry) ZS_LAUNCH(KERNEL, float, true, true, TAB, PRE, NS, NCH);              \
+      else if (ams) ZS_LAUNCH(KERNEL, float, true, false, TAB, PRE, NS, NCH);                 \
+      else if (carry) ZS_LAUNCH(KERNEL, float, false, true, TAB, PRE, NS, NCH);               \
+      else ZS_LAUNCH(KERNEL, float, false, false, TAB, PRE, NS, NCH);                         \
+    } else {                                                                                  \
+      if (ams && carry) ZS_LAUNCH(KERNEL, unsigned short, true, true, TAB, PRE, NS, NCH);     \
+      else if (ams) ZS_LAUNCH(KERNEL, unsigned short, true, false, TAB, PRE, NS, NCH);        \
+      else if (carry) ZS_LAUNCH(KERNEL, unsigned short, false, true, TAB, PRE, NS, NCH);      \
+      else ZS_LAUNCH(KERNEL, unsigned short, false, false, TAB, PRE, NS, NCH);                \
+    }                                                                                         \
+  } while (0)
+  if (as->vec_chunks) {
+    ZS_DISPATCH(adam_segments_kernel, as->d_vec, as->d_vec_prefix, as->nvec, as->vec_chunks);
+    ZS_HIP(hipGetLastError());
   }
-#undef ZS_LAUNCH_ADAM
-  ZS_HIP(hipGetLastError());
+  if (as->sca_chunks) {
+    ZS_DISPATCH(adam_scalar_kernel, as->d_sca, as->d_sca_prefix, as->nsca, as->sca_chunks);
+    ZS_HIP(hipGetLastError());
+  }
+#undef ZS_DISPATCH
+#undef ZS_LAUNCH
   return ZS_OK;
 }
 
 int zs_adamset_destroy(zs_adamset* as) {
   if (!as) return ZS_OK;
-  if (as->d_segs) (void)hipFree(as->d_segs);
-  if (as->d_prefix) (void)hipFree(as->d_prefix);
+  if (as->d_vec) (void)hipFree(as->d_vec);
+  if (as->d_vec_prefix) (void)hipFree(as->d_vec_prefix);
+  if (as->d_sca) (void)hipFree(as->d_sca);
+  if (as->d_sca_prefix) (void)hipFree(as->d_sca_prefix);
   delete as;
   return ZS_OK;
 }
