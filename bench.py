@@ -66,6 +66,22 @@ def cpu_baseline(shapes, sample_elems: int, min_seconds: float = 10.0):
                        f"bf16 params out) by oracle/adam_oracle.c, {el:.1f} s")
 
 
+class _NoComm:
+    """Timing-only stand-in for the collectives (--simulate-ws): leaves buffers untouched."""
+
+    def __init__(self, ws):
+        self.ws, self.rank = ws, 0
+
+    def reduce_scatter(self, send, recv, stream):
+        pass
+
+    def all_gather(self, send, recv, stream):
+        pass
+
+    def all_reduce(self, t, stream):
+        pass
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -78,7 +94,13 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=256 << 20)
-    ap.add_argument("--traffic-json", default=None,
+    ap.add_argument("--simulate-ws", type=int, default=0,
+                    help="DIAGNOSTIC (N=1 only): run the ws>1 bucket path of rank 0 of a ws-rank job "
+                         "with the collectives replaced by no-ops, to time pack / Adam / unpack "
+                         "at that layout; prints a diagnostic line, not the metric")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "gloo-staged"],
+                    help="gloo-staged = TEST ONLY (tests/_gloo_comm.py): N ranks sharing one GPU")
+    ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "r01_c4_n1_adam_pmc.json"),
                     help="PMC HBM-bytes summary (profiles/*.json) for the roofline 'traffic' field")
     args = ap.parse_args()
 
@@ -94,12 +116,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE")
+    if args.comm == "gloo-staged":  # test-only: every rank shares the box's GPUs round-robin
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29531")
-    dist.init_process_group("nccl" if world > 1 else "gloo", rank=rank, world_size=world,
-                            device_id=dev if world > 1 else None)
+    use_nccl = world > 1 and args.comm == "rccl"
+    dist.init_process_group("nccl" if use_nccl else "gloo", rank=rank, world_size=world,
+                            device_id=dev if use_nccl else None)
 
     name, shape_fn = CONFIGS[args.config]
     shapes = shape_fn()
@@ -117,8 +142,21 @@ def main():
         grads.append((torch.empty(s, dtype=torch.float32, device=dev).normal_(generator=gen) * 1e-3).to(dt))
     torch.cuda.synchronize()
     mod = zero1 if args.zero == 1 else zero2
+    kw = {}
+    if args.comm == "gloo-staged" and world > 1:
+        sys.path.insert(0, str(REPO / "tests"))
+        from _gloo_comm import GlooStagedComm
+
+        kw["comm"] = GlooStagedComm()
+    if args.simulate_ws > 1:
+        assert world == 1, "--simulate-ws is a single-GPU diagnostic"
+        kw["comm"] = _NoComm(args.simulate_ws)
+        import zero_amd._sharded as sh
+        sim_ws, real_get = args.simulate_ws, sh.get
+        sh.get = lambda what, dm=None: {"ws": sim_ws, "rank": 0}.get(what) if what in ("ws", "rank") \
+            else real_get(what, dm)
     opt = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), layout=args.layout,
-                               bucket_mb=args.bucket_mb, sync=False)
+                               bucket_mb=args.bucket_mb, sync=False, **kw)
 
     def step():
         for p, g in zip(params, grads):
@@ -139,7 +177,8 @@ def main():
     el = time.perf_counter() - t0
     eng_events = eng.timing_events
     eng.timing_events = None
-    el_t = torch.tensor([el], dtype=torch.float64, device=dev if world > 1 else "cpu")
+    red_dev = dev if use_nccl else "cpu"
+    el_t = torch.tensor([el], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     el = float(el_t.item())
@@ -151,7 +190,7 @@ def main():
     launches = len(eng_events)
     achieved = adam_bytes / (adam_ms / 1e3) / 1e9 if adam_ms > 0 else 0.0
     stats = torch.tensor([achieved, adam_ms / max(launches, 1), adam_bytes / max(launches, 1)],
-                         dtype=torch.float64, device=dev if world > 1 else "cpu")
+                         dtype=torch.float64, device=red_dev)
     if world > 1:  # report the slowest rank's Adam
         dist.all_reduce(stats, op=dist.ReduceOp.MIN)
     achieved = float(stats[0])
@@ -160,9 +199,20 @@ def main():
     tj = Path(args.traffic_json) if args.traffic_json else None
     if tj is not None and tj.exists():
         d = json.loads(tj.read_text())
-        traffic = d.get("hbm_bytes_per_launch")
-        traffic_src = str(tj.relative_to(REPO) if tj.is_absolute() else tj)
+        want = {"workload": args.config, "zero": args.zero, "param_dtype": args.dtype,
+                "layout": args.layout, "n_gpus": world}
+        if d.get("config") == want:  # PMC passes of this same configuration (profiles/README.md)
+            traffic = d.get("hbm_bytes_per_launch")
+            traffic_src = str(tj.relative_to(REPO) if tj.is_absolute() else tj)
 
+    if rank == 0 and args.simulate_ws > 1:
+        print(json.dumps({"diagnostic": f"simulate-ws {args.simulate_ws}: rank-0 compute of the "
+                          "bucket path, collectives skipped (NOT the metric)",
+                          "ms_per_step": ms, "adam_achieved_gbs": achieved,
+                          "adam_ms_per_step": adam_ms / args.steps, "buckets": eng.K,
+                          "window_elems": eng.W, "stream_elems": eng.L}), flush=True)
+        dist.destroy_process_group()
+        return
     if rank == 0:
         out = {
             "metric": METRIC,

@@ -1,0 +1,57 @@
+"""bench.py's contract on the GPU box: the JSON line (N=1), the N>1 harness (2 ranks sharing the
+one GPU through the test-only gloo-staged communicator) and the ws=8 bucket path at scale."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+        "scaling", "vs_baseline", "dtype", "data", "config", "roofline"}
+
+
+def _run(cmd, timeout=240):
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=timeout, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    return json.loads(lines[0])
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_bench_json_line_n1(gpu):
+    out = _run([sys.executable, "bench.py", "--config", "C2", "--dtype", "fp32", "--steps", "3",
+                "--warmup", "1", "--no-cpu-baseline"])
+    assert KEYS <= set(out) and out["n_gpus"] == 1 and out["value"] > 0
+    rf = out["roofline"]
+    assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1.2 and rf["achieved"] > 0
+
+
+def test_bench_harness_two_ranks_gloo_staged(gpu):
+    out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+                "--config", "C2", "--dtype", "fp32", "--steps", "2", "--warmup", "1",
+                "--comm", "gloo-staged", "--bucket-mb", "64"], timeout=600)
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["value"] > 0
+    assert out["config"]["buckets"] > 1 and out["roofline"]["launches_per_step"] >= 1
+
+
+def test_bench_simulated_ws8_bucket_path(gpu):
+    """The ws=8 Layout-R bucket path (pack / Adam / unpack over all buckets) at C4 scale."""
+    out = _run([sys.executable, "bench.py", "--config", "C4", "--steps", "3", "--warmup", "1",
+                "--simulate-ws", "8", "--no-cpu-baseline"])
+    assert "diagnostic" in out and out["buckets"] > 1 and out["ms_per_step"] > 0
