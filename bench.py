@@ -25,6 +25,8 @@ sys.path.insert(0, str(REPO / "distributed-training-sandbox_amd"))
 sys.path.insert(0, str(REPO))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured copy)
+XGMI_LINK_GBS = 153.0  # one xGMI link, per direction (task brief: 7 links x ~153 GB/s per GPU)
+XGMI_LINKS = 7
 METRIC = "ZeRO step time & params/sec at 1/2/4/8 GPU; Adam HBM GB/s vs peak"
 
 
@@ -66,6 +68,82 @@ def cpu_baseline(shapes, sample_elems: int, min_seconds: float = 10.0):
                        f"bf16 params out) by oracle/adam_oracle.c, {el:.1f} s")
 
 
+def _busbw(bus_bytes, ms):
+    return bus_bytes / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+
+
+def collective_summary(events, steps, world, red_dev):
+    """Per-step time and bus bandwidth of the step's collectives, from HIP events on the comm stream
+    (max over ranks).  Bus bytes: ring reduce-scatter / all-gather move (ws-1)/ws of the bucket per
+    rank; a reduce / broadcast (ragged buckets) moves its whole message."""
+    import torch
+    import torch.distributed as dist
+
+    acc = {}
+    for kind, even, e0, e1, bus in events:
+        key = ("reduce" if kind == "rs" else "gather") + ("_even" if even else "_ragged")
+        ms, b, n = acc.get(key, (0.0, 0.0, 0))
+        acc[key] = (ms + e0.elapsed_time(e1), b + bus, n + 1)
+    keys = ["reduce_even", "reduce_ragged", "gather_even", "gather_ragged"]
+    t = torch.tensor([acc.get(k, (0.0, 0.0, 0))[0] for k in keys], dtype=torch.float64, device=red_dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    out = {"source": "HIP events around each collective on the comm stream, max over ranks",
+           "link_peak_gbs": XGMI_LINK_GBS, "aggregate_peak_gbs": XGMI_LINK_GBS * XGMI_LINKS}
+    tot_ms = tot_bus = 0.0
+    for k, ms in zip(keys, t.tolist()):
+        if k not in acc:
+            continue
+        _, b, n = acc[k]
+        out[k] = {"calls_per_step": n / steps, "ms_per_step": ms / steps,
+                  "bus_gb_per_step": b / steps / 1e9, "busbw_gbs": _busbw(b, ms)}
+        tot_ms += ms
+        tot_bus += b
+    out["ms_per_step"] = tot_ms / steps
+    out["busbw_gbs"] = _busbw(tot_bus, tot_ms)
+    out["frac_of_aggregate"] = out["busbw_gbs"] / (XGMI_LINK_GBS * XGMI_LINKS)
+    return out
+
+
+def comm_sweep(comm, arena, world, red_dev, sizes_mb=(4, 16, 64, 256), iters=5):
+    """Bucket-size sweep of in-place RCCL reduce-scatter / all-gather on the bf16 arena (the C5
+    sweep of BASELINE.json, run on whatever N the bench runs): busBW = bytes*(ws-1)/ws / time."""
+    import torch
+    import torch.distributed as dist
+
+    st = torch.cuda.Stream(device=arena.device)
+    es = arena.element_size()
+    rows = []
+    for mb in sizes_mb:
+        n = (int(mb * (1 << 20)) // es) // world * world
+        if n == 0 or n > arena.numel():
+            continue
+        buf = arena[:n]
+        mine = buf[dist.get_rank() * (n // world):(dist.get_rank() + 1) * (n // world)]
+        res = []
+        for kind in ("rs", "ag"):
+            op = (lambda: comm.reduce_scatter(buf, mine, st)) if kind == "rs" else \
+                (lambda: comm.all_gather(mine, buf, st))
+            op()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            dist.barrier()
+            torch.cuda.synchronize()
+            e0.record(st)
+            for _ in range(iters):
+                op()
+            e1.record(st)
+            torch.cuda.synchronize()
+            res.append(e0.elapsed_time(e1) / iters)
+        t = torch.tensor(res, dtype=torch.float64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        bus = n * es * (world - 1) / world
+        rs_ms, ag_ms = t.tolist()
+        rows.append({"bucket_mb": mb, "rs_ms": rs_ms, "rs_busbw_gbs": _busbw(bus, rs_ms),
+                     "ag_ms": ag_ms, "ag_busbw_gbs": _busbw(bus, ag_ms)})
+    torch.cuda.synchronize()
+    arena.zero_()  # the sweep scribbled over the arena; padding must stay zero
+    return rows
+
+
 class _NoComm:
     """Timing-only stand-in for the collectives (--simulate-ws): leaves buffers untouched."""
 
@@ -76,6 +154,12 @@ class _NoComm:
         pass
 
     def all_gather(self, send, recv, stream):
+        pass
+
+    def reduce_v(self, buf, win_off, win_len, stream):
+        pass
+
+    def broadcast_v(self, buf, win_off, win_len, stream):
         pass
 
     def all_reduce(self, t, stream):
@@ -91,6 +175,11 @@ def main():
     ap.add_argument("--zero", type=int, default=2, choices=[1, 2])
     ap.add_argument("--layout", default="reference", choices=["reference", "flat"])
     ap.add_argument("--bucket-mb", type=float, default=256.0)
+    ap.add_argument("--buckets", default="ragged", choices=["ragged", "padded"],
+                    help="ragged: equal-count RS/AG over the shortest stream + one grouped "
+                         "reduce/broadcast per owner for the rest; padded: every window padded")
+    ap.add_argument("--no-comm-sweep", action="store_true",
+                    help="skip the RS/AG bus-bandwidth sweep (N>1, after the timed region)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=256 << 20)
@@ -156,7 +245,7 @@ def main():
         sh.get = lambda what, dm=None: {"ws": sim_ws, "rank": 0}.get(what) if what in ("ws", "rank") \
             else real_get(what, dm)
     opt = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), layout=args.layout,
-                               bucket_mb=args.bucket_mb, sync=False, **kw)
+                               bucket_mb=args.bucket_mb, sync=False, buckets=args.buckets, **kw)
 
     def step():
         for p, g in zip(params, grads):
@@ -167,6 +256,7 @@ def main():
         step()
     eng = opt.engine
     eng.timing_events = []
+    eng.comm_events = [] if world > 1 or args.simulate_ws > 1 else None
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -177,6 +267,7 @@ def main():
     el = time.perf_counter() - t0
     eng_events = eng.timing_events
     eng.timing_events = None
+    comm_events, eng.comm_events = eng.comm_events, None
     red_dev = dev if use_nccl else "cpu"
     el_t = torch.tensor([el], dtype=torch.float64, device=red_dev)
     if world > 1:
@@ -204,6 +295,12 @@ def main():
         if d.get("config") == want:  # PMC passes of this same configuration (profiles/README.md)
             traffic = d.get("hbm_bytes_per_launch")
             traffic_src = str(tj.relative_to(REPO) if tj.is_absolute() else tj)
+
+    collectives = None
+    if world > 1:
+        collectives = collective_summary(comm_events, args.steps, world, red_dev)
+        if args.comm == "rccl" and not args.no_comm_sweep:
+            collectives["sweep"] = comm_sweep(opt._comm, eng.arena, world, red_dev)
 
     if rank == 0 and args.simulate_ws > 1:
         print(json.dumps({"diagnostic": f"simulate-ws {args.simulate_ws}: rank-0 compute of the "
@@ -234,6 +331,7 @@ def main():
                 "param_dtype": args.dtype, "grad_dtype": args.dtype,
                 "state_dtype": "fp32 (master, exp_avg, exp_avg_sq)",
                 "zero": args.zero, "layout": args.layout, "bucket_mb": args.bucket_mb,
+                "bucket_mode": args.buckets,
                 "buckets": eng.K, "parallelism": f"dp{world}",
             },
             "roofline": {
@@ -245,6 +343,8 @@ def main():
                 "traffic_source": traffic_src,
             },
         }
+        if collectives is not None:
+            out["collectives"] = collectives
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(shapes, args.cpu_sample)
         print(json.dumps(out), flush=True)

@@ -119,6 +119,36 @@ int zs_all_reduce(zs_comm* c, const void* send, void* recv, int64_t count, int d
   return ZS_OK;
 }
 
+int zs_reduce(zs_comm* c, const void* send, void* recv, int64_t count, int dtype, int root,
+              uintptr_t stream) {
+  ZS_REQUIRE(c && c->comm, "zs_reduce: NULL communicator");
+  ZS_REQUIRE(count >= 0, "zs_reduce: count < 0");
+  ZS_REQUIRE(root >= 0 && root < c->ws, "zs_reduce: root %d out of range", root);
+  if (count == 0) return ZS_OK;
+  ZS_REQUIRE(send && (recv || c->rank != root), "zs_reduce: NULL buffer");
+  ncclDataType_t t;
+  int rc = to_nccl(dtype, &t);
+  if (rc) return rc;
+  ZS_NCCL(ncclReduce(send, recv, size_t(count), t, ncclSum, root, c->comm,
+                     reinterpret_cast<hipStream_t>(stream)));
+  return ZS_OK;
+}
+
+int zs_broadcast(zs_comm* c, const void* send, void* recv, int64_t count, int dtype, int root,
+                 uintptr_t stream) {
+  ZS_REQUIRE(c && c->comm, "zs_broadcast: NULL communicator");
+  ZS_REQUIRE(count >= 0, "zs_broadcast: count < 0");
+  ZS_REQUIRE(root >= 0 && root < c->ws, "zs_broadcast: root %d out of range", root);
+  if (count == 0) return ZS_OK;
+  ZS_REQUIRE(recv && (send || c->rank != root), "zs_broadcast: NULL buffer");
+  ncclDataType_t t;
+  int rc = to_nccl(dtype, &t);
+  if (rc) return rc;
+  ZS_NCCL(ncclBroadcast(send, recv, size_t(count), t, root, c->comm,
+                        reinterpret_cast<hipStream_t>(stream)));
+  return ZS_OK;
+}
+
 int zs_group_start(void) {
   ZS_NCCL(ncclGroupStart());
   return ZS_OK;

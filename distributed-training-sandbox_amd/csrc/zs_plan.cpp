@@ -8,9 +8,15 @@
 //     i < (ppr+1)*rem ? i // (ppr+1) : (i - rem) // ppr
 //
 // A rank's *stream* is the ordered list of pieces whose optimizer state it owns; pieces start at
-// multiples of align_elems so that every device access can be 16-byte vectorised.  A bucket k
-// concatenates, rank-major, the window [kW, (k+1)W) of every rank's stream, which is exactly the
-// buffer one equal-count reduce-scatter / all-gather moves (Layout R / Layout Z).
+// multiples of align_elems so that every device access can be 16-byte vectorised.  A bucket
+// concatenates, rank-major, one *window* of every rank's stream:
+//   * even buckets cover stream positions [0, Lmin) (Lmin = the shortest stream) with equal windows
+//     of <= W elements: exactly the buffer one equal-count reduce-scatter / all-gather moves;
+//   * ragged buckets (ZS_BUCKETS_RAGGED) cover the rest, [Lmin, L_r) of each longer stream, with
+//     per-rank windows of different length, moved by one grouped reduce / broadcast per owner.
+// Layout R's ownership is uneven (SmolLM3-3B at ws=8: 585.6M vs 335.0M elements), so padding every
+// window to the longest stream (ZS_BUCKETS_PADDED, the simple scheme) makes each equal-count
+// collective move 1.52x the data; the ragged tail moves only the bytes that exist.
 #include <algorithm>
 #include <cstring>
 #include <new>
@@ -26,6 +32,12 @@ struct Piece {
 struct Seg {
   int64_t param, rank, param_off, buf_off, len;
 };
+struct Bucket {
+  int64_t arena_off = 0, elems = 0;
+  int even = 1;
+  std::vector<int64_t> win_off, win_len, win_stream;  // per rank: offset in bucket, length,
+                                                      // offset in the rank's stream
+};
 
 inline int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
@@ -34,10 +46,12 @@ inline int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 struct zs_plan {
   int64_t n = 0;
   int ws = 1, rank = 0, layout = 0;
-  int64_t align = 1, W = 0, K = 0, M = 0;
+  int64_t align = 1, W = 0, K = 0, M = 0, Lmin = 0, arena = 0, K_even = 0;
+  int mode = ZS_BUCKETS_RAGGED;
   std::vector<int64_t> numel;
   std::vector<std::vector<Piece>> pieces;  // per rank
   std::vector<int64_t> stream_len;         // per rank
+  std::vector<Bucket> buckets;
   std::vector<std::vector<Seg>> segs;      // per bucket
 };
 
@@ -53,10 +67,80 @@ static int owner_of(int64_t n, int ws, int64_t i) {
   return int((i - rem) / ppr);
 }
 
+// Buckets over the per-rank streams, then the segments (param slices) of every bucket.
+static void plan_buckets(zs_plan* p) {
+  const int ws = p->ws;
+  const int64_t W = p->W, A = p->align;
+  auto add = [&](Bucket&& b) {
+    b.arena_off = p->arena;
+    p->arena += round_up(b.elems, A);
+    p->buckets.push_back(std::move(b));
+  };
+  // even part: equal windows over [0, Lmin) (all of [0, M) with padding in ZS_BUCKETS_PADDED)
+  const int64_t even_end = p->mode == ZS_BUCKETS_PADDED ? p->M : p->Lmin;
+  for (int64_t pos = 0; pos < even_end; pos += W) {
+    const int64_t wk = std::min(W, even_end - pos);  // multiple of A: every stream length is
+    Bucket b;
+    b.even = 1;
+    for (int r = 0; r < ws; ++r) {
+      b.win_off.push_back(int64_t(r) * wk);
+      b.win_len.push_back(wk);
+      b.win_stream.push_back(pos);
+    }
+    b.elems = int64_t(ws) * wk;
+    add(std::move(b));
+  }
+  p->K_even = int64_t(p->buckets.size());
+  // ragged tail: per-rank cursors from Lmin; each bucket holds at most ws*W elements, shared
+  // equally by the ranks that still have stream left (a rank with a short tail leaves its share
+  // to the others in the next bucket)
+  std::vector<int64_t> cur(ws, even_end);
+  const int64_t cap = int64_t(ws) * W;
+  for (;;) {
+    int active = 0;
+    for (int r = 0; r < ws; ++r) active += cur[r] < p->stream_len[r];
+    if (active == 0) break;
+    const int64_t share = std::max(A, cap / active / A * A);
+    Bucket b;
+    b.even = 0;
+    int64_t off = 0;
+    for (int r = 0; r < ws; ++r) {
+      const int64_t len = std::min(share, p->stream_len[r] - cur[r]);  // <= 0: rank is done
+      b.win_off.push_back(off);
+      b.win_len.push_back(std::max<int64_t>(len, 0));
+      b.win_stream.push_back(cur[r]);
+      if (len > 0) {
+        off += round_up(len, A);
+        cur[r] += len;
+      }
+    }
+    b.elems = off;
+    add(std::move(b));
+  }
+  p->K = int64_t(p->buckets.size());
+  // segments: walk each rank's windows (monotone in its stream) against its pieces
+  p->segs.assign(p->K, {});
+  for (int r = 0; r < ws; ++r) {
+    for (const Piece& pc : p->pieces[r]) {
+      if (pc.len == 0) continue;
+      const int64_t a = pc.stream_off, e = pc.stream_off + pc.len;
+      for (int64_t k = 0; k < p->K; ++k) {
+        const Bucket& b = p->buckets[k];
+        const int64_t lo = std::max(a, b.win_stream[r]);
+        const int64_t hi = std::min(e, b.win_stream[r] + b.win_len[r]);
+        if (lo >= hi) continue;
+        p->segs[k].push_back({pc.param, r, pc.param_off + (lo - a),
+                              b.win_off[r] + (lo - b.win_stream[r]), hi - lo});
+      }
+    }
+  }
+}
+
 extern "C" {
 
 int zs_plan_create(int64_t n_params, const int64_t* numels, const int64_t* dim0, int ws, int rank,
-                   int layout, int64_t align_elems, int64_t window_elems, zs_plan** out) {
+                   int layout, int64_t align_elems, int64_t window_elems, int bucket_mode,
+                   zs_plan** out) {
   ZS_REQUIRE(out != nullptr, "zs_plan_create: out is NULL");
   *out = nullptr;
   ZS_REQUIRE(n_params >= 0, "zs_plan_create: n_params < 0");
@@ -67,6 +151,8 @@ int zs_plan_create(int64_t n_params, const int64_t* numels, const int64_t* dim0,
              "zs_plan_create: unknown layout %d", layout);
   ZS_REQUIRE(align_elems >= 1, "zs_plan_create: align_elems must be >= 1");
   ZS_REQUIRE(window_elems >= 0, "zs_plan_create: window_elems < 0");
+  ZS_REQUIRE(bucket_mode == ZS_BUCKETS_RAGGED || bucket_mode == ZS_BUCKETS_PADDED,
+             "zs_plan_create: unknown bucket_mode %d", bucket_mode);
   ZS_REQUIRE(layout != ZS_LAYOUT_Z || dim0 != nullptr, "zs_plan_create: layout Z needs dim0");
   for (int64_t i = 0; i < n_params; ++i) {
     ZS_REQUIRE(numels[i] >= 0, "zs_plan_create: numel[%lld] < 0", (long long)i);
@@ -131,24 +217,16 @@ int zs_plan_create(int64_t n_params, const int64_t* numels, const int64_t* dim0,
   }
 
   p->M = 0;
-  for (int r = 0; r < ws; ++r) p->M = std::max(p->M, p->stream_len[r]);
+  p->Lmin = ws > 0 ? p->stream_len[0] : 0;
+  for (int r = 0; r < ws; ++r) {
+    p->M = std::max(p->M, p->stream_len[r]);
+    p->Lmin = std::min(p->Lmin, p->stream_len[r]);
+  }
   int64_t W = window_elems == 0 ? p->M : round_up(window_elems, align_elems);
   if (W > p->M) W = p->M;
   p->W = W;
-  p->K = (W == 0) ? 0 : (p->M + W - 1) / W;
-  p->segs.assign(p->K, {});
-  for (int r = 0; r < ws; ++r) {
-    for (const Piece& pc : p->pieces[r]) {
-      if (pc.len == 0) continue;
-      const int64_t k0 = pc.stream_off / W, k1 = (pc.stream_off + pc.len - 1) / W;
-      for (int64_t k = k0; k <= k1; ++k) {
-        const int64_t lo = std::max(pc.stream_off, k * W);
-        const int64_t hi = std::min(pc.stream_off + pc.len, (k + 1) * W);
-        p->segs[k].push_back({pc.param, r, pc.param_off + (lo - pc.stream_off),
-                              int64_t(r) * W + (lo - k * W), hi - lo});
-      }
-    }
-  }
+  p->mode = bucket_mode;
+  if (W > 0) plan_buckets(p);
   *out = p;
   return ZS_OK;
 }
@@ -167,6 +245,27 @@ int zs_plan_info(const zs_plan* p, int64_t* info) {
   info[4] = p->W;
   info[5] = p->K;
   info[6] = p->M;
+  info[7] = p->arena;
+  info[8] = p->K_even;
+  info[9] = p->mode;
+  return ZS_OK;
+}
+
+int zs_plan_bucket(const zs_plan* p, int64_t bucket, int64_t* arena_off, int64_t* elems,
+                   int* even, int64_t* win_off, int64_t* win_len, int64_t* win_stream) {
+  ZS_REQUIRE(p && arena_off && elems && even && win_off && win_len && win_stream,
+             "zs_plan_bucket: NULL argument");
+  ZS_REQUIRE(bucket >= 0 && bucket < p->K, "zs_plan_bucket: bucket %lld out of range",
+             (long long)bucket);
+  const Bucket& b = p->buckets[bucket];
+  *arena_off = b.arena_off;
+  *elems = b.elems;
+  *even = b.even;
+  for (int r = 0; r < p->ws; ++r) {
+    win_off[r] = b.win_off[r];
+    win_len[r] = b.win_len[r];
+    win_stream[r] = b.win_stream[r];
+  }
   return ZS_OK;
 }
 

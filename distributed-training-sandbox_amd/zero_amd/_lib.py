@@ -17,19 +17,21 @@ LIB_PATH = Path(os.environ.get("ZERO_AMD_LIB", Path(__file__).resolve().parent /
 ZS_OK, ZS_ERR_INVALID, ZS_ERR_HIP, ZS_ERR_RCCL, ZS_ERR_NOMEM = 0, 1, 2, 3, 4
 ZS_F32, ZS_BF16 = 0, 1
 ZS_LAYOUT_R, ZS_LAYOUT_Z, ZS_LAYOUT_F = 0, 1, 2
+ZS_BUCKETS_RAGGED, ZS_BUCKETS_PADDED = 0, 1
+ABI_VERSION = 2
 ZS_UNIQUE_ID_BYTES = 128
 
 # Every symbol include/zero_amd.h declares (tests check the library exports all of them).
 EXPORTED = (
     "zs_abi_version", "zs_last_error",
     "zs_plan_create", "zs_plan_destroy", "zs_plan_info", "zs_plan_owner_range", "zs_plan_owner_of",
-    "zs_plan_stream_len", "zs_plan_num_pieces", "zs_plan_pieces", "zs_plan_num_segments",
-    "zs_plan_segments",
+    "zs_plan_stream_len", "zs_plan_num_pieces", "zs_plan_pieces", "zs_plan_bucket",
+    "zs_plan_num_segments", "zs_plan_segments",
     "zs_copyset_create", "zs_copyset_run", "zs_copyset_destroy",
     "zs_adam_hparams_init", "zs_adamset_create", "zs_adamset_run", "zs_adamset_destroy",
     "zs_adamset_stats",
     "zs_comm_unique_id", "zs_comm_init", "zs_comm_destroy", "zs_reduce_scatter", "zs_all_gather",
-    "zs_all_reduce", "zs_group_start", "zs_group_end", "zs_rccl_version",
+    "zs_all_reduce", "zs_reduce", "zs_broadcast", "zs_group_start", "zs_group_end", "zs_rccl_version",
 )
 
 
@@ -67,7 +69,7 @@ _SIGS = {
     "zs_abi_version": ([], ctypes.c_int),
     "zs_last_error": ([], ctypes.c_char_p),
     "zs_plan_create": ([_I64, _PI64, _PI64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _I64, _I64,
-                        ctypes.POINTER(_P)], ctypes.c_int),
+                        ctypes.c_int, ctypes.POINTER(_P)], ctypes.c_int),
     "zs_plan_destroy": ([_P], ctypes.c_int),
     "zs_plan_info": ([_P, _PI64], ctypes.c_int),
     "zs_plan_owner_range": ([_P, ctypes.c_int, _PI64, _PI64], ctypes.c_int),
@@ -75,6 +77,8 @@ _SIGS = {
     "zs_plan_stream_len": ([_P, ctypes.c_int, _PI64], ctypes.c_int),
     "zs_plan_num_pieces": ([_P, ctypes.c_int, _PI64], ctypes.c_int),
     "zs_plan_pieces": ([_P, ctypes.c_int, _PI64, _PI64, _PI64, _PI64], ctypes.c_int),
+    "zs_plan_bucket": ([_P, _I64, _PI64, _PI64, ctypes.POINTER(ctypes.c_int), _PI64, _PI64, _PI64],
+                       ctypes.c_int),
     "zs_plan_num_segments": ([_P, _I64, _PI64], ctypes.c_int),
     "zs_plan_segments": ([_P, _I64, _PI64, _PI64, _PI64, _PI64, _PI64], ctypes.c_int),
     "zs_copyset_create": ([_PU64, _PU64, _PI64, _I64, ctypes.POINTER(_P)], ctypes.c_int),
@@ -94,6 +98,8 @@ _SIGS = {
     "zs_reduce_scatter": ([_P, _P, _P, _I64, ctypes.c_int, _U], ctypes.c_int),
     "zs_all_gather": ([_P, _P, _P, _I64, ctypes.c_int, _U], ctypes.c_int),
     "zs_all_reduce": ([_P, _P, _P, _I64, ctypes.c_int, _U], ctypes.c_int),
+    "zs_reduce": ([_P, _P, _P, _I64, ctypes.c_int, ctypes.c_int, _U], ctypes.c_int),
+    "zs_broadcast": ([_P, _P, _P, _I64, ctypes.c_int, ctypes.c_int, _U], ctypes.c_int),
     "zs_group_start": ([], ctypes.c_int),
     "zs_group_end": ([], ctypes.c_int),
     "zs_rccl_version": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
@@ -110,8 +116,9 @@ def _load():
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
-    if lib.zs_abi_version() != 1:
-        raise ImportError(f"zero_amd: ABI version {lib.zs_abi_version()} != 1 in {LIB_PATH}")
+    if lib.zs_abi_version() != ABI_VERSION:
+        raise ImportError(f"zero_amd: ABI version {lib.zs_abi_version()} != {ABI_VERSION} in "
+                          f"{LIB_PATH} (rebuild: make -C distributed-training-sandbox_amd)")
     return lib
 
 

@@ -39,7 +39,7 @@ class ShardedOptimizerBase:
     _variant = 2
 
     def __init__(self, optimizer: Optimizer, *, layout: str = "reference",
-                 bucket_mb: float = 256.0, comm=None, sync: bool = True):
+                 bucket_mb: float = 256.0, comm=None, sync: bool = True, buckets: str = "ragged"):
         if not isinstance(optimizer, torch.optim.Adam):
             raise TypeError("zero_amd ShardedOptimizer wraps torch.optim.Adam / AdamW "
                             f"(got {type(optimizer).__name__})")
@@ -67,6 +67,7 @@ class ShardedOptimizerBase:
         self.step_time = 0.0
         self.world_size, self.rank = world_size, rank
         self._layout = layout
+        self._buckets = buckets
         self._bucket_bytes = int(bucket_mb * (1 << 20))
         self._comm = comm
         self._sync = sync
@@ -87,7 +88,7 @@ class ShardedOptimizerBase:
             self._comm = comm
         self.engine = ShardEngine(self.params, self._group_of, self.world_size, self.rank,
                                   layout=self._layout, carry=self._carry, comm=comm,
-                                  bucket_bytes=self._bucket_bytes)
+                                  bucket_bytes=self._bucket_bytes, buckets=self._buckets)
         if self.engine.plan.layout != 0:
             return
         self._expose_state()

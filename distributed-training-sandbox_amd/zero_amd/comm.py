@@ -5,7 +5,8 @@ bootstrapped by broadcasting an ``ncclUniqueId`` over the default ``torch.distri
 bucketed reduce-scatter / all-gather / all-reduce enqueued on the caller's HIP stream.  It replaces
 the reference's per-tensor blocking c10d calls (zero1.py:83,102; zero2.py:107,133; zero3.py:39,146).
 
-The engine only needs three methods with this signature, so tests can substitute a gloo-backed
+The engine only needs the methods below (reduce_scatter / all_gather for even buckets,
+reduce_v / broadcast_v for ragged ones, all_reduce for ZeRO-3), so tests can substitute a gloo-backed
 implementation to exercise the multi-rank orchestration on one GPU (RCCL does not allow two ranks
 of one communicator on the same device).
 """
@@ -84,6 +85,25 @@ class RcclComm:
         assert recv.numel() == send.numel() * self.ws and send.dtype == recv.dtype
         _lib.call("zs_all_gather", self._h, send.data_ptr(), recv.data_ptr(), send.numel(),
                   zs_dtype(send.dtype), stream_handle(stream))
+
+    def reduce_v(self, buf: torch.Tensor, win_off, win_len, stream) -> None:
+        """Reduce-scatter-v in place: window r of ``buf`` (offset win_off[r], win_len[r] elements)
+        is SUM-reduced onto rank r — one ncclReduce per owner, launched as one RCCL group."""
+        dt, h, base, es = zs_dtype(buf.dtype), stream_handle(stream), buf.data_ptr(), buf.element_size()
+        with self.group():
+            for root, (off, n) in enumerate(zip(win_off, win_len)):
+                if n:
+                    ptr = base + int(off) * es
+                    _lib.call("zs_reduce", self._h, ptr, ptr, int(n), dt, root, h)
+
+    def broadcast_v(self, buf: torch.Tensor, win_off, win_len, stream) -> None:
+        """All-gather-v in place: window r of ``buf`` is broadcast from rank r (one RCCL group)."""
+        dt, h, base, es = zs_dtype(buf.dtype), stream_handle(stream), buf.data_ptr(), buf.element_size()
+        with self.group():
+            for root, (off, n) in enumerate(zip(win_off, win_len)):
+                if n:
+                    ptr = base + int(off) * es
+                    _lib.call("zs_broadcast", self._h, ptr, ptr, int(n), dt, root, h)
 
     def all_reduce(self, t: torch.Tensor, stream) -> None:
         _lib.call("zs_all_reduce", self._h, t.data_ptr(), t.data_ptr(), t.numel(),

@@ -3,17 +3,24 @@
 One ``ShardEngine`` per ``ShardedOptimizer``.  It owns, for this rank's optimizer shard (the
 *stream* the planner assigns it), flat fp32 buffers for exp_avg / exp_avg_sq (+ max_exp_avg_sq,
 the fp32 master of bf16 params, and the ZeRO-1 gradient carry), and one persistent *arena* of
-bucket buffers in the parameter dtype.  A bucket buffer is ws windows of W elements, rank-major,
-so a single in-place RCCL reduce-scatter hands every rank the summed gradient of its own window
-and a single in-place all-gather hands every rank all updated windows.
+bucket buffers in the parameter dtype.  A bucket buffer is one window of every rank's stream,
+rank-major.  In an *even* bucket (stream positions every rank has) the windows are equal, so a
+single in-place RCCL reduce-scatter hands every rank the summed gradient of its own window and a
+single in-place all-gather hands every rank all updated windows.  Layout R's streams differ in
+length (the reference assigns whole parameters by index); the part of the longer streams beyond
+the shortest one goes into *ragged* buckets, moved by one grouped RCCL reduce (and broadcast) per
+owner — the reduce-scatter-v / all-gather-v — instead of zero-padding every window to the longest
+stream (SURVEY.md §7 "Uneven ownership vs equal-count reduce-scatter").
 
 Per step and bucket k (reference loop it replaces in brackets):
   compute stream: pack(k)  — gfx950 gather of every param's grad slice into bucket k
                               [zero2.py:99-104 flatten + cat×ws; zero1.py has no copy]
-  comm stream:    RS(k)     — RCCL reduce-scatter, in place    [zero1.py:81-84 / zero2.py:107]
+  comm stream:    RS(k)     — RCCL reduce-scatter (ragged: grouped reduce), in place
+                              [zero1.py:81-84 / zero2.py:107]
   compute stream: adam(k)  — fused Adam on this rank's window, grad /ws folded in, writes the
                               updated param into its bucket slot [zero1.py:88 / zero2.py:111,120]
-  comm stream:    AG(k)     — RCCL all-gather, in place          [zero1.py:95-102 / zero2.py:126-133]
+  comm stream:    AG(k)     — RCCL all-gather (ragged: grouped broadcast), in place
+                              [zero1.py:95-102 / zero2.py:126-133]
   compute stream: unpack(k) — gfx950 scatter of bucket k back into module storage
 Streams are ordered by events only; adam(k) overlaps RS(k+1), unpack(k) overlaps AG(k+1).
 With ws == 1 there is nothing to exchange and the step is one fused-Adam launch that reads
@@ -40,7 +47,8 @@ def _ptr(t: torch.Tensor | None) -> int:
 
 class ShardEngine:
     def __init__(self, params, group_of, ws: int, rank: int, *, layout="reference", carry=False,
-                 comm=None, bucket_bytes: int = 256 << 20, align: int = ALIGN_ELEMS):
+                 comm=None, bucket_bytes: int = 256 << 20, align: int = ALIGN_ELEMS,
+                 buckets: str = "ragged"):
         if not params:
             raise ValueError("ShardEngine: no parameters")
         dev = params[0].device
@@ -68,7 +76,8 @@ class ShardEngine:
         numels = [p.numel() for p in params]
         dim0 = [p.shape[0] if p.dim() > 0 else 1 for p in params]
         window = 0 if ws == 1 else max(align, int(bucket_bytes) // (ws * self.es))
-        self.plan = Plan(numels, ws, rank, layout, dim0=dim0, align_elems=align, window_elems=window)
+        self.plan = Plan(numels, ws, rank, layout, dim0=dim0, align_elems=align, window_elems=window,
+                         buckets=buckets)
         self.W, self.K = self.plan.window, self.plan.num_buckets
         self.L = self.plan.stream_len(rank)
         self.pieces = self.plan.pieces(rank)
@@ -85,7 +94,8 @@ class ShardEngine:
                 self.master[so:so + n].copy_(params[i].detach().reshape(-1)[po:po + n])
         self.arena = None
         if ws > 1:
-            self.arena = torch.zeros(self.K * self.plan.bucket_elems, dtype=dtype, device=dev)
+            self.arena = torch.zeros(self.plan.arena_elems, dtype=dtype, device=dev)
+            self.buckets = [self.plan.bucket(k) for k in range(self.K)]
             self.segs = [self.plan.segments(k) for k in range(self.K)]
             self.comm_stream = torch.cuda.Stream(device=dev)
             mk = lambda: [torch.cuda.Event() for _ in range(self.K)]  # noqa: E731
@@ -95,6 +105,7 @@ class ShardEngine:
         self.steps = np.zeros(len(params), np.int64)  # torch's per-param state['step']
         self._cache = {}
         self.timing_events = None  # optional list of (start, end) events around each Adam launch
+        self.comm_events = None    # optional list of (kind, even, start, end, bus_bytes) per collective
         self.last_adam_bytes = 0
 
     # ------------------------------------------------------------------------------------------
@@ -214,33 +225,61 @@ class ShardEngine:
             rows = self._adam_rows(idx, g, p, p, 0, so, n)
         self._run_adam("local", rows, idx, hparams_of, stream)
 
+    def _bucket_buf(self, k):
+        b = self.buckets[k]
+        return b, self.arena[b.arena_off:b.arena_off + b.elems]
+
+    def _collective(self, k, kind):
+        """Reduce ("rs") or gather ("ag") bucket k in place on the comm stream."""
+        b, buf = self._bucket_buf(k)
+        cs, r, ws = self.comm_stream, self.rank, self.ws
+        if self.comm_events is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(cs)
+        if b.even:
+            w = int(b.win_len[0])
+            mine = buf[r * w:(r + 1) * w]
+            if kind == "rs":
+                self.comm.reduce_scatter(buf, mine, cs)
+            else:
+                self.comm.all_gather(mine, buf, cs)
+            bus = b.elems * self.es * (ws - 1) / ws  # ring RS / AG bus bytes
+        else:
+            if kind == "rs":
+                self.comm.reduce_v(buf, b.win_off, b.win_len, cs)
+            else:
+                self.comm.broadcast_v(buf, b.win_off, b.win_len, cs)
+            bus = int(b.win_len.sum()) * self.es  # reduce / broadcast bus bytes = message bytes
+        if self.comm_events is not None:
+            e1.record(cs)
+            self.comm_events.append((kind, bool(b.even), e0, e1, bus))
+
     def _step_buckets(self, gptr, has, hparams_of, stream):
         es = np.uint64(self.es)
         pptr = np.fromiter((_ptr(p) for p in self.params), np.uint64, len(self.params))
         base = np.uint64(self.arena.data_ptr())
-        BE, W, r = self.plan.bucket_elems, self.W, self.rank
+        r = self.rank
         cs = self.comm_stream
         self.ev_c0.record(cs)
         for k in range(self.K):  # pack every bucket on the compute stream
-            s = self.segs[k]
+            s, b = self.segs[k], self.buckets[k]
             src = np.where(has[s.param], gptr[s.param] + s.param_off.astype(np.uint64) * es, 0)
-            dst = base + np.uint64(k * BE) * es + s.buf_off.astype(np.uint64) * es
+            dst = base + np.uint64(b.arena_off) * es + s.buf_off.astype(np.uint64) * es
             nb = s.length * self.es
             sig = src.tobytes() + dst.tobytes()
             self._cached(("pack", k), sig, lambda: CopySet(src, dst, nb)).run(stream)
             self.ev_pack[k].record(stream)
-        for k in range(self.K):  # in-place reduce-scatter of each bucket
+        for k in range(self.K):  # in-place reduce-scatter (-v) of each bucket
             cs.wait_event(self.ev_pack[k])
-            buf = self.arena[k * BE:(k + 1) * BE]
-            self.comm.reduce_scatter(buf, buf[r * W:(r + 1) * W], cs)
+            self._collective(k, "rs")
             self.ev_rs[k].record(cs)
         for k in range(self.K):  # fused Adam on this rank's window
             stream.wait_event(self.ev_rs[k])
-            s = self.segs[k]
+            s, b = self.segs[k], self.buckets[k]
             own = np.nonzero(s.rank == r)[0]
             idx = s.param[own]
-            slot = base + np.uint64(k * BE) * es + s.buf_off[own].astype(np.uint64) * es
-            so = (s.buf_off[own] - r * W) + k * W
+            slot = base + np.uint64(b.arena_off) * es + s.buf_off[own].astype(np.uint64) * es
+            so = (s.buf_off[own] - int(b.win_off[r])) + int(b.win_stream[r])
             ln = s.length[own]
             po = s.param_off[own].astype(np.uint64)
             live = has[idx]
@@ -258,16 +297,15 @@ class ShardEngine:
                 self._cached(("pass", k), src.tobytes() + slot[dead].tobytes(),
                              lambda: CopySet(src, slot[dead], nb)).run(stream)
             self.ev_adam[k].record(stream)
-        for k in range(self.K):  # in-place all-gather of the updated windows
+        for k in range(self.K):  # in-place all-gather (-v) of the updated windows
             cs.wait_event(self.ev_adam[k])
-            buf = self.arena[k * BE:(k + 1) * BE]
-            self.comm.all_gather(buf[r * W:(r + 1) * W], buf, cs)
+            self._collective(k, "ag")
             self.ev_ag[k].record(cs)
         self.ev_c1.record(cs)
         for k in range(self.K):  # scatter every bucket back into module storage
             stream.wait_event(self.ev_ag[k])
-            s = self.segs[k]
-            src = base + np.uint64(k * BE) * es + s.buf_off.astype(np.uint64) * es
+            s, b = self.segs[k], self.buckets[k]
+            src = base + np.uint64(b.arena_off) * es + s.buf_off.astype(np.uint64) * es
             dst = pptr[s.param] + s.param_off.astype(np.uint64) * es
             self._cached(("unpack", k), dst.tobytes(),
                          lambda: CopySet(src, dst, s.length * self.es)).run(stream)

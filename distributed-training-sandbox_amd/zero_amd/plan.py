@@ -13,10 +13,11 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from ._lib import ZS_LAYOUT_F, ZS_LAYOUT_R, ZS_LAYOUT_Z
+from ._lib import ZS_BUCKETS_PADDED, ZS_BUCKETS_RAGGED, ZS_LAYOUT_F, ZS_LAYOUT_R, ZS_LAYOUT_Z
 
 LAYOUTS = {"reference": ZS_LAYOUT_R, "R": ZS_LAYOUT_R, "chunk": ZS_LAYOUT_Z, "Z": ZS_LAYOUT_Z,
            "flat": ZS_LAYOUT_F, "F": ZS_LAYOUT_F}
+BUCKET_MODES = {"ragged": ZS_BUCKETS_RAGGED, "padded": ZS_BUCKETS_PADDED}
 
 
 def _i64p(a: np.ndarray):
@@ -40,11 +41,21 @@ class Segments:
     length: np.ndarray
 
 
+@dataclass(frozen=True)
+class Bucket:
+    arena_off: int          # element offset of the bucket inside the arena
+    elems: int              # bucket buffer length (elements)
+    even: bool              # equal windows at r*len → reduce-scatter / all-gather
+    win_off: np.ndarray     # per rank: window offset inside the bucket
+    win_len: np.ndarray     # per rank: window length (0 = nothing)
+    win_stream: np.ndarray  # per rank: stream offset of the window's first element
+
+
 class Plan:
     """Ownership + bucket layout for ``n`` parameters over ``ws`` ranks (seen from ``rank``)."""
 
     def __init__(self, numels, ws: int, rank: int, layout="reference", dim0=None,
-                 align_elems: int = 64, window_elems: int = 0):
+                 align_elems: int = 64, window_elems: int = 0, buckets: str = "ragged"):
         self.layout = LAYOUTS[layout] if isinstance(layout, str) else int(layout)
         numels = np.ascontiguousarray(np.asarray(numels, dtype=np.int64))
         self.numels = numels
@@ -55,12 +66,13 @@ class Plan:
         h = ctypes.c_void_p()
         _lib.call("zs_plan_create", len(numels), _i64p(numels) if len(numels) else None,
                   _i64p(d0) if d0 is not None else None, int(ws), int(rank), self.layout,
-                  int(align_elems), int(window_elems), ctypes.byref(h))
+                  int(align_elems), int(window_elems), BUCKET_MODES[buckets], ctypes.byref(h))
         self._h = h
-        info = np.zeros(7, np.int64)
+        info = np.zeros(10, np.int64)
         _lib.call("zs_plan_info", self._h, _i64p(info))
-        (self.n, self.ws, self.rank, _, self.window, self.num_buckets,
-         self.max_stream_len) = (int(x) for x in info)
+        (self.n, self.ws, self.rank, _, self.window, self.num_buckets, self.max_stream_len,
+         self.arena_elems, self.num_even, _) = (int(x) for x in info)
+        self.bucket_mode = buckets
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -106,7 +118,9 @@ class Plan:
             _lib.call("zs_plan_segments", self._h, int(bucket), *(_i64p(a) for a in arrs))
         return Segments(*arrs)
 
-    @property
-    def bucket_elems(self) -> int:
-        """Elements of one bucket buffer (ws windows of W)."""
-        return self.ws * self.window
+    def bucket(self, k: int) -> Bucket:
+        ao, el, ev = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int()
+        arrs = [np.zeros(self.ws, np.int64) for _ in range(3)]
+        _lib.call("zs_plan_bucket", self._h, int(k), ctypes.byref(ao), ctypes.byref(el),
+                  ctypes.byref(ev), *(_i64p(a) for a in arrs))
+        return Bucket(ao.value, el.value, bool(ev.value), *arrs)

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ZS_ABI_VERSION 1
+#define ZS_ABI_VERSION 2
 
 enum zs_status {
   ZS_OK = 0,
@@ -43,6 +43,12 @@ enum zs_layout {
   ZS_LAYOUT_F = 2   /* flat: one balanced contiguous 1/ws slice of the concatenated params */
 };
 
+/* Bucketing of the per-rank streams (see zs_plan_bucket). */
+enum zs_bucket_mode {
+  ZS_BUCKETS_RAGGED = 0, /* equal windows over the shortest stream, then per-owner ragged windows */
+  ZS_BUCKETS_PADDED = 1  /* equal windows over the longest stream, shorter streams zero-padded */
+};
+
 int zs_abi_version(void);
 const char* zs_last_error(void);
 
@@ -55,13 +61,16 @@ typedef struct zs_plan zs_plan;
  * zero3.py:82-110).  numels[i] = params[i].numel(); dim0[i] = params[i].shape[0] (1 for 0-d;
  * only read for ZS_LAYOUT_Z, may be NULL otherwise).  align_elems: every piece starts at a
  * multiple of this in its rank's stream (>=1).  window_elems: per-rank elements per bucket
- * (0 = one bucket holding the whole longest stream). */
+ * (0 = one bucket holding the whole longest stream).  bucket_mode: ZS_BUCKETS_*. */
 int zs_plan_create(int64_t n_params, const int64_t* numels, const int64_t* dim0, int ws, int rank,
-                   int layout, int64_t align_elems, int64_t window_elems, zs_plan** out);
+                   int layout, int64_t align_elems, int64_t window_elems, int bucket_mode,
+                   zs_plan** out);
 int zs_plan_destroy(zs_plan* plan);
 
-/* info[0..6] = {n_params, ws, rank, layout, window_elems W, num_buckets K, max_stream_len M} */
-int zs_plan_info(const zs_plan* plan, int64_t* info7);
+/* info[0..9] = {n_params, ws, rank, layout, window_elems W, num_buckets K, max_stream_len M,
+ *              arena_elems (all buckets, each starting align_elems-aligned), num_even_buckets,
+ *              bucket_mode} */
+int zs_plan_info(const zs_plan* plan, int64_t* info10);
 
 /* Parameter-index ownership [start,end) of `rank` (zero1.py:55-62).  Same formula for every
  * layout: it is what the reference uses to filter the inner optimizer's param_groups. */
@@ -79,8 +88,17 @@ int zs_plan_num_pieces(const zs_plan* plan, int rank, int64_t* n);
 int zs_plan_pieces(const zs_plan* plan, int rank, int64_t* param, int64_t* param_off,
                    int64_t* stream_off, int64_t* len);
 
-/* Segments of bucket k (all ranks): bucket buffer = ws windows of W elements, rank-major.
- * buf_off is the element offset inside the bucket buffer (rank*W + offset in window). */
+/* Bucket k: its offset and length (elements) in the arena, whether it is *even* (every window
+ * the same length and window r at r*len: one equal-count reduce-scatter / all-gather moves it;
+ * buckets 0..num_even-1) or *ragged* (one grouped reduce / broadcast per owner moves it), and per
+ * rank r (arrays of ws): the window's offset inside the bucket, its length (0 = no data), and the
+ * stream offset of its first element.  Replaces the per-tensor collective loop over
+ * self.params (zero1.py:80-84, zero2.py:94-113) with a fixed bucket schedule. */
+int zs_plan_bucket(const zs_plan* plan, int64_t bucket, int64_t* arena_off, int64_t* elems,
+                   int* even, int64_t* win_off, int64_t* win_len, int64_t* win_stream);
+
+/* Segments of bucket k (all ranks): param slices and where they sit in the bucket buffer.
+ * buf_off is the element offset inside the bucket buffer (win_off[rank] + offset in window). */
 int zs_plan_num_segments(const zs_plan* plan, int64_t bucket, int64_t* n);
 int zs_plan_segments(const zs_plan* plan, int64_t bucket, int64_t* param, int64_t* rank,
                      int64_t* param_off, int64_t* buf_off, int64_t* len);
@@ -166,6 +184,13 @@ int zs_all_gather(zs_comm* comm, const void* send, void* recv, int64_t send_coun
                   uintptr_t stream);
 int zs_all_reduce(zs_comm* comm, const void* send, void* recv, int64_t count, int dtype,
                   uintptr_t stream);
+/* SUM-reduce count elements onto `root` (recv only read on root; in place when send == recv) and
+ * broadcast count elements from `root`.  Issued once per owner inside zs_group_start/end they
+ * form the reduce-scatter-v / all-gather-v of a ragged bucket (zero2.py:107 / zero2.py:133). */
+int zs_reduce(zs_comm* comm, const void* send, void* recv, int64_t count, int dtype, int root,
+              uintptr_t stream);
+int zs_broadcast(zs_comm* comm, const void* send, void* recv, int64_t count, int dtype, int root,
+                 uintptr_t stream);
 int zs_group_start(void);
 int zs_group_end(void);
 /* RCCL version the library is bound to at run time (e.g. 22606). */

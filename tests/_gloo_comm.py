@@ -39,6 +39,37 @@ class GlooStagedComm:
             recv.copy_(out.to(recv.device))
         self.calls.append(("ag", recv.numel()))
 
+    def reduce_v(self, buf, win_off, win_len, stream):
+        stream.synchronize()
+        h = buf.detach().to("cpu", torch.float32)
+        for root, (off, n) in enumerate(zip(win_off, win_len)):
+            if n:
+                part = h[int(off):int(off) + int(n)].clone()
+                dist.reduce(part, dst=dist.get_global_rank(self.group, root) if self.group else root,
+                            group=self.group)
+                if root == self.rank:
+                    h[int(off):int(off) + int(n)] = part
+        with torch.cuda.stream(stream):
+            buf.copy_(h.to(buf.device).to(buf.dtype))
+        self.calls.append(("rsv", int(sum(win_len))))
+
+    def broadcast_v(self, buf, win_off, win_len, stream):
+        stream.synchronize()
+        h = buf.detach().to("cpu")
+        if h.dtype == torch.bfloat16:
+            h = h.view(torch.int16)
+        for root, (off, n) in enumerate(zip(win_off, win_len)):
+            if n:
+                part = h[int(off):int(off) + int(n)].clone()
+                dist.broadcast(part, src=dist.get_global_rank(self.group, root) if self.group else root,
+                               group=self.group)
+                h[int(off):int(off) + int(n)] = part
+        if buf.dtype == torch.bfloat16:
+            h = h.view(torch.bfloat16)
+        with torch.cuda.stream(stream):
+            buf.copy_(h.to(buf.device))
+        self.calls.append(("agv", int(sum(win_len))))
+
     def all_reduce(self, t, stream):
         stream.synchronize()
         h = t.detach().to("cpu", torch.float32)

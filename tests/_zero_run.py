@@ -35,7 +35,8 @@ def module_for(variant: int):
     return mod
 
 
-def run_injected(z, variant: int, rank: int, ws: int, device, comm=None, window_elems=64, tol=1e-6):
+def run_injected(z, variant: int, rank: int, ws: int, device, comm=None, window_elems=64, tol=1e-6,
+                 buckets=None):
     """Replay the fixture's grads through ShardedOptimizer; assert params match every step."""
     mod = module_for(variant)
     steps = int(z["steps"])
@@ -43,6 +44,8 @@ def run_injected(z, variant: int, rank: int, ws: int, device, comm=None, window_
     kw = dict(bucket_mb=ws * window_elems * 4 / (1 << 20))
     if comm is not None:
         kw["comm"] = comm
+    if buckets is not None:
+        kw["buckets"] = buckets
     opt = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), **kw)
     worst = 0.0
     for t in range(steps):

@@ -35,9 +35,9 @@ def test_library_is_gfx950_code_object():
 def test_abi_version_and_error_text():
     from zero_amd import _lib
 
-    assert _lib.lib.zs_abi_version() == 1
+    assert _lib.lib.zs_abi_version() == 2
     h = ctypes.c_void_p()
-    rc = _lib.lib.zs_plan_create(0, None, None, 0, 0, 0, 64, 0, ctypes.byref(h))
+    rc = _lib.lib.zs_plan_create(0, None, None, 0, 0, 0, 64, 0, 0, ctypes.byref(h))
     assert rc == _lib.ZS_ERR_INVALID
     assert b"ws must be >= 1" in _lib.lib.zs_last_error()
 

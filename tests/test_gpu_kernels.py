@@ -182,12 +182,13 @@ def test_pack_unpack_round_trip_c2(gpu):
     ps = [torch.randn(s, device=gpu) for s in shapes]
     outs = [torch.empty_like(p) for p in ps]
     plan = Plan([p.numel() for p in ps], 4, 0, "reference", window_elems=4 << 20)
-    buf = torch.zeros(plan.bucket_elems, device=gpu)
+    arena = torch.zeros(plan.arena_elems, device=gpu)
     st = torch.cuda.current_stream()
+    assert plan.num_even < plan.num_buckets  # ranks own 33.6M / 16.8M elements: ragged tail
     for k in range(plan.num_buckets):
-        s = plan.segments(k)
+        s, b = plan.segments(k), plan.bucket(k)
         src = [ps[i].data_ptr() + 4 * po for i, po in zip(s.param, s.param_off)]
-        dst = [buf.data_ptr() + 4 * bo for bo in s.buf_off]
+        dst = [arena.data_ptr() + 4 * (b.arena_off + bo) for bo in s.buf_off]
         CopySet(src, dst, s.length * 4).run(st)
         CopySet(dst, [outs[i].data_ptr() + 4 * po for i, po in zip(s.param, s.param_off)],
                 s.length * 4).run(st)

@@ -80,6 +80,8 @@ def test_rccl_comm_ws1(gpu, pg1):
     comm.reduce_scatter(t, t, st)
     comm.all_gather(t, t, st)
     comm.all_reduce(t, st)
+    comm.reduce_v(t, [64], [900], st)      # ncclReduce / ncclBroadcast in an RCCL group
+    comm.broadcast_v(t, [0], [1000], st)
     b = t.to(torch.bfloat16)
     comm.all_reduce(b, st)
     torch.cuda.synchronize()
@@ -87,7 +89,7 @@ def test_rccl_comm_ws1(gpu, pg1):
     comm.close()
 
 
-def _mr_worker(rank, ws, port, variant, name):
+def _mr_worker(rank, ws, port, variant, name, buckets="ragged"):
     import sys
     from conftest import PKG, REPO  # noqa: F401  (sets sys.path in the child)
     from _gloo_comm import GlooStagedComm
@@ -95,7 +97,7 @@ def _mr_worker(rank, ws, port, variant, name):
     torch.cuda.set_device(0)
     init_pg(rank, ws, port)
     z = np.load(GOLDEN / name)
-    run_injected(z, variant, rank, ws, torch.device("cuda:0"), comm=GlooStagedComm())
+    run_injected(z, variant, rank, ws, torch.device("cuda:0"), comm=GlooStagedComm(), buckets=buckets)
     dist.barrier()
     dist.destroy_process_group()
     sys.stdout.flush()
@@ -110,3 +112,15 @@ MR_CASES = [(v, f"traj_z{v}_ws{ws}_d16_{m}.npz") for v in (1, 2) for ws in (2, 3
 def test_multirank_injected(gpu, variant, name):
     ws = int(name.split("_ws")[1].split("_")[0])
     mp.spawn(_mr_worker, args=(ws, _port(), variant, name), nprocs=ws, join=True)
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+def test_multirank_padded_buckets(gpu, variant):
+    """The zero-padded bucket schedule (ablation) gives the same trajectory."""
+    mp.spawn(_mr_worker, args=(3, _port(), variant, f"traj_z{variant}_ws3_d16_distinct.npz", "padded"),
+             nprocs=3, join=True)
+
+
+def test_multirank_ws8_ragged(gpu):
+    """ws=8 over the 12-param MLP: most buckets are ragged (one reduce / broadcast per owner)."""
+    mp.spawn(_mr_worker, args=(8, _port(), 2, "traj_z2_ws8_d16_distinct.npz"), nprocs=8, join=True)

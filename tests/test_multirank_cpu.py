@@ -3,7 +3,7 @@ real in-place reduce-scatter / all-gather slices reproduce the reference ZeRO-1/
 
 This emulates, with numpy and the oracle's Adam, exactly the data movement the GPU engine performs
 (engine.py ShardEngine._step_buckets): pack every bucket by the plan's segments, reduce-scatter
-the rank-major buffer so each rank receives its own window, Adam on the owned window (grad /ws and
+the rank-major buffer so each rank receives its own window (ragged buckets: one reduce per owner), Adam on the owned window (grad /ws and
 the ZeRO-1 carry folded in), write the updated params into the window, all-gather, unpack.  The
 device kernels themselves are covered by the -m gpu tests.
 """
@@ -26,7 +26,7 @@ def _port():
     return p
 
 
-def _worker(rank, ws, port, variant, name, window):
+def _worker(rank, ws, port, variant, name, window, buckets="ragged"):
     import os
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -39,8 +39,7 @@ def _worker(rank, ws, port, variant, name, window):
     z = np.load(GOLDEN / name)
     params = [z[f"init_{i}"].copy().reshape(-1) for i in range(12)]
     shapes = [z[f"init_{i}"].shape for i in range(12)]
-    plan = Plan([p.size for p in params], ws, rank, "reference", window_elems=window)
-    W, BE = plan.window, plan.bucket_elems
+    plan = Plan([p.size for p in params], ws, rank, "reference", window_elems=window, buckets=buckets)
     L = plan.stream_len(rank)
     m, v = np.zeros(L, np.float32), np.zeros(L, np.float32)
     carry = np.zeros(L, np.float32)
@@ -49,18 +48,28 @@ def _worker(rank, ws, port, variant, name, window):
         grads = [z[f"r{rank}_t{t}_lg{i}"].reshape(-1) for i in range(12)]
         steps += 1
         for k in range(plan.num_buckets):
-            s = plan.segments(k)
-            buf = np.zeros(BE, np.float32)
+            s, b = plan.segments(k), plan.bucket(k)
+            buf = np.zeros(b.elems, np.float32)
             for i, po, bo, ln in zip(s.param, s.param_off, s.buf_off, s.length):  # pack
                 buf[bo:bo + ln] = grads[i][po:po + ln]
-            out = torch.empty(W)
-            dist.reduce_scatter_tensor(out, torch.from_numpy(buf))  # rank's window = summed grads
-            win = out.numpy()
+            o0, n0 = int(b.win_off[rank]), int(b.win_len[rank])
+            if b.even:  # one equal-count reduce-scatter: rank's window = summed grads
+                out = torch.empty(n0)
+                dist.reduce_scatter_tensor(out, torch.from_numpy(buf))
+                buf[o0:o0 + n0] = out.numpy()
+            else:  # ragged: one reduce per owner (reduce-scatter-v)
+                for root in range(ws):
+                    o, n = int(b.win_off[root]), int(b.win_len[root])
+                    if n:
+                        part = torch.from_numpy(buf[o:o + n].copy())
+                        dist.reduce(part, dst=root)
+                        if root == rank:
+                            buf[o:o + n] = part.numpy()
             for i, r, po, bo, ln in zip(s.param, s.rank, s.param_off, s.buf_off, s.length):
                 if r != rank:
                     continue
-                so = k * W + bo - rank * W
-                gsum = win[bo - rank * W: bo - rank * W + ln]
+                so = int(b.win_stream[rank]) + bo - o0
+                gsum = buf[bo:bo + ln]
                 if variant == 1:  # A_t = (Σ G + (ws-1) A_{t-1}) / ws
                     g = ((gsum + np.float32(ws - 1) * carry[so:so + ln]) / np.float32(ws)).astype(np.float32)
                     carry[so:so + ln] = g
@@ -68,12 +77,20 @@ def _worker(rank, ws, port, variant, name, window):
                     g = (gsum / np.float32(ws)).astype(np.float32)
                 p, mm, vv, _ = zo.adam_update(params[i][po:po + ln], g, m[so:so + ln], v[so:so + ln], steps)
                 m[so:so + ln], v[so:so + ln] = mm, vv
-                win[bo - rank * W: bo - rank * W + ln] = p
-            full = torch.empty(BE)
-            dist.all_gather_into_tensor(full, torch.from_numpy(win))
-            full = full.numpy()
+                buf[bo:bo + ln] = p
+            if b.even:
+                full = torch.empty(b.elems)
+                dist.all_gather_into_tensor(full, torch.from_numpy(buf[o0:o0 + n0].copy()))
+                buf = full.numpy()
+            else:  # all-gather-v: one broadcast per owner
+                for root in range(ws):
+                    o, n = int(b.win_off[root]), int(b.win_len[root])
+                    if n:
+                        part = torch.from_numpy(buf[o:o + n].copy())
+                        dist.broadcast(part, src=root)
+                        buf[o:o + n] = part.numpy()
             for i, po, bo, ln in zip(s.param, s.param_off, s.buf_off, s.length):  # unpack
-                params[i][po:po + ln] = full[bo:bo + ln]
+                params[i][po:po + ln] = buf[bo:bo + ln]
         if f"r{rank}_t{t}_p0" in z.files:
             for i in range(12):
                 ref = z[f"r{rank}_t{t}_p{i}"].reshape(-1)
@@ -90,6 +107,18 @@ def _worker(rank, ws, port, variant, name, window):
 def test_bucketed_exchange_matches_reference(variant, ws, window):
     name = f"traj_z{variant}_ws{ws}_d16_distinct.npz"
     mp.spawn(_worker, args=(ws, _port(), variant, name, window), nprocs=ws, join=True)
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+def test_padded_buckets_match_reference(variant):
+    """ZS_BUCKETS_PADDED (every window zero-padded to the longest stream) gives the same result."""
+    name = f"traj_z{variant}_ws3_d16_distinct.npz"
+    mp.spawn(_worker, args=(3, _port(), variant, name, 64, "padded"), nprocs=3, join=True)
+
+
+def test_ws8_ragged_buckets_match_reference():
+    """ws=8 with 12 params: ranks 4-7 own one param each, so most buckets are ragged."""
+    mp.spawn(_worker, args=(8, _port(), 2, "traj_z2_ws8_d16_distinct.npz", 64), nprocs=8, join=True)
 
 
 def test_collective_kats_gloo():

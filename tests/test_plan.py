@@ -56,29 +56,56 @@ def _coverage(plan, numels):
     for c in cover:
         assert (c == 1).all()
     seen = [np.zeros(n, np.int32) for n in numels]
+    arena_used = np.zeros(max(plan.arena_elems, 1), np.int8)
+    stream_seen = [np.zeros(plan.stream_len(r), np.int32) for r in range(ws)]
     for k in range(plan.num_buckets):
+        b = plan.bucket(k)
+        assert b.arena_off % 64 == 0 and b.arena_off + b.elems <= plan.arena_elems
+        assert arena_used[b.arena_off:b.arena_off + b.elems].sum() == 0
+        arena_used[b.arena_off:b.arena_off + b.elems] = 1
+        assert b.even == (k < plan.num_even)
+        if b.even:  # one equal-count reduce-scatter / all-gather: window r at r*len
+            w = int(b.win_len[0])
+            assert (b.win_len == w).all() and (b.win_off == np.arange(ws) * w).all()
+            assert b.elems == ws * w and w <= plan.window
+        for r in range(ws):
+            assert b.win_off[r] % 64 == 0 and b.win_off[r] + b.win_len[r] <= b.elems
+            lo, n = int(b.win_stream[r]), int(b.win_len[r])
+            hi = min(lo + n, plan.stream_len(r))
+            if hi > lo:
+                stream_seen[r][lo:hi] += 1
         s = plan.segments(k)
-        used = np.zeros(plan.bucket_elems, np.int8)
+        used = np.zeros(b.elems, np.int8)
         for i, r, po, bo, ln in zip(s.param, s.rank, s.param_off, s.buf_off, s.length):
-            assert r * plan.window <= bo and bo + ln <= (r + 1) * plan.window
+            assert b.win_off[r] <= bo and bo + ln <= b.win_off[r] + b.win_len[r]
             assert used[bo:bo + ln].sum() == 0
             used[bo:bo + ln] = 1
             seen[i][po:po + ln] += 1
+            # the element's stream position is the same through the piece and through the window
+            pc = plan.pieces(r)
+            j = np.nonzero((pc.param == i) & (pc.param_off <= po) & (po < pc.param_off + pc.length))[0]
+            assert len(j) == 1
+            assert pc.stream_off[j[0]] + (po - pc.param_off[j[0]]) == b.win_stream[r] + (bo - b.win_off[r])
     for c in seen:
         assert (c == 1).all()
+    for r in range(ws):  # every stream position lies in exactly one window
+        assert (stream_seen[r] == 1).all()
 
 
+@pytest.mark.parametrize("buckets", ["ragged", "padded"])
 @pytest.mark.parametrize("layout", ["reference", "chunk", "flat"])
 @pytest.mark.parametrize("ws", [1, 2, 3, 4, 8])
-def test_layout_invariants(layout, ws):
+def test_layout_invariants(layout, ws, buckets):
     rng = np.random.default_rng(ws)
     shapes = [(int(rng.integers(1, 40)), int(rng.integers(1, 9))) for _ in range(23)]
     shapes += [(16, 16), (16,), (1,), (0,), (5, 3)]
     numels = [int(np.prod(s)) for s in shapes]
     dim0 = [s[0] for s in shapes]
     for window in (0, 64, 128, 1000):
-        plan = Plan(numels, ws, 0, layout, dim0=dim0, window_elems=window)
+        plan = Plan(numels, ws, 0, layout, dim0=dim0, window_elems=window, buckets=buckets)
         _coverage(plan, numels)
+        if buckets == "padded" or layout == "flat":
+            assert plan.num_even == plan.num_buckets
         if window:
             assert plan.window % 64 == 0
 
@@ -123,6 +150,33 @@ def test_reference_layout_padding_smollm3():
     assert 1.4 < ratio < 1.6
 
 
+def _bus_elems(plan):
+    """Elements one rank's links carry for the reduce phase: ring RS moves (ws-1)/ws of an even
+    bucket, a reduce moves its whole message."""
+    tot = 0.0
+    for k in range(plan.num_buckets):
+        b = plan.bucket(k)
+        tot += b.elems * (plan.ws - 1) / plan.ws if b.even else int(b.win_len.sum())
+    return tot
+
+
+@pytest.mark.parametrize("ws,max_ratio", [(2, 1.0), (4, 0.85), (8, 0.70)])
+def test_ragged_buckets_cut_smollm3_traffic(ws, max_ratio):
+    """Ragged tails (grouped reduce per owner) instead of zero-padding every window to the longest
+    stream: SmolLM3-3B Layout R moves ~1/3 fewer bytes at ws=8 (SURVEY.md §7 padding figures)."""
+    from zero_amd.shapes import smollm3_3b_shapes
+
+    numels = [int(np.prod(s)) for s in smollm3_3b_shapes()]
+    W = (256 << 20) // (ws * 2)
+    rag = Plan(numels, ws, 0, "reference", window_elems=W, buckets="ragged")
+    pad = Plan(numels, ws, 0, "reference", window_elems=W, buckets="padded")
+    assert rag.arena_elems < pad.arena_elems or ws == 2
+    r = _bus_elems(rag) / _bus_elems(pad)
+    assert r <= max_ratio + 1e-9, r
+    # no bucket buffer exceeds the requested bucket size
+    assert max(rag.bucket(k).elems for k in range(rag.num_buckets)) <= ws * W
+
+
 def test_invalid_arguments_raise():
     from zero_amd._lib import ZeroAmdError
 
@@ -135,6 +189,8 @@ def test_invalid_arguments_raise():
     plan = Plan([4, 4], 2, 0)
     with pytest.raises(ZeroAmdError):
         plan.segments(5)
+    with pytest.raises(ZeroAmdError):
+        plan.bucket(5)
     with pytest.raises(ZeroAmdError):
         plan.owner_of(2)
 
