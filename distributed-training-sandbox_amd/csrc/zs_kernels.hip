@@ -268,6 +268,45 @@ __global__ __launch_bounds__(kThreads) void adam_segments_kernel(
   }
 }
 
+// ----------------------------------------------------------------------------------------------
+// in-place scale: x /= div (DDP's `param.grad /= world_size`, ddp.py:45-47)
+// ----------------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ float to_f32(T x) {
+  if constexpr (sizeof(T) == 4) return x;
+  else return bf16_to_f32(x);
+}
+template <typename T>
+__device__ __forceinline__ T from_f32(float x) {
+  if constexpr (sizeof(T) == 4) return x;
+  else return f32_to_bf16(x);
+}
+
+// 16 B per lane per access; the tail (n % (16/sizeof(T))) is done by the first lanes of block 0.
+// fp32: IEEE division (x / div), or an exact reciprocal multiply when div is a power of two;
+// bf16: the same in fp32, rounded to bf16 (RNE) — torch's div_ on a bf16 tensor.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void scale_kernel(T* __restrict__ x, int64_t n, float div,
+                                                         float inv, int pow2) {
+#pragma clang fp contract(off)
+  constexpr int V = 16 / sizeof(T);
+  const gptr<T> gx = glob(x);
+  const int64_t nv = n / V;
+  auto op = [&](float f) { return pow2 ? f * inv : f / div; };
+  for (int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x; i < nv;
+       i += int64_t(gridDim.x) * kThreads) {
+    uint4 raw = *reinterpret_cast<gptr<const uint4>>(gx + i * V);
+    T* e = reinterpret_cast<T*>(&raw);
+#pragma unroll
+    for (int j = 0; j < V; ++j) e[j] = from_f32<T>(op(to_f32<T>(e[j])));
+    *reinterpret_cast<gptr<uint4>>(gx + i * V) = raw;
+  }
+  if (blockIdx.x == 0) {
+    const int64_t i = nv * V + threadIdx.x;
+    if (i < n) gx[i] = from_f32<T>(op(to_f32<T>(gx[i])));
+  }
+}
+
 inline bool aligned(uint64_t p, uint64_t a) { return p % a == 0; }
 
 }  // namespace
@@ -354,6 +393,30 @@ int zs_copyset_destroy(zs_copyset* cs) {
   if (cs->d_segs) (void)hipFree(cs->d_segs);
   if (cs->d_prefix) (void)hipFree(cs->d_prefix);
   delete cs;
+  return ZS_OK;
+}
+
+int zs_scale(void* x, int64_t n, int dtype, double div, uintptr_t stream) {
+  ZS_REQUIRE(n >= 0, "zs_scale: n < 0");
+  ZS_REQUIRE(dtype == ZS_F32 || dtype == ZS_BF16, "zs_scale: bad dtype %d", dtype);
+  ZS_REQUIRE(div != 0.0, "zs_scale: div == 0");
+  if (n == 0) return ZS_OK;
+  ZS_REQUIRE(x != nullptr && aligned(reinterpret_cast<uint64_t>(x), 16),
+             "zs_scale: x must be non-NULL and 16-byte aligned");
+  int e = 0;
+  const int pow2 = std::frexp(div, &e) == 0.5 ? 1 : 0;
+  const float fdiv = float(div), inv = float(1.0 / div);
+  const int V = dtype == ZS_F32 ? 4 : 8;
+  const int64_t blocks = std::max<int64_t>(1, (n / V + kThreads - 1) / kThreads);
+  const int grid = int(std::min<int64_t>(blocks, grid_cap()));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == ZS_F32)
+    hipLaunchKernelGGL(scale_kernel<float>, dim3(grid), dim3(kThreads), 0, st,
+                       static_cast<float*>(x), n, fdiv, inv, pow2);
+  else
+    hipLaunchKernelGGL(scale_kernel<unsigned short>, dim3(grid), dim3(kThreads), 0, st,
+                       static_cast<unsigned short*>(x), n, fdiv, inv, pow2);
+  ZS_HIP(hipGetLastError());
   return ZS_OK;
 }
 

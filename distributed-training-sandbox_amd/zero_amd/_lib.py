@@ -27,7 +27,7 @@ EXPORTED = (
     "zs_plan_create", "zs_plan_destroy", "zs_plan_info", "zs_plan_owner_range", "zs_plan_owner_of",
     "zs_plan_stream_len", "zs_plan_num_pieces", "zs_plan_pieces", "zs_plan_bucket",
     "zs_plan_num_segments", "zs_plan_segments",
-    "zs_copyset_create", "zs_copyset_run", "zs_copyset_destroy",
+    "zs_copyset_create", "zs_copyset_run", "zs_copyset_destroy", "zs_scale",
     "zs_adam_hparams_init", "zs_adamset_create", "zs_adamset_run", "zs_adamset_destroy",
     "zs_adamset_stats",
     "zs_comm_unique_id", "zs_comm_init", "zs_comm_destroy", "zs_reduce_scatter", "zs_all_gather",
@@ -84,6 +84,7 @@ _SIGS = {
     "zs_copyset_create": ([_PU64, _PU64, _PI64, _I64, ctypes.POINTER(_P)], ctypes.c_int),
     "zs_copyset_run": ([_P, _U], ctypes.c_int),
     "zs_copyset_destroy": ([_P], ctypes.c_int),
+    "zs_scale": ([_P, _I64, ctypes.c_int, ctypes.c_double, _U], ctypes.c_int),
     "zs_adam_hparams_init": ([ctypes.c_double] * 5 + [ctypes.c_int] * 3 +
                              [_I64, ctypes.c_double, ctypes.c_double, ctypes.POINTER(AdamHParams)],
                              ctypes.c_int),

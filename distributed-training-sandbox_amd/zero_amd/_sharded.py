@@ -39,7 +39,8 @@ class ShardedOptimizerBase:
     _variant = 2
 
     def __init__(self, optimizer: Optimizer, *, layout: str = "reference",
-                 bucket_mb: float = 256.0, comm=None, sync: bool = True, buckets: str = "ragged"):
+                 bucket_mb: float = 256.0, comm=None, sync: bool = True, buckets: str = "ragged",
+                 overlap: bool = False, overlap_bucket_mb: float = 64.0):
         if not isinstance(optimizer, torch.optim.Adam):
             raise TypeError("zero_amd ShardedOptimizer wraps torch.optim.Adam / AdamW "
                             f"(got {type(optimizer).__name__})")
@@ -73,6 +74,14 @@ class ShardedOptimizerBase:
         self._sync = sync
         self.engine: ShardEngine | None = None
         self._step_tensors = {}
+        self._overlap = bool(overlap)
+        self._overlap_hooks = []
+        if self._overlap:
+            # hooks must exist before the first backward: build the engine (and the communicator,
+            # a collective call every rank makes here) now
+            self._build_engine()
+            gb = self.engine.enable_overlap(int(overlap_bucket_mb * (1 << 20)))
+            self._overlap_hooks = gb.register_hooks()
 
     def _shard_optimizer_params(self):
         """zero1.py:71-74: drop non-owned params from the inner optimizer's groups."""
@@ -154,10 +163,16 @@ class ShardedOptimizerBase:
     def _release_grads(self):
         # zero2.py:113 frees non-owned grads; the reduced grads live in the bucket arena, so
         # every grad is released (the next backward allocates fresh ones).
+        if self._overlap:
+            self.engine.gb.release()
+            return
         for p in self.params:
             p.grad = None
 
     def zero_grad(self, set_to_none: bool = True):
+        if self._overlap:  # grads become zeroed views of the overlap buckets (no pack copy)
+            self.engine.gb.install_views()
+            return
         for p in self.params:
             if p.grad is not None:
                 if set_to_none:

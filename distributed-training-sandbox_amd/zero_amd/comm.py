@@ -86,6 +86,15 @@ class RcclComm:
         _lib.call("zs_all_gather", self._h, send.data_ptr(), recv.data_ptr(), send.numel(),
                   zs_dtype(send.dtype), stream_handle(stream))
 
+    def reduce(self, t: torch.Tensor, root: int, stream) -> None:
+        """SUM-reduce ``t`` onto ``root`` in place (ZeRO overlap buckets: one owner each)."""
+        _lib.call("zs_reduce", self._h, t.data_ptr(), t.data_ptr(), t.numel(), zs_dtype(t.dtype),
+                  int(root), stream_handle(stream))
+
+    def broadcast(self, t: torch.Tensor, root: int, stream) -> None:
+        _lib.call("zs_broadcast", self._h, t.data_ptr(), t.data_ptr(), t.numel(),
+                  zs_dtype(t.dtype), int(root), stream_handle(stream))
+
     def reduce_v(self, buf: torch.Tensor, win_off, win_len, stream) -> None:
         """Reduce-scatter-v in place: window r of ``buf`` (offset win_off[r], win_len[r] elements)
         is SUM-reduced onto rank r — one ncclReduce per owner, launched as one RCCL group."""

@@ -92,9 +92,8 @@ class ShardEngine:
             self.master = torch.zeros(self.L, **f32)
             for i, po, so, n in zip(*self._piece_cols()):
                 self.master[so:so + n].copy_(params[i].detach().reshape(-1)[po:po + n])
-        self.arena = None
+        self.arena = None  # allocated on the first bucketed step (not at all in overlap mode)
         if ws > 1:
-            self.arena = torch.zeros(self.plan.arena_elems, dtype=dtype, device=dev)
             self.buckets = [self.plan.bucket(k) for k in range(self.K)]
             self.segs = [self.plan.segments(k) for k in range(self.K)]
             self.comm_stream = torch.cuda.Stream(device=dev)
@@ -199,13 +198,21 @@ class ShardEngine:
         n = len(self.params)
         has = np.fromiter((g is not None for g in grads), bool, n)
         gptr = np.fromiter((_ptr(g) for g in grads), np.uint64, n)
+        gb = getattr(self, "gb", None)
+        if gb is not None and gb.views_installed:  # a zeroed view no backward touched = no grad
+            base = gb.buf.data_ptr()
+            is_view = np.fromiter((g is not None and g.data_ptr() == base + int(gb.slot[i]) * self.es
+                                   for i, g in enumerate(grads)), bool, n)
+            has &= gb.marked | ~is_view
         if any(hparams_of(g)["amsgrad"] for g in set(self.group_of)):
             self.ensure_vmax()
         owned = np.zeros(n, bool)
         owned[self.owned_param_indices()] = True
         self.steps[owned & has] += 1
         self.last_adam_bytes = 0
-        if self.ws == 1:
+        if getattr(self, "gb", None) is not None:
+            self._step_overlap(has, hparams_of, stream)
+        elif self.ws == 1:
             self._step_local(gptr, has, hparams_of, stream)
         else:
             self._step_buckets(gptr, has, hparams_of, stream)
@@ -255,6 +262,8 @@ class ShardEngine:
             self.comm_events.append((kind, bool(b.even), e0, e1, bus))
 
     def _step_buckets(self, gptr, has, hparams_of, stream):
+        if self.arena is None:
+            self.arena = torch.zeros(self.plan.arena_elems, dtype=self.dtype, device=self.device)
         es = np.uint64(self.es)
         pptr = np.fromiter((_ptr(p) for p in self.params), np.uint64, len(self.params))
         base = np.uint64(self.arena.data_ptr())
@@ -309,6 +318,91 @@ class ShardEngine:
             dst = pptr[s.param] + s.param_off.astype(np.uint64) * es
             self._cached(("unpack", k), dst.tobytes(),
                          lambda: CopySet(src, dst, s.length * self.es)).run(stream)
+
+    # ------------------------------------------------------------------------------------------
+    # backward-overlapped mode: grads reduced to their owner from
+    # post-accumulate-grad hooks while backward runs; step() = Adam + broadcast + unpack.
+    def enable_overlap(self, bucket_bytes: int):
+        from .overlap import GradBuckets
+
+        if self.plan.layout != 0:
+            raise ValueError("backward overlap needs the reference (owner-by-index) layout")
+        if self.ws > 1 and not hasattr(self.comm, "reduce"):
+            raise ValueError("backward overlap needs a communicator with reduce / broadcast")
+        owner = [self.plan.owner_of(i) for i in range(len(self.params))]
+        self.gb = GradBuckets(self.params, owner, bucket_bytes, self._overlap_reduce)
+        pc = self.pieces
+        self._so_of = {int(i): int(so) for i, so, n in zip(pc.param, pc.stream_off, pc.length)}
+        mk = lambda: [torch.cuda.Event() for _ in range(self.gb.K)]  # noqa: E731
+        self.ev_oadam, self.ev_obc = mk(), mk()
+        return self.gb
+
+    def _overlap_reduce(self, k, region, cs):
+        if self.ws == 1:
+            return
+        if self.comm_events is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(cs)
+        self.comm.reduce(region, self.gb.key[k], cs)
+        if self.comm_events is not None:
+            e1.record(cs)
+            self.comm_events.append(("rs", False, e0, e1, region.numel() * self.es))
+
+    def _step_overlap(self, has, hparams_of, stream):
+        gb, r, es = self.gb, self.rank, np.uint64(self.es)
+        gb.flush()
+        cs = gb.comm_stream
+        base = np.uint64(gb.buf.data_ptr())
+        for k in range(gb.K):  # fused Adam on the owned buckets, reading the reduced grads
+            if gb.key[k] != r:
+                continue
+            stream.wait_event(gb.ev_done[k])
+            idx = np.array([i for i in gb.groups[k] if has[i]], np.int64)
+            if len(idx):
+                slot = base + gb.slot[idx].astype(np.uint64) * es
+                so = np.array([self._so_of[int(i)] for i in idx], np.int64)
+                ln = np.array([self.params[int(i)].numel() for i in idx], np.int64)
+                if self.mixed:
+                    mst = np.uint64(self.master.data_ptr()) + so.astype(np.uint64) * np.uint64(4)
+                    rows = self._adam_rows(idx, slot, mst, mst, slot, so, ln)
+                else:
+                    p = np.fromiter((_ptr(self.params[int(i)]) for i in idx), np.uint64, len(idx))
+                    rows = self._adam_rows(idx, slot, p, slot, 0, so, ln)
+                self._run_adam(("overlap", k), rows, idx, hparams_of, stream)
+            dead = [i for i in gb.groups[k] if not has[i]]
+            if dead:  # params without a grad keep their value: copy it into the slot
+                src = [_ptr(self.params[i]) for i in dead]
+                dst = [int(base) + int(gb.slot[i]) * self.es for i in dead]
+                self._cached(("opass", k), np.array(src + dst, np.uint64).tobytes(),
+                             lambda: CopySet(src, dst, [self.params[i].numel() * self.es
+                                                        for i in dead])).run(stream)
+            self.ev_oadam[k].record(stream)
+        if self.ws > 1:
+            self.ev_c0.record(cs)
+            for k in range(gb.K):  # every rank, same order: broadcast each bucket from its owner
+                cs.wait_event(self.ev_oadam[k] if gb.key[k] == r else gb.ev_done[k])
+                region = gb.region(k)
+                if self.comm_events is not None:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(cs)
+                self.comm.broadcast(region, gb.key[k], cs)
+                if self.comm_events is not None:
+                    e1.record(cs)
+                    self.comm_events.append(("ag", False, e0, e1, region.numel() * self.es))
+                self.ev_obc[k].record(cs)
+            self.ev_c1.record(cs)
+        for k in range(gb.K):  # unpack updated params into module storage
+            if self.ws > 1:
+                stream.wait_event(self.ev_obc[k])
+            elif gb.key[k] != r:
+                continue
+            g = gb.groups[k]
+            src = [int(base) + int(gb.slot[i]) * self.es for i in g]
+            dst = [_ptr(self.params[i]) for i in g]
+            self._cached(("ounpack", k), np.array(dst, np.uint64).tobytes(),
+                         lambda: CopySet(src, dst, [self.params[i].numel() * self.es
+                                                    for i in g])).run(stream)
+        gb.reset()
 
     def comm_time_s(self) -> float:
         """Seconds between the first reduce-scatter and the last all-gather of the last step

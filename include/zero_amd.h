@@ -116,6 +116,12 @@ int zs_copyset_create(const uint64_t* src, const uint64_t* dst, const int64_t* n
 int zs_copyset_run(const zs_copyset* cs, uintptr_t stream);
 int zs_copyset_destroy(zs_copyset* cs);
 
+/* In-place x[i] /= div over n elements (dtype ZS_F32 / ZS_BF16, x 16-byte aligned): the
+ * `param.grad /= dist.get_world_size()` of DDP's sync_gradients (DDP/ddp.py:45-47), applied to a
+ * whole all-reduced gradient bucket.  fp32: IEEE division (reciprocal multiply when div is a power
+ * of two, which is exact); bf16: computed in fp32, rounded to nearest even. */
+int zs_scale(void* x, int64_t n, int dtype, double div, uintptr_t stream);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Fused Adam / AdamW.  Replaces torch.optim.Adam.step on the owned shard (zero1.py:88,          */
 /* zero2.py:120, zero3.py:161; math of torch/optim/adam.py:457-547) plus the grad averaging     */

@@ -39,6 +39,30 @@ class GlooStagedComm:
             recv.copy_(out.to(recv.device))
         self.calls.append(("ag", recv.numel()))
 
+    def _root(self, root):
+        return dist.get_global_rank(self.group, root) if self.group else root
+
+    def reduce(self, t, root, stream):
+        stream.synchronize()
+        h = t.detach().to("cpu", torch.float32)
+        dist.reduce(h, dst=self._root(root), group=self.group)
+        if root == self.rank:
+            with torch.cuda.stream(stream):
+                t.copy_(h.to(t.device).to(t.dtype))
+        self.calls.append(("reduce", t.numel()))
+
+    def broadcast(self, t, root, stream):
+        stream.synchronize()
+        h = t.detach().to("cpu")
+        if h.dtype == torch.bfloat16:
+            h = h.view(torch.int16)
+        dist.broadcast(h, src=self._root(root), group=self.group)
+        if t.dtype == torch.bfloat16:
+            h = h.view(torch.bfloat16)
+        with torch.cuda.stream(stream):
+            t.copy_(h.to(t.device))
+        self.calls.append(("bcast", t.numel()))
+
     def reduce_v(self, buf, win_off, win_len, stream):
         stream.synchronize()
         h = buf.detach().to("cpu", torch.float32)

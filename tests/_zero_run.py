@@ -69,3 +69,41 @@ def run_injected(z, variant: int, rank: int, ws: int, device, comm=None, window_
             assert rel(st["exp_avg_sq"].cpu().numpy(), z[f"r{rank}_state_{i}_exp_avg_sq"]) <= tol
     assert opt.local_param_indices == z[f"r{rank}_local"].tolist()
     return worst
+
+
+def run_backward(z, variant: int, rank: int, ws: int, device, comm=None, tol=1e-6, overlap=True,
+                 views=True, bucket_mb=None):
+    """Like run_injected, but the fixture's grads arrive through a real backward pass
+    (loss = Σ_i <p_i, G_i>, so p_i.grad == G_i exactly), which fires the post-accumulate-grad
+    hooks of the backward-overlapped mode.  ``views``: zero_grad() installs bucket views
+    (autograd accumulates in place); otherwise grads are set to None and copied into the buckets."""
+    mod = module_for(variant)
+    steps = int(z["steps"])
+    params = [torch.nn.Parameter(torch.from_numpy(z[f"init_{i}"].copy()).to(device)) for i in range(12)]
+    kw = dict(overlap=overlap)
+    if bucket_mb is not None:
+        kw["overlap_bucket_mb"] = bucket_mb
+    if comm is not None:
+        kw["comm"] = comm
+    opt = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), **kw)
+    for t in range(steps):
+        if views:
+            opt.zero_grad()
+        else:
+            for p in params:
+                p.grad = None
+        gs = [torch.from_numpy(z[f"r{rank}_t{t}_lg{i}"].copy()).to(device) for i in range(12)]
+        loss = sum((p * g).sum() for p, g in zip(params, gs))
+        loss.backward()
+        opt.step()
+        if f"r{rank}_t{t}_p0" in z.files:
+            for i, p in enumerate(params):
+                e = rel(p.detach().cpu().numpy(), z[f"r{rank}_t{t}_p{i}"])
+                assert e <= tol, (variant, ws, rank, t, i, e)
+    for i, p in enumerate(params):
+        key = f"r{rank}_state_{i}_exp_avg"
+        if key in z.files:
+            st = opt.optimizer.state[p]
+            assert int(st["step"].item()) == int(z[f"r{rank}_state_{i}_step"])
+            assert rel(st["exp_avg"].cpu().numpy(), z[key]) <= tol
+    return opt

@@ -1,0 +1,198 @@
+"""Backward-overlapped gradient buckets (overlap.py) on the MI355X: ZeRO-1/2 with per-owner
+reduces launched from post-accumulate-grad hooks, and the DDP drop-in's bucketed all-reduce.
+
+ZeRO: the reference trajectories (tests/golden) are replayed through a real backward pass
+(loss = Σ <p_i, G_i>, so p_i.grad == G_i bit-for-bit) at 1e-6 normwise, every step.  Multi-rank
+cases share the one GPU through the test-only gloo-staged communicator, as in test_gpu_parity.
+DDP: every rank's averaged grads against numpy (sum over ranks in rank order, then / ws).
+"""
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN
+from _zero_run import init_pg, run_backward
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture
+def pg1():
+    init_pg(0, 1, _port())
+    yield
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("views", [True, False])
+def test_ws1_overlap_backward(gpu, golden, pg1, variant, views):
+    z = golden(f"traj_z{variant}_ws1_d16_distinct.npz")
+    opt = run_backward(z, variant, 0, 1, gpu, views=views, bucket_mb=2e-3)
+    assert opt.engine.gb.K > 1 and opt.engine.gb.launched_in_backward > 0
+
+
+def test_overlap_bf16_matches_bucket_engine(gpu, pg1):
+    """bf16 params + fp32 master: the overlap path and the bucketed path give identical bits."""
+    from zero_amd import zero2
+
+    g = torch.Generator().manual_seed(3)
+    shapes = [(96, 40), (40,), (33, 7), (7,), (128, 64), (64,)]
+    init = [(torch.randn(s, generator=g) * 0.02).to(torch.bfloat16) for s in shapes]
+    grads = [[(torch.randn(s, generator=g) * 1e-3).to(torch.bfloat16) for s in shapes] for _ in range(3)]
+    out = []
+    for overlap in (False, True):
+        ps = [torch.nn.Parameter(t.clone().to(gpu)) for t in init]
+        opt = zero2.ShardedOptimizer(torch.optim.Adam(ps, lr=1e-3), overlap=overlap,
+                                     overlap_bucket_mb=0.01)
+        for gs in grads:
+            opt.zero_grad()
+            loss = sum((p.float() * gg.to(gpu).float()).sum() for p, gg in zip(ps, gs))
+            loss.backward()
+            opt.step()
+        out.append([p.detach().cpu().view(torch.int16) for p in ps])
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+
+
+def test_overlap_unused_param_keeps_value(gpu, pg1):
+    """A parameter no backward touches has no grad: Adam skips it (the reference's None grad)."""
+    from zero_amd import zero2
+
+    ps = [torch.nn.Parameter(torch.randn(64, 8, device=gpu)) for _ in range(3)]
+    before = ps[1].detach().clone()
+    before0 = ps[0].detach().clone()
+    opt = zero2.ShardedOptimizer(torch.optim.Adam(ps, lr=1e-2), overlap=True, overlap_bucket_mb=1e-3)
+    opt.zero_grad()
+    (ps[0].sum() + ps[2].sum()).backward()
+    opt.step()
+    assert torch.equal(ps[1].detach(), before)
+    assert not torch.equal(ps[0].detach(), before0)
+    assert "exp_avg" in opt.optimizer.state[ps[0]]
+
+
+def test_overlap_double_backward_raises(gpu, pg1):
+    from zero_amd import zero2
+
+    ps = [torch.nn.Parameter(torch.randn(64, device=gpu))]
+    opt = zero2.ShardedOptimizer(torch.optim.Adam(ps, lr=1e-3), overlap=True)
+    opt.zero_grad()
+    ps[0].sum().backward()
+    with pytest.raises(RuntimeError, match="accumulated twice"):
+        ps[0].sum().backward()
+
+
+def _mr_worker(rank, ws, port, variant, name, views):
+    import sys
+    from conftest import PKG, REPO  # noqa: F401
+    from _gloo_comm import GlooStagedComm
+
+    torch.cuda.set_device(0)
+    init_pg(rank, ws, port)
+    z = np.load(GOLDEN / name)
+    run_backward(z, variant, rank, ws, torch.device("cuda:0"), comm=GlooStagedComm(), views=views,
+                 bucket_mb=2e-3)
+    dist.barrier()
+    dist.destroy_process_group()
+    sys.stdout.flush()
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("ws,views", [(2, True), (3, True), (3, False)])
+def test_multirank_overlap_backward(gpu, variant, ws, views):
+    name = f"traj_z{variant}_ws{ws}_d16_distinct.npz"
+    mp.spawn(_mr_worker, args=(ws, _port(), variant, name, views), nprocs=ws, join=True)
+
+
+# ---------------------------------------------------------------------------------------------
+# DDP
+def _ddp_grads(ws, shapes, step):
+    g = torch.Generator().manual_seed(1000 + step)
+    return [[torch.randn(s, generator=g) for s in shapes] for _ in range(ws)]
+
+
+def _ddp_worker(rank, ws, port, dtype_name):
+    import sys
+    from conftest import PKG, REPO  # noqa: F401
+    from _gloo_comm import GlooStagedComm
+    from zero_amd.ddp import SimpleDistributedDataParallelism
+
+    torch.cuda.set_device(0)
+    init_pg(rank, ws, port)
+    dev = torch.device("cuda:0")
+    dt = getattr(torch, dtype_name)
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(40, 24), torch.nn.ReLU(), torch.nn.Linear(24, 8),
+                                torch.nn.Linear(8, 8)).to(dev).to(dt)
+    ddp = SimpleDistributedDataParallelism(model, bucket_mb=1e-3,
+                                           comm=GlooStagedComm() if ws > 1 else None)
+    shapes = [tuple(p.shape) for p in model.parameters()]
+    for step in range(3):
+        allg = _ddp_grads(ws, shapes, step)
+        if step == 1:
+            ddp.zero_grad()          # views: autograd accumulates in place
+        else:
+            model.zero_grad(set_to_none=True)
+        used = list(model.parameters())[:4]  # the last Linear gets no gradient
+        loss = sum((p.float() * g.to(dev).to(dt).float()).sum() for p, g in zip(used, allg[rank]))
+        loss.backward()
+        ddp.sync_gradients()
+        torch.cuda.synchronize()
+        for i, p in enumerate(model.parameters()):
+            if i >= 4:
+                assert p.grad is None
+                continue
+            acc = np.zeros(shapes[i], np.float32)
+            for r in range(ws):  # the staged comm sums in fp32 in rank order
+                acc = acc + allg[r][i].to(dt).float().numpy()
+            if dt == torch.float32:
+                want = acc / np.float32(ws)
+                got = p.grad.cpu().numpy()
+            else:  # sum rounded to bf16 once, then / ws in fp32 rounded to bf16
+                want = (torch.from_numpy(acc).to(torch.bfloat16).float() / ws).to(torch.bfloat16).float().numpy()
+                got = p.grad.cpu().float().numpy()
+            if ws <= 2:  # a two-term sum is order-free: bit-exact
+                assert np.array_equal(got, want), (rank, step, i)
+            else:  # gloo's ring may add in another order
+                tol = 1e-6 if dt == torch.float32 else 2.0 ** -7
+                assert np.max(np.abs(got - want)) <= tol * np.max(np.abs(want)), (rank, step, i)
+    dist.barrier()
+    dist.destroy_process_group()
+    sys.stdout.flush()
+
+
+@pytest.mark.parametrize("ws", [1, 2, 3])
+@pytest.mark.parametrize("dtype_name", ["float32", "bfloat16"])
+def test_ddp_sync_gradients(gpu, ws, dtype_name):
+    mp.spawn(_ddp_worker, args=(ws, _port(), dtype_name), nprocs=ws, join=True)
+
+
+@pytest.mark.parametrize("n", [1, 7, 1000, 4099, 1 << 20])
+@pytest.mark.parametrize("div", [2.0, 3.0, 8.0, 6.0])
+def test_scale_kernel_bit_exact(gpu, n, div):
+    from zero_amd import _lib
+    from zero_amd.comm import zs_dtype
+
+    g = torch.Generator().manual_seed(n)
+    x = torch.randn(n, generator=g) * 10
+    for dt in (torch.float32, torch.bfloat16):
+        d = x.to(dt).to(gpu)
+        _lib.call("zs_scale", d.data_ptr(), n, zs_dtype(dt), div, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        if dt == torch.float32:
+            want = x.numpy() / np.float32(div)
+            assert np.array_equal(d.cpu().numpy(), want)
+        else:
+            want = (x.to(dt).float() / div).to(dt)
+            assert torch.equal(d.cpu(), want)

@@ -201,3 +201,25 @@ def test_empty_and_tiny():
     plan = Plan([3], 4, 3)  # ws > n: ranks 1..3 own nothing
     assert plan.owner_range(3) == (1, 1) and plan.stream_len(3) == 0
     assert plan.owner_of(0) == 0
+
+
+def test_grad_bucket_grouping():
+    """overlap.plan_grad_buckets: reverse order, size cap, no key mixing, aligned disjoint slots."""
+    from zero_amd.overlap import plan_grad_buckets
+
+    rng = np.random.default_rng(0)
+    numels = [int(x) for x in rng.integers(1, 5000, 40)] + [100000]
+    keys = sorted(int(k) for k in rng.integers(0, 4, len(numels)))
+    groups, bkeys, slot, bucket_of, boff, blen = plan_grad_buckets(numels, keys, 4 * 8192, 4)
+    flat = [i for g in groups for i in g]
+    assert flat == list(range(len(numels)))[::-1]
+    for k, g in enumerate(groups):
+        assert len({keys[i] for i in g}) == 1 and bkeys[k] == keys[g[0]]
+        assert blen[k] <= 8192 or len(g) == 1
+        for i in g:
+            assert bucket_of[i] == k and slot[i] % 64 == 0
+            assert boff[k] <= slot[i] and slot[i] + numels[i] <= boff[k] + blen[k]
+    ends = sorted((slot[i], slot[i] + numels[i]) for i in range(len(numels)))
+    assert all(a[1] <= b[0] for a, b in zip(ends, ends[1:]))
+    with pytest.raises(ValueError):
+        plan_grad_buckets([1, 2], [0, 0], 64, 4, order=[0, 0])
