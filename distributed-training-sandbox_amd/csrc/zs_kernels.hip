@@ -34,7 +34,9 @@ int grid_cap() {
       if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
         cus = prop.multiProcessorCount;
     }
-    cap = cus * 32;  // ~4x the resident workgroups: measured best for these streaming kernels
+    // 128 workgroups per CU (16x the resident 8): the best of 32/64/128/512/one-per-chunk for the
+    // Adam and copy kernels at C4 scale (profiles/r01_adam_variants2.log)
+    cap = cus * 128;
   }
   return cap;
 }
@@ -51,6 +53,30 @@ using gptr = T*;
 template <typename T>
 __device__ __forceinline__ gptr<T> glob(T* p) {
   return (gptr<T>)p;
+}
+
+// Streaming accesses carry the non-temporal hint (global_load/store ... nt): nothing these kernels
+// touch is re-read while it could still be cached, and at C4 scale (86 GB per Adam launch) the hint
+// measured +4-6 % over plain accesses, loads and stores alike (profiles/r01_adam_variants2.log).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint4 nt_ld16(const void* p) {
+  const u32x4 v = __builtin_nontemporal_load((gptr<const u32x4>)p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void nt_st16(void* p, uint4 x) {
+  const u32x4 v = {x.x, x.y, x.z, x.w};
+  __builtin_nontemporal_store(v, (gptr<u32x4>)p);
+}
+__device__ __forceinline__ uint2 nt_ld8(const void* p) {
+  const u32x2 v = __builtin_nontemporal_load((gptr<const u32x2>)p);
+  return make_uint2(v.x, v.y);
+}
+__device__ __forceinline__ void nt_st8(void* p, uint2 x) {
+  const u32x2 v = {x.x, x.y};
+  __builtin_nontemporal_store(v, (gptr<u32x2>)p);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -80,13 +106,13 @@ __global__ __launch_bounds__(kThreads) void copy_segments_kernel(
       for (int u = 0; u < 4; ++u) {  // all loads first: 4 x 16 B in flight per lane
         const int64_t off = b0 + (int64_t(u) * kThreads + threadIdx.x) * 16;
         val[u] = make_uint4(0, 0, 0, 0);
-        if (src && off + 16 <= b1) val[u] = *reinterpret_cast<gptr<const uint4>>(src + off);
+        if (src && off + 16 <= b1) val[u] = nt_ld16(s.src + off);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t off = b0 + (int64_t(u) * kThreads + threadIdx.x) * 16;
         if (off + 16 <= b1) {
-          *reinterpret_cast<gptr<uint4>>(dst + off) = val[u];
+          nt_st16(s.dst + off, val[u]);
         } else if (off < b1) {
           for (int64_t b = off; b < b1; ++b) dst[b] = src ? src[b] : 0;
         }
@@ -188,23 +214,25 @@ __global__ __launch_bounds__(kThreads) void adam_scalar_kernel(
   }
 }
 
+__device__ __forceinline__ float4 ld4(const float* p, int64_t i) {
+  const uint4 r = nt_ld16(p + i);
+  return make_float4(__uint_as_float(r.x), __uint_as_float(r.y), __uint_as_float(r.z),
+                     __uint_as_float(r.w));
+}
+__device__ __forceinline__ void st4(float* p, int64_t i, float4 x) {
+  nt_st16(p + i, make_uint4(__float_as_uint(x.x), __float_as_uint(x.y), __float_as_uint(x.z),
+                            __float_as_uint(x.w)));
+}
+
 template <typename GT>
 __device__ __forceinline__ float4 load_g4(const void* g, int64_t i) {
   if constexpr (sizeof(GT) == 4) {
-    return *reinterpret_cast<gptr<const float4>>(glob(static_cast<const float*>(g)) + i);
+    return ld4(static_cast<const float*>(g), i);
   } else {
-    const uint2 r =
-        *reinterpret_cast<gptr<const uint2>>(glob(static_cast<const unsigned short*>(g)) + i);
+    const uint2 r = nt_ld8(static_cast<const unsigned short*>(g) + i);
     return make_float4(__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u),
                        __uint_as_float(r.y << 16), __uint_as_float(r.y & 0xffff0000u));
   }
-}
-
-__device__ __forceinline__ float4 ld4(const float* p, int64_t i) {
-  return *reinterpret_cast<gptr<const float4>>(glob(p) + i);
-}
-__device__ __forceinline__ void st4(float* p, int64_t i, float4 x) {
-  *reinterpret_cast<gptr<float4>>(glob(p) + i) = x;
 }
 
 // Vector kernel: every segment 16-B aligned (8-B for bf16 arrays) with n % 4 == 0 (the host
@@ -257,7 +285,7 @@ __global__ __launch_bounds__(kThreads) void adam_segments_kernel(
           uint2 r;
           r.x = uint32_t(f32_to_bf16(pp[0])) | (uint32_t(f32_to_bf16(pp[1])) << 16);
           r.y = uint32_t(f32_to_bf16(pp[2])) | (uint32_t(f32_to_bf16(pp[3])) << 16);
-          *reinterpret_cast<gptr<uint2>>(glob(s.p_out) + i) = r;
+          nt_st8(s.p_out + i, r);
         }
         st4(s.m, i, m4[u]);
         st4(s.v, i, v4[u]);
