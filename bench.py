@@ -104,6 +104,30 @@ def collective_summary(events, steps, world, red_dev):
     return out
 
 
+def copy_summary(events, steps, world, red_dev):
+    """Pack / unpack (copy_segments_kernel) achieved HBM bandwidth: algorithmic bytes (read + write
+    of every byte moved) / kernel time from HIP events on the compute stream, slowest rank."""
+    import torch
+    import torch.distributed as dist
+
+    out = {}
+    for kind in ("pack", "unpack"):
+        ev = [(e0, e1, b) for k, e0, e1, b in events if k == kind]
+        if not ev:
+            continue
+        ms = sum(e0.elapsed_time(e1) for e0, e1, _ in ev)
+        nbytes = sum(b for _, _, b in ev)
+        t = torch.tensor([ms], dtype=torch.float64, device=red_dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+        gbs = nbytes / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+        out[kind] = {"kernel": "copy_segments_kernel", "launches_per_step": len(ev) / steps,
+                     "ms_per_step": ms / steps, "alg_gb_per_step": nbytes / steps / 1e9,
+                     "achieved_gbs": gbs, "frac": gbs / HBM_PEAK_GBS}
+    return out
+
+
 def comm_sweep(comm, arena, world, red_dev, sizes_mb=(4, 16, 64, 256), iters=5):
     """Bucket-size sweep of in-place RCCL reduce-scatter / all-gather on the bf16 arena (the C5
     sweep of BASELINE.json, run on whatever N the bench runs): busBW = bytes*(ws-1)/ws / time."""
@@ -257,6 +281,7 @@ def main():
     eng = opt.engine
     eng.timing_events = []
     eng.comm_events = [] if world > 1 or args.simulate_ws > 1 else None
+    eng.copy_events = [] if world > 1 or args.simulate_ws > 1 else None
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -268,6 +293,7 @@ def main():
     eng_events = eng.timing_events
     eng.timing_events = None
     comm_events, eng.comm_events = eng.comm_events, None
+    copy_events, eng.copy_events = eng.copy_events, None
     red_dev = dev if use_nccl else "cpu"
     el_t = torch.tensor([el], dtype=torch.float64, device=red_dev)
     if world > 1:
@@ -296,6 +322,7 @@ def main():
             traffic = d.get("hbm_bytes_per_launch")
             traffic_src = str(tj.relative_to(REPO) if tj.is_absolute() else tj)
 
+    copy_kernels = copy_summary(copy_events, args.steps, world, red_dev) if copy_events else None
     collectives = None
     if world > 1:
         collectives = collective_summary(comm_events, args.steps, world, red_dev)
@@ -307,7 +334,8 @@ def main():
                           "bucket path, collectives skipped (NOT the metric)",
                           "ms_per_step": ms, "adam_achieved_gbs": achieved,
                           "adam_ms_per_step": adam_ms / args.steps, "buckets": eng.K,
-                          "window_elems": eng.W, "stream_elems": eng.L}), flush=True)
+                          "window_elems": eng.W, "stream_elems": eng.L,
+                          "copy_kernels": copy_kernels}), flush=True)
         dist.destroy_process_group()
         return
     if rank == 0:
@@ -345,6 +373,8 @@ def main():
         }
         if collectives is not None:
             out["collectives"] = collectives
+        if copy_kernels is not None:
+            out["copy_kernels"] = copy_kernels
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(shapes, args.cpu_sample)
         print(json.dumps(out), flush=True)

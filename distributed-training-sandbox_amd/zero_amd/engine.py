@@ -105,6 +105,7 @@ class ShardEngine:
         self._cache = {}
         self.timing_events = None  # optional list of (start, end) events around each Adam launch
         self.comm_events = None    # optional list of (kind, even, start, end, bus_bytes) per collective
+        self.copy_events = None    # optional list of (kind, start, end, bytes) per pack / unpack
         self.last_adam_bytes = 0
 
     # ------------------------------------------------------------------------------------------
@@ -232,6 +233,18 @@ class ShardEngine:
             rows = self._adam_rows(idx, g, p, p, 0, so, n)
         self._run_adam("local", rows, idx, hparams_of, stream)
 
+    def _run_copy(self, kind, cs, stream):
+        """Launch a pack / unpack CopySet; with timing on, bracket it with HIP events (algorithmic
+        bytes = read + write of every byte moved)."""
+        if self.copy_events is None:
+            cs.run(stream)
+            return
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        cs.run(stream)
+        e1.record(stream)
+        self.copy_events.append((kind, e0, e1, 2 * cs.nbytes))
+
     def _bucket_buf(self, k):
         b = self.buckets[k]
         return b, self.arena[b.arena_off:b.arena_off + b.elems]
@@ -276,7 +289,8 @@ class ShardEngine:
             dst = base + np.uint64(b.arena_off) * es + s.buf_off.astype(np.uint64) * es
             nb = s.length * self.es
             sig = src.tobytes() + dst.tobytes()
-            self._cached(("pack", k), sig, lambda: CopySet(src, dst, nb)).run(stream)
+            self._run_copy("pack", self._cached(("pack", k), sig, lambda: CopySet(src, dst, nb)),
+                           stream)
             self.ev_pack[k].record(stream)
         for k in range(self.K):  # in-place reduce-scatter (-v) of each bucket
             cs.wait_event(self.ev_pack[k])
@@ -316,8 +330,9 @@ class ShardEngine:
             s, b = self.segs[k], self.buckets[k]
             src = base + np.uint64(b.arena_off) * es + s.buf_off.astype(np.uint64) * es
             dst = pptr[s.param] + s.param_off.astype(np.uint64) * es
-            self._cached(("unpack", k), dst.tobytes(),
-                         lambda: CopySet(src, dst, s.length * self.es)).run(stream)
+            self._run_copy("unpack", self._cached(("unpack", k), dst.tobytes(),
+                                                  lambda: CopySet(src, dst, s.length * self.es)),
+                           stream)
 
     # ------------------------------------------------------------------------------------------
     # backward-overlapped mode: grads reduced to their owner from
