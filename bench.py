@@ -190,13 +190,96 @@ class _NoComm:
         pass
 
 
+def bench_zero3(args, world, rank, dev, use_nccl):
+    """ZeRO-3 (BASELINE.json configs[2]): one step = one training iteration of the reference
+    harness loop (zero3.py:171-258: zero_grad → forward → MSE → backward → step) on the
+    6×Linear(D,D)+ReLU MLP, with every parameter dim-0 sharded, the hooks' all-gathers grouped per
+    module and prefetched on a side stream, and update-mode step() = grouped reduce-scatter of the
+    full grads + fused Adam on the local chunks.  value = params / iteration time."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from zero_amd import zero3
+    from zero_amd.shapes import CONFIGS
+
+    if args.config not in ("C2", "C3"):
+        raise SystemExit("--zero 3 runs the MLP configs C2 / C3")
+    D = CONFIGS[args.config][1]()[0][0]
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    torch.manual_seed(0)
+    layers = []
+    for i in range(6):
+        layers += [torch.nn.Linear(D, D, device=dev, dtype=dt)] + ([torch.nn.ReLU()] if i < 5 else [])
+    model = torch.nn.Sequential(*layers)
+    total = sum(p.numel() for p in model.parameters())
+    g = torch.Generator(device=dev).manual_seed(42)  # identical data on every rank (zero3.py:186)
+    x = torch.randn(args.batch, D, device=dev, generator=g).to(dt)
+    y = torch.randn(args.batch, D, device=dev, generator=g).to(dt)
+    opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
+                                 sync=False)
+    zero3.register_zero3_hooks(model, opt.param_managers)
+
+    def step():
+        opt.zero_grad()
+        loss = torch.nn.functional.mse_loss(model(x), y)
+        loss.backward()
+        opt.step()
+
+    for _ in range(args.warmup):
+        step()
+    opt.timing_events = []
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    ev, opt.timing_events = opt.timing_events, None
+    red_dev = dev if use_nccl else "cpu"
+    adam_ms = sum(a.elapsed_time(b) for a, b, _ in ev)
+    adam_bytes = sum(nb for _, _, nb in ev)
+    achieved = adam_bytes / (adam_ms / 1e3) / 1e9 if adam_ms > 0 else 0.0
+    t = torch.tensor([el, -achieved], dtype=torch.float64, device=red_dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)  # slowest rank's time and Adam bandwidth
+    el, achieved = float(t[0]), -float(t[1])
+    ms = el / args.steps * 1e3
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": total / (ms / 1e3), "unit": "params/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic",
+            "config": {"workload": f"{args.config} ZeRO-3 training iteration of the reference MLP "
+                                   f"6xLinear({D},{D})+ReLU (hooked all-gathers, update-mode step)",
+                       "params": int(total), "batch": args.batch, "param_dtype": args.dtype,
+                       "zero": 3, "parallelism": f"dp{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "adam_segments_kernel",
+                         "avg_launch_ms": adam_ms / max(len(ev), 1),
+                         "alg_bytes_per_launch": adam_bytes / max(len(ev), 1),
+                         "launches_per_step": len(ev) / args.steps},
+            "zero3": {"gathers_per_step": opt.runtime.n_gathers / (args.steps + args.warmup),
+                      "prefetch_hits": opt.runtime.n_prefetch_hits},
+        }
+        print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C4", choices=["C2", "C3", "C4", "C5"])
-    ap.add_argument("--zero", type=int, default=2, choices=[1, 2])
+    ap.add_argument("--zero", type=int, default=2, choices=[1, 2, 3],
+                    help="3 = a ZeRO-3 training iteration (hooked forward/backward + update-mode "
+                         "step) of the MLP configs C2/C3 (BASELINE.json configs[2])")
+    ap.add_argument("--batch", type=int, default=16, help="ZeRO-3 MLP batch (zero1.py:144: 16)")
     ap.add_argument("--layout", default="reference", choices=["reference", "flat"])
     ap.add_argument("--bucket-mb", type=float, default=256.0)
     ap.add_argument("--buckets", default="ragged", choices=["ragged", "padded"],
@@ -239,6 +322,8 @@ def main():
     dist.init_process_group("nccl" if use_nccl else "gloo", rank=rank, world_size=world,
                             device_id=dev if use_nccl else None)
 
+    if args.zero == 3:
+        return bench_zero3(args, world, rank, dev, use_nccl)
     name, shape_fn = CONFIGS[args.config]
     shapes = shape_fn()
     total = int(sum(int(np.prod(s)) for s in shapes))

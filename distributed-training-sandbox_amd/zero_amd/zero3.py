@@ -272,6 +272,7 @@ class ShardedOptimizer:
         self.step_time = 0.0
         self.last_reduced_grads = None
         self._engine = None
+        self.timing_events = None  # optional list of (start, end, bytes) around each Adam launch
 
     # ------------------------------------------------------------------------------------------
     def _build_update_engine(self):
@@ -381,7 +382,14 @@ class ShardedOptimizer:
             hp = adam_hparams(h["lr"], h["beta1"], h["beta2"], h["eps"], h["weight_decay"], int(key[1]),
                               decoupled=h["decoupled"], amsgrad=h["amsgrad"], maximize=h["maximize"],
                               grad_div=float(ws))
-            hit[1].run(hp, cur)
+            if self.timing_events is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(cur)
+                hit[1].run(hp, cur)
+                e1.record(cur)
+                self.timing_events.append((e0, e1, hit[1].bytes))
+            else:
+                hit[1].run(hp, cur)
         for i in idx:
             st = self.optimizer.state[self.params[i]]
             st["step"] = torch.tensor(float(eng["steps"][i]))

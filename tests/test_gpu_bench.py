@@ -55,3 +55,11 @@ def test_bench_simulated_ws8_bucket_path(gpu):
     out = _run([sys.executable, "bench.py", "--config", "C4", "--steps", "3", "--warmup", "1",
                 "--simulate-ws", "8", "--no-cpu-baseline"])
     assert "diagnostic" in out and out["buckets"] > 1 and out["ms_per_step"] > 0
+
+
+def test_bench_zero3_training_iteration(gpu):
+    """--zero 3: hooked forward/backward + update-mode step of the C2 MLP (configs[2] harness)."""
+    out = _run([sys.executable, "bench.py", "--config", "C2", "--zero", "3", "--dtype", "fp32",
+                "--steps", "3", "--warmup", "1", "--no-cpu-baseline"])
+    assert out["config"]["zero"] == 3 and out["value"] > 0
+    assert out["roofline"]["launches_per_step"] >= 1 and out["zero3"]["gathers_per_step"] > 0
