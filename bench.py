@@ -214,8 +214,9 @@ def bench_zero3(args, world, rank, dev, use_nccl):
     model = torch.nn.Sequential(*layers)
     total = sum(p.numel() for p in model.parameters())
     g = torch.Generator(device=dev).manual_seed(42)  # identical data on every rank (zero3.py:186)
-    x = torch.randn(args.batch, D, device=dev, generator=g).to(dt)
-    y = torch.randn(args.batch, D, device=dev, generator=g).to(dt)
+    batch = args.batch or 16
+    x = torch.randn(batch, D, device=dev, generator=g).to(dt)
+    y = torch.randn(batch, D, device=dev, generator=g).to(dt)
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
                                  sync=False)
     zero3.register_zero3_hooks(model, opt.param_managers)
@@ -255,7 +256,7 @@ def bench_zero3(args, world, rank, dev, use_nccl):
             "data": "synthetic",
             "config": {"workload": f"{args.config} ZeRO-3 training iteration of the reference MLP "
                                    f"6xLinear({D},{D})+ReLU (hooked all-gathers, update-mode step)",
-                       "params": int(total), "batch": args.batch, "param_dtype": args.dtype,
+                       "params": int(total), "batch": batch, "param_dtype": args.dtype,
                        "zero": 3, "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -270,6 +271,62 @@ def bench_zero3(args, world, rank, dev, use_nccl):
     dist.destroy_process_group()
 
 
+def bench_train_smollm3(args, world, rank, dev, use_nccl):
+    """SmolLM3-3B training (fsdp/train_fsdp.py's loop on random-init weights and synthetic
+    tokens): tokens/s over all ranks (per-rank batch fixed → weak scaling) and the reference's
+    MFU accounting.  Optimizer: zero2.ShardedOptimizer(AdamW(lr=1e-5), overlap=True)."""
+    import torch
+    import torch.distributed as dist
+
+    from zero_amd import zero2
+    from zero_amd.training_utils import smollm3 as sm
+
+    cfg = sm.smollm3_config(layers=args.train_layers)
+    model = sm.build_model(cfg, dev)
+    params = sum(p.numel() for p in model.parameters())
+    opt = zero2.ShardedOptimizer(torch.optim.AdamW(model.parameters(), lr=1e-5), overlap=True,
+                                 sync=False)
+    batch = args.batch or 1
+    g = torch.Generator(device=dev).manual_seed(42 + rank)  # each rank its own data shard
+    ids = torch.randint(0, cfg.vocab_size, (batch, args.seq), device=dev, generator=g)
+    opt.zero_grad()
+    for _ in range(args.warmup):
+        sm.train_step(model, opt, ids)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = sm.train_step(model, opt, ids)
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    red_dev = dev if use_nccl else "cpu"
+    t = torch.tensor([el], dtype=torch.float64, device=red_dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    ms = el / args.steps * 1e3
+    tok_s = world * batch * args.seq / (ms / 1e3)
+    fpt = sm.model_flops_per_token(cfg, args.seq)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "SmolLM3-3B ZeRO-2 training throughput (SURVEY §8(f) 3; not the headline)",
+            "value": tok_s, "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random tokens, random init)",
+            "config": {"workload": "SmolLM3 causal-LM training step, ZeRO-2 AdamW(lr=1e-5) "
+                                   "backward-overlapped", "params": int(params),
+                       "layers": cfg.num_hidden_layers, "seq_len": args.seq,
+                       "global_batch": world * batch, "parallelism": f"dp{world}"},
+            "mfu_flops_per_token": fpt,
+            "tflops_per_gpu": fpt * tok_s / world / 1e12,
+            "loss": float(loss.item()),
+            "reference_published": "fsdp/train_fsdp.py:85-86: 1849 tok/s (ZeRO-3) / 3000 tok/s "
+                                   "(ZeRO-2), 2x A100-80GB, different harness",
+        }), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -279,7 +336,14 @@ def main():
     ap.add_argument("--zero", type=int, default=2, choices=[1, 2, 3],
                     help="3 = a ZeRO-3 training iteration (hooked forward/backward + update-mode "
                          "step) of the MLP configs C2/C3 (BASELINE.json configs[2])")
-    ap.add_argument("--batch", type=int, default=16, help="ZeRO-3 MLP batch (zero1.py:144: 16)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="ZeRO-3 MLP batch (default 16, zero1.py:144) / --train batch (default 1)")
+    ap.add_argument("--train", default=None, choices=["smollm3"],
+                    help="SURVEY §8(f) 3: SmolLM3-3B training step (forward + backward + ZeRO-2 "
+                         "AdamW, backward-overlapped) in tokens/s; not the headline metric")
+    ap.add_argument("--seq", type=int, default=8192, help="--train sequence length "
+                    "(fsdp/train_fsdp.py:44: 8192)")
+    ap.add_argument("--train-layers", type=int, default=None, help="--train: fewer decoder layers")
     ap.add_argument("--layout", default="reference", choices=["reference", "flat"])
     ap.add_argument("--bucket-mb", type=float, default=256.0)
     ap.add_argument("--buckets", default="ragged", choices=["ragged", "padded"],
@@ -322,6 +386,8 @@ def main():
     dist.init_process_group("nccl" if use_nccl else "gloo", rank=rank, world_size=world,
                             device_id=dev if use_nccl else None)
 
+    if args.train == "smollm3":
+        return bench_train_smollm3(args, world, rank, dev, use_nccl)
     if args.zero == 3:
         return bench_zero3(args, world, rank, dev, use_nccl)
     name, shape_fn = CONFIGS[args.config]

@@ -31,6 +31,13 @@ def zs_dtype(dt: torch.dtype) -> int:
         raise TypeError(f"zero_amd: unsupported dtype {dt} (float32 and bfloat16 only)") from None
 
 
+def comm_stream(device) -> torch.cuda.Stream:
+    """Side stream for collectives, at the highest priority: the compute stream's streaming kernels
+    launch 128 workgroups per CU, and an RCCL kernel queued behind them would wait for CU slots
+    while its peers spin; a high-priority queue gets its workgroups dispatched first."""
+    return torch.cuda.Stream(device=device, priority=-1)  # < 0: torch's high-priority pool
+
+
 def rccl_version() -> int:
     v = ctypes.c_int()
     _lib.call("zs_rccl_version", ctypes.byref(v))

@@ -34,7 +34,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .comm import zs_dtype
+from .comm import comm_stream, zs_dtype
 from .kernels import AdamSet, CopySet, adam_hparams
 from .plan import Plan
 
@@ -96,7 +96,7 @@ class ShardEngine:
         if ws > 1:
             self.buckets = [self.plan.bucket(k) for k in range(self.K)]
             self.segs = [self.plan.segments(k) for k in range(self.K)]
-            self.comm_stream = torch.cuda.Stream(device=dev)
+            self.comm_stream = comm_stream(dev)
             mk = lambda: [torch.cuda.Event() for _ in range(self.K)]  # noqa: E731
             self.ev_pack, self.ev_rs, self.ev_adam, self.ev_ag = mk(), mk(), mk(), mk()
         self.ev_c0 = torch.cuda.Event(enable_timing=True)

@@ -28,6 +28,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from .comm import comm_stream
 from .kernels import CopySet
 
 ALIGN = 64  # elements: every slot 16-byte aligned for the vector kernels
@@ -88,7 +89,7 @@ class GradBuckets:
         self.K = len(self.groups)
         off = int(self.bucket_off[-1] + self.bucket_len[-1])
         self.buf = torch.zeros(max(off, align), dtype=self.dtype, device=self.device)
-        self.comm_stream = torch.cuda.Stream(device=self.device)
+        self.comm_stream = comm_stream(self.device)
         self.ev_ready = [torch.cuda.Event() for _ in range(self.K)]
         self.ev_done = [torch.cuda.Event() for _ in range(self.K)]
         self._size = np.array([len(g) for g in self.groups], np.int64)

@@ -33,7 +33,7 @@ import numpy as np
 import torch
 from torch.optim import Optimizer
 
-from .comm import RcclComm
+from .comm import RcclComm, comm_stream
 from .engine import ALIGN_ELEMS
 from .kernels import AdamSet, adam_hparams
 from .plan import Plan
@@ -58,7 +58,7 @@ class _GatherRuntime:
 
     def __init__(self, ws, rank, comm, device):
         self.ws, self.rank, self.comm, self.device = ws, rank, comm, device
-        self.stream = torch.cuda.Stream(device=device)
+        self.stream = comm_stream(device)
         self.pending = {}      # key -> (list[(manager, full_tensor)], event)
         self.sequence = []     # learned order of group keys
         self.pos = 0

@@ -1,0 +1,50 @@
+"""SmolLM3 training step through the ZeRO-2 drop-in: a shrunken SmolLM3
+(transformers, random init) trains with zero2.ShardedOptimizer(AdamW) in backward-overlapped mode;
+after every step every parameter's bf16 bits equal the C oracle's AdamW (decoupled weight decay,
+fp32 master) applied to the gradients the backward produced."""
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+from _zero_run import init_pg
+
+pytestmark = pytest.mark.gpu
+
+
+def test_smollm3_zero2_adamw_overlap_bit_exact(gpu):
+    from oracle import c_oracle
+    from zero_amd import zero2
+    from zero_amd.training_utils import smollm3 as sm
+
+    init_pg(0, 1, 29655)
+    try:
+        cfg = sm.smollm3_config(layers=2, hidden=128, intermediate=256, heads=4, kv_heads=2, vocab=512)
+        model = sm.build_model(cfg, gpu)
+        params = list(model.parameters())
+        lr, wd = 1e-3, 0.01
+        opt = zero2.ShardedOptimizer(torch.optim.AdamW(params, lr=lr, weight_decay=wd), overlap=True,
+                                     overlap_bucket_mb=0.05)
+        assert opt.engine.gb.K > 1
+        master = [p.detach().float().cpu().numpy().reshape(-1).copy() for p in params]
+        m = [np.zeros_like(x) for x in master]
+        v = [np.zeros_like(x) for x in master]
+        g = torch.Generator(device=gpu).manual_seed(1)
+        ids = torch.randint(0, cfg.vocab_size, (2, 64), device=gpu, generator=g)
+        opt.zero_grad()
+        for t in range(1, 5):
+            loss = model(input_ids=ids, labels=ids).loss
+            loss.backward()
+            grads = [p.grad.detach().reshape(-1).view(torch.int16).cpu().numpy().view(np.uint16).copy()
+                     for p in params]
+            opt.step()
+            opt.zero_grad()
+            hp = c_oracle.hparams(lr=lr, weight_decay=wd, step=t, decoupled=True)
+            for i, p in enumerate(params):
+                want = np.zeros(master[i].size, np.uint16)
+                c_oracle.adam_bf16(master[i], want, grads[i], m[i], v[i], hp)
+                got = p.detach().reshape(-1).view(torch.int16).cpu().numpy().view(np.uint16)
+                assert np.array_equal(got, want), (t, i)
+            assert torch.isfinite(loss)
+    finally:
+        dist.destroy_process_group()

@@ -223,3 +223,18 @@ def test_grad_bucket_grouping():
     assert all(a[1] <= b[0] for a, b in zip(ends, ends[1:]))
     with pytest.raises(ValueError):
         plan_grad_buckets([1, 2], [0, 0], 64, 4, order=[0, 0])
+
+
+def test_smollm3_shapes_match_transformers_model():
+    """shapes.smollm3_3b_shapes (the bench's synthetic set) is exactly the parameter list of
+    transformers' SmolLM3-3B (built on the meta device: no memory)."""
+    import torch
+    from zero_amd.shapes import smollm3_3b_shapes
+    from zero_amd.training_utils import smollm3 as sm
+    from transformers import SmolLM3ForCausalLM
+
+    with torch.device("meta"):
+        model = SmolLM3ForCausalLM(sm.smollm3_config())
+    got = [tuple(p.shape) for p in model.parameters()]
+    assert got == [tuple(s) for s in smollm3_3b_shapes()]
+    assert sm.model_flops_per_token(model.config, 8192) > 6 * 3.0e9
