@@ -13,6 +13,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -355,12 +357,31 @@ struct zs_adamset {
   int g_dtype = ZS_F32, p_dtype = ZS_BF16, has_carry = 0, has_vmax = 0;
 };
 
+// Table uploads run on a private non-blocking stream per device, so creating a set never
+// synchronises with the legacy null stream (which may hold kernels waiting on collectives).
+static hipStream_t upload_stream() {
+  static std::mutex mu;
+  static std::map<int, hipStream_t> streams;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = streams.find(dev);
+  if (it != streams.end()) return it->second;
+  hipStream_t st = nullptr;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  streams[dev] = st;
+  return st;
+}
+
 template <typename T>
 static int upload(const std::vector<T>& h, T** d) {
   *d = nullptr;
   if (h.empty()) return ZS_OK;
+  hipStream_t st = upload_stream();
+  if (!st) return zs::fail(ZS_ERR_HIP, "table upload: no upload stream");
   ZS_HIP(hipMalloc(reinterpret_cast<void**>(d), h.size() * sizeof(T)));
-  hipError_t e = hipMemcpy(*d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice);
+  hipError_t e = hipMemcpyAsync(*d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) {
     (void)hipFree(*d);
     *d = nullptr;

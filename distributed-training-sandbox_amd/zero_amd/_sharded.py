@@ -157,6 +157,10 @@ class ShardedOptimizerBase:
         if self._sync:
             torch.cuda.synchronize(self.engine.device)
             self.communication_time += self.engine.comm_time_s()
+            self.engine.release_retired()
+        elif self.engine.n_retired() > 64:
+            torch.cuda.synchronize(self.engine.device)
+            self.engine.release_retired()
         self.step_time += time.perf_counter() - step_start
         return loss
 

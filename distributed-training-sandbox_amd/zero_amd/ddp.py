@@ -83,6 +83,9 @@ class SimpleDistributedDataParallelism:
                 p.grad = gb.view(i) if has[i] else None
         gb.views_installed = False
         gb.reset()
+        if len(gb.retired) > 64:  # tables replaced because grads moved: free at an idle point
+            torch.cuda.synchronize(gb.device)
+            gb.retired.clear()
 
     def __call__(self, *args, **kwargs):
         return self.model(*args, **kwargs)

@@ -103,6 +103,7 @@ class ShardEngine:
         self.ev_c1 = torch.cuda.Event(enable_timing=True)
         self.steps = np.zeros(len(params), np.int64)  # torch's per-param state['step']
         self._cache = {}
+        self.retired = []
         self.timing_events = None  # optional list of (start, end) events around each Adam launch
         self.comm_events = None    # optional list of (kind, even, start, end, bus_bytes) per collective
         self.copy_events = None    # optional list of (kind, start, end, bytes) per pack / unpack
@@ -141,8 +142,22 @@ class ShardEngine:
         if hit is not None and hit[0] == sig:
             return hit[1]
         obj = build()
+        if hit is not None:
+            # tensors moved: the old table may still be read by queued kernels, and hipFree
+            # synchronises the device — keep it until the next point the device is idle
+            self.retired.append(hit[1])
         self._cache[key] = (sig, obj)
         return obj
+
+    def n_retired(self) -> int:
+        gb = getattr(self, "gb", None)
+        return len(self.retired) + (len(gb.retired) if gb is not None else 0)
+
+    def release_retired(self):
+        """Free replaced segment tables; call only after the device has been synchronised."""
+        self.retired.clear()
+        if getattr(self, "gb", None) is not None:
+            self.gb.retired.clear()
 
     # ------------------------------------------------------------------------------------------
     def _adam_rows(self, idx, g_ptr, mst, mst_out, p_out, so, n):

@@ -94,6 +94,7 @@ class GradBuckets:
         self.ev_done = [torch.cuda.Event() for _ in range(self.K)]
         self._size = np.array([len(g) for g in self.groups], np.int64)
         self._cache = {}
+        self.retired = []
         self.views_installed = False
         self.launched_in_backward = 0
         self.reset()
@@ -174,6 +175,8 @@ class GradBuckets:
             sig = np.array(src + dst, np.uint64).tobytes()
             cs = self._cache.get(k)
             if cs is None or cs[0] != sig:
+                if cs is not None:  # queued kernels may still read the old table (see engine)
+                    self.retired.append(cs[1])
                 cs = (sig, CopySet(src, dst, nb))
                 self._cache[k] = cs
             cs[1].run(stream)

@@ -287,7 +287,7 @@ class ShardedOptimizer:
                    m=torch.zeros(L, dtype=torch.float32, device=dev),
                    v=torch.zeros(L, dtype=torch.float32, device=dev),
                    vmax=None, gshard=torch.zeros(L, dtype=dtype, device=dev), master=None,
-                   steps=np.zeros(len(self.params), np.int64), cache={})
+                   steps=np.zeros(len(self.params), np.int64), cache={}, retired=[])
         if dtype == torch.bfloat16:
             eng["master"] = torch.zeros(L, dtype=torch.float32, device=dev)
             for i, so, ln in zip(pc.param, pc.stream_off, pc.length):
@@ -376,6 +376,8 @@ class ShardedOptimizer:
             ck = (int(key[0]), len(sel), int(sel[0]))
             hit = eng["cache"].get(ck)
             if hit is None or hit[0] != sub.tobytes():
+                if hit is not None:  # keep until the device is idle (hipFree would sync it)
+                    eng["retired"].append(hit[1])
                 hit = (sub.tobytes(), AdamSet(sub, ZS_BF16 if eng["dtype"] == torch.bfloat16 else ZS_F32))
                 eng["cache"][ck] = hit
             h = adam_group_hparams(self._groups[int(key[0])], self.optimizer)
@@ -407,8 +409,10 @@ class ShardedOptimizer:
                 self._step_update()
             else:
                 self._reduce_reference()
-        if self._sync:
+        if self._sync or (self._engine is not None and len(self._engine["retired"]) > 64):
             torch.cuda.synchronize()
+            if self._engine is not None:
+                self._engine["retired"].clear()
         self.communication_time += time.perf_counter() - step_start
         self.runtime.end_iteration()
         self.step_time += time.perf_counter() - step_start
