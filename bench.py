@@ -218,7 +218,7 @@ def bench_zero3(args, world, rank, dev, use_nccl):
     x = torch.randn(batch, D, device=dev, generator=g).to(dt)
     y = torch.randn(batch, D, device=dev, generator=g).to(dt)
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
-                                 sync=False)
+                                 sync=False, gather_dtype=args.gather)
     zero3.register_zero3_hooks(model, opt.param_managers)
 
     def step():
@@ -257,7 +257,8 @@ def bench_zero3(args, world, rank, dev, use_nccl):
             "config": {"workload": f"{args.config} ZeRO-3 training iteration of the reference MLP "
                                    f"6xLinear({D},{D})+ReLU (hooked all-gathers, update-mode step)",
                        "params": int(total), "batch": batch, "param_dtype": args.dtype,
-                       "zero": 3, "parallelism": f"dp{world}"},
+                       "zero": 3, "gather_dtype": args.gather or args.dtype,
+                       "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": "adam_segments_kernel",
@@ -338,6 +339,8 @@ def main():
                          "step) of the MLP configs C2/C3 (BASELINE.json configs[2])")
     ap.add_argument("--batch", type=int, default=None,
                     help="ZeRO-3 MLP batch (default 16, zero1.py:144) / --train batch (default 1)")
+    ap.add_argument("--gather", default=None, choices=["fp8"],
+                    help="--zero 3: all-gather parameters as row-scaled fp8 E4M3 (SURVEY §8(f) 4)")
     ap.add_argument("--train", default=None, choices=["smollm3"],
                     help="SURVEY §8(f) 3: SmolLM3-3B training step (forward + backward + ZeRO-2 "
                          "AdamW, backward-overlapped) in tokens/s; not the headline metric")

@@ -34,6 +34,7 @@ static int to_nccl(int dtype, ncclDataType_t* t) {
   switch (dtype) {
     case ZS_F32: *t = ncclFloat32; return ZS_OK;
     case ZS_BF16: *t = ncclBfloat16; return ZS_OK;
+    case ZS_U8: *t = ncclUint8; return ZS_OK;
     default: return zs::fail(ZS_ERR_INVALID, "unsupported dtype %d", dtype);
   }
 }

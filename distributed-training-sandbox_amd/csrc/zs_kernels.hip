@@ -337,6 +337,130 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(T* __restrict__ x, int6
   }
 }
 
+// ----------------------------------------------------------------------------------------------
+// row-wise fp8 (OCP E4M3) quantise / dequantise for the low-precision parameter all-gather
+// ----------------------------------------------------------------------------------------------
+constexpr float kE4M3Max = 448.0f;
+
+__device__ __forceinline__ uint32_t e4m3x4(float a, float b, float c, float d) {
+  // v_cvt_pk_fp8_f32: round to nearest even, OCP E4M3 on gfx950; inputs pre-clamped to ±448
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return uint32_t(w);
+}
+__device__ __forceinline__ float qclamp(float x, float inv) {
+#pragma clang fp contract(off)
+  return __builtin_amdgcn_fmed3f(x * inv, kE4M3Max, -kE4M3Max);
+}
+
+// One workgroup per row (grid-stride over rows): amax by wave shuffles + 4-entry LDS, then the
+// row is re-read (L2-resident: <= 64 KiB) and converted.  VEC: 8 elements per lane per access
+// (16 B bf16 / 2 x 16 B fp32 loads, 8 B fp8 stores) when row_len % 8 == 0 and rows are aligned.
+template <typename T, bool VEC>
+__global__ __launch_bounds__(kThreads) void fp8_quantize_rows_kernel(
+    const T* __restrict__ src, unsigned char* __restrict__ dst, float* __restrict__ scales,
+    int64_t rows, int64_t row_len) {
+#pragma clang fp contract(off)
+  __shared__ float red[kThreads / 64];
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+    const gptr<const T> x = glob(src + r * row_len);
+    const gptr<unsigned char> q = glob(dst + r * row_len);
+    float amax = 0.0f;
+    if constexpr (VEC) {
+      for (int64_t i = int64_t(threadIdx.x) * 8; i < row_len; i += kThreads * 8) {
+        float v[8];
+        if constexpr (sizeof(T) == 2) {
+          const uint4 raw = *reinterpret_cast<gptr<const uint4>>(x + i);
+          const unsigned short* h = reinterpret_cast<const unsigned short*>(&raw);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = bf16_to_f32(h[j]);
+        } else {
+          const float4 a = *reinterpret_cast<gptr<const float4>>(x + i);
+          const float4 b = *reinterpret_cast<gptr<const float4>>(x + i + 4);
+          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+          v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[j]));
+      }
+    } else {
+      for (int64_t i = threadIdx.x; i < row_len; i += kThreads) amax = fmaxf(amax, fabsf(to_f32<T>(x[i])));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+    __syncthreads();
+    amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    __syncthreads();
+    const float inv = amax > 0.0f ? kE4M3Max / amax : 1.0f;
+    if (threadIdx.x == 0) glob(scales)[r] = amax > 0.0f ? amax / kE4M3Max : 1.0f;
+    if constexpr (VEC) {
+      for (int64_t i = int64_t(threadIdx.x) * 8; i < row_len; i += kThreads * 8) {
+        float v[8];
+        if constexpr (sizeof(T) == 2) {
+          const uint4 raw = *reinterpret_cast<gptr<const uint4>>(x + i);
+          const unsigned short* h = reinterpret_cast<const unsigned short*>(&raw);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = bf16_to_f32(h[j]);
+        } else {
+          const float4 a = *reinterpret_cast<gptr<const float4>>(x + i);
+          const float4 b = *reinterpret_cast<gptr<const float4>>(x + i + 4);
+          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+          v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        }
+        uint2 out;
+        out.x = e4m3x4(qclamp(v[0], inv), qclamp(v[1], inv), qclamp(v[2], inv), qclamp(v[3], inv));
+        out.y = e4m3x4(qclamp(v[4], inv), qclamp(v[5], inv), qclamp(v[6], inv), qclamp(v[7], inv));
+        *reinterpret_cast<gptr<uint2>>(q + i) = out;
+      }
+    } else {
+      for (int64_t i = threadIdx.x; i < row_len; i += kThreads) {
+        const float c = qclamp(to_f32<T>(x[i]), inv);
+        q[i] = (unsigned char)(__builtin_amdgcn_cvt_pk_fp8_f32(c, c, 0, false) & 0xff);
+      }
+    }
+  }
+}
+
+// Grid-stride over 8-element groups (VEC) or elements; a group never straddles rows (row_len % 8
+// == 0 in the VEC instantiation).
+template <typename T, bool VEC>
+__global__ __launch_bounds__(kThreads) void fp8_dequantize_rows_kernel(
+    const unsigned char* __restrict__ src, const float* __restrict__ scales, T* __restrict__ dst,
+    int64_t n, int64_t row_len) {
+#pragma clang fp contract(off)
+  const gptr<const unsigned char> q = glob(src);
+  const gptr<T> y = glob(dst);
+  const int64_t stride = int64_t(gridDim.x) * kThreads;
+  if constexpr (VEC) {
+    for (int64_t g = int64_t(blockIdx.x) * kThreads + threadIdx.x; g < n / 8; g += stride) {
+      const int64_t i = g * 8;
+      const float sc = glob(scales)[i / row_len];
+      const uint2 raw = *reinterpret_cast<gptr<const uint2>>(q + i);
+      const int lo = int(raw.x), hi = int(raw.y);
+      float v[8] = {__builtin_amdgcn_cvt_f32_fp8(lo, 0) * sc, __builtin_amdgcn_cvt_f32_fp8(lo, 1) * sc,
+                    __builtin_amdgcn_cvt_f32_fp8(lo, 2) * sc, __builtin_amdgcn_cvt_f32_fp8(lo, 3) * sc,
+                    __builtin_amdgcn_cvt_f32_fp8(hi, 0) * sc, __builtin_amdgcn_cvt_f32_fp8(hi, 1) * sc,
+                    __builtin_amdgcn_cvt_f32_fp8(hi, 2) * sc, __builtin_amdgcn_cvt_f32_fp8(hi, 3) * sc};
+      if constexpr (sizeof(T) == 2) {
+        uint4 o;
+        unsigned short* h = reinterpret_cast<unsigned short*>(&o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) h[j] = f32_to_bf16(v[j]);
+        *reinterpret_cast<gptr<uint4>>(y + i) = o;
+      } else {
+        *reinterpret_cast<gptr<float4>>(y + i) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<gptr<float4>>(y + i + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+    }
+  } else {
+    for (int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x; i < n; i += stride) {
+      const float v = __builtin_amdgcn_cvt_f32_fp8(int(q[i]), 0) * glob(scales)[i / row_len];
+      y[i] = from_f32<T>(v);
+    }
+  }
+}
+
 inline bool aligned(uint64_t p, uint64_t a) { return p % a == 0; }
 
 }  // namespace
@@ -465,6 +589,57 @@ int zs_scale(void* x, int64_t n, int dtype, double div, uintptr_t stream) {
   else
     hipLaunchKernelGGL(scale_kernel<unsigned short>, dim3(grid), dim3(kThreads), 0, st,
                        static_cast<unsigned short*>(x), n, fdiv, inv, pow2);
+  ZS_HIP(hipGetLastError());
+  return ZS_OK;
+}
+
+int zs_fp8_quantize_rows(const void* src, int src_dtype, void* dst, float* scales, int64_t rows,
+                         int64_t row_len, uintptr_t stream) {
+  ZS_REQUIRE(rows >= 0 && row_len >= 0, "zs_fp8_quantize_rows: negative size");
+  ZS_REQUIRE(src_dtype == ZS_F32 || src_dtype == ZS_BF16, "zs_fp8_quantize_rows: bad dtype %d",
+             src_dtype);
+  if (rows == 0 || row_len == 0) return ZS_OK;
+  ZS_REQUIRE(src && dst && scales, "zs_fp8_quantize_rows: NULL buffer");
+  const bool vec = row_len % 8 == 0 && aligned(uint64_t(src), 16) && aligned(uint64_t(dst), 8);
+  const int grid = int(std::min<int64_t>(rows, grid_cap()));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  unsigned char* q = static_cast<unsigned char*>(dst);
+  if (src_dtype == ZS_F32) {
+    const float* x = static_cast<const float*>(src);
+    if (vec) hipLaunchKernelGGL((fp8_quantize_rows_kernel<float, true>), dim3(grid), dim3(kThreads), 0, st, x, q, scales, rows, row_len);
+    else hipLaunchKernelGGL((fp8_quantize_rows_kernel<float, false>), dim3(grid), dim3(kThreads), 0, st, x, q, scales, rows, row_len);
+  } else {
+    const unsigned short* x = static_cast<const unsigned short*>(src);
+    if (vec) hipLaunchKernelGGL((fp8_quantize_rows_kernel<unsigned short, true>), dim3(grid), dim3(kThreads), 0, st, x, q, scales, rows, row_len);
+    else hipLaunchKernelGGL((fp8_quantize_rows_kernel<unsigned short, false>), dim3(grid), dim3(kThreads), 0, st, x, q, scales, rows, row_len);
+  }
+  ZS_HIP(hipGetLastError());
+  return ZS_OK;
+}
+
+int zs_fp8_dequantize_rows(const void* src, const float* scales, void* dst, int dst_dtype,
+                           int64_t rows, int64_t row_len, uintptr_t stream) {
+  ZS_REQUIRE(rows >= 0 && row_len >= 0, "zs_fp8_dequantize_rows: negative size");
+  ZS_REQUIRE(dst_dtype == ZS_F32 || dst_dtype == ZS_BF16, "zs_fp8_dequantize_rows: bad dtype %d",
+             dst_dtype);
+  if (rows == 0 || row_len == 0) return ZS_OK;
+  ZS_REQUIRE(src && dst && scales, "zs_fp8_dequantize_rows: NULL buffer");
+  const int64_t n = rows * row_len;
+  const bool vec = row_len % 8 == 0 && aligned(uint64_t(src), 8) && aligned(uint64_t(dst), 16);
+  const int64_t work = vec ? n / 8 : n;
+  const int grid = int(std::min<int64_t>(std::max<int64_t>(1, (work + kThreads - 1) / kThreads),
+                                         grid_cap()));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const unsigned char* q = static_cast<const unsigned char*>(src);
+  if (dst_dtype == ZS_F32) {
+    float* y = static_cast<float*>(dst);
+    if (vec) hipLaunchKernelGGL((fp8_dequantize_rows_kernel<float, true>), dim3(grid), dim3(kThreads), 0, st, q, scales, y, n, row_len);
+    else hipLaunchKernelGGL((fp8_dequantize_rows_kernel<float, false>), dim3(grid), dim3(kThreads), 0, st, q, scales, y, n, row_len);
+  } else {
+    unsigned short* y = static_cast<unsigned short*>(dst);
+    if (vec) hipLaunchKernelGGL((fp8_dequantize_rows_kernel<unsigned short, true>), dim3(grid), dim3(kThreads), 0, st, q, scales, y, n, row_len);
+    else hipLaunchKernelGGL((fp8_dequantize_rows_kernel<unsigned short, false>), dim3(grid), dim3(kThreads), 0, st, q, scales, y, n, row_len);
+  }
   ZS_HIP(hipGetLastError());
   return ZS_OK;
 }

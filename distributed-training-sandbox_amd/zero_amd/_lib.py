@@ -15,7 +15,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_PATH = Path(os.environ.get("ZERO_AMD_LIB", Path(__file__).resolve().parent / "libzero_amd.so"))
 
 ZS_OK, ZS_ERR_INVALID, ZS_ERR_HIP, ZS_ERR_RCCL, ZS_ERR_NOMEM = 0, 1, 2, 3, 4
-ZS_F32, ZS_BF16 = 0, 1
+ZS_F32, ZS_BF16, ZS_U8 = 0, 1, 2
 ZS_LAYOUT_R, ZS_LAYOUT_Z, ZS_LAYOUT_F = 0, 1, 2
 ZS_BUCKETS_RAGGED, ZS_BUCKETS_PADDED = 0, 1
 ABI_VERSION = 2
@@ -28,6 +28,7 @@ EXPORTED = (
     "zs_plan_stream_len", "zs_plan_num_pieces", "zs_plan_pieces", "zs_plan_bucket",
     "zs_plan_num_segments", "zs_plan_segments",
     "zs_copyset_create", "zs_copyset_run", "zs_copyset_destroy", "zs_scale",
+    "zs_fp8_quantize_rows", "zs_fp8_dequantize_rows",
     "zs_adam_hparams_init", "zs_adamset_create", "zs_adamset_run", "zs_adamset_destroy",
     "zs_adamset_stats",
     "zs_comm_unique_id", "zs_comm_init", "zs_comm_destroy", "zs_reduce_scatter", "zs_all_gather",
@@ -85,6 +86,8 @@ _SIGS = {
     "zs_copyset_run": ([_P, _U], ctypes.c_int),
     "zs_copyset_destroy": ([_P], ctypes.c_int),
     "zs_scale": ([_P, _I64, ctypes.c_int, ctypes.c_double, _U], ctypes.c_int),
+    "zs_fp8_quantize_rows": ([_P, ctypes.c_int, _P, _P, _I64, _I64, _U], ctypes.c_int),
+    "zs_fp8_dequantize_rows": ([_P, _P, _P, ctypes.c_int, _I64, _I64, _U], ctypes.c_int),
     "zs_adam_hparams_init": ([ctypes.c_double] * 5 + [ctypes.c_int] * 3 +
                              [_I64, ctypes.c_double, ctypes.c_double, ctypes.POINTER(AdamHParams)],
                              ctypes.c_int),

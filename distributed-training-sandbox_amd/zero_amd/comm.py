@@ -21,14 +21,14 @@ import torch.distributed as dist
 from . import _lib
 from .kernels import stream_handle
 
-_DTYPES = {torch.float32: _lib.ZS_F32, torch.bfloat16: _lib.ZS_BF16}
+_DTYPES = {torch.float32: _lib.ZS_F32, torch.bfloat16: _lib.ZS_BF16, torch.uint8: _lib.ZS_U8}
 
 
 def zs_dtype(dt: torch.dtype) -> int:
     try:
         return _DTYPES[dt]
     except KeyError:
-        raise TypeError(f"zero_amd: unsupported dtype {dt} (float32 and bfloat16 only)") from None
+        raise TypeError(f"zero_amd: unsupported dtype {dt} (float32, bfloat16, uint8)") from None
 
 
 def comm_stream(device) -> torch.cuda.Stream:

@@ -33,7 +33,9 @@ import numpy as np
 import torch
 from torch.optim import Optimizer
 
-from .comm import RcclComm, comm_stream
+from . import _lib
+from .comm import RcclComm, comm_stream, zs_dtype
+from .kernels import stream_handle
 from .engine import ALIGN_ELEMS
 from .kernels import AdamSet, adam_hparams
 from .plan import Plan
@@ -77,12 +79,15 @@ class _GatherRuntime:
             return
         ev_ready = torch.cuda.Event()
         ev_ready.record(torch.cuda.current_stream(self.device))  # shards may just have been updated
-        out = []
         with torch.cuda.stream(self.stream):
             self.stream.wait_event(ev_ready)
+            # kernels (pad copies, fp8 quantisation) before the RCCL group, dequantisation after:
+            # an RCCL group only launches its collectives at group end
+            states = [m._gather_prepare(self.stream) for m in managers]
             with self._group():
-                for m in managers:
-                    out.append((m, m._gather_into_new(self.comm, self.stream)))
+                for m, st in zip(managers, states):
+                    m._gather_issue(self.comm, self.stream, st)
+            out = [(m, m._gather_finish(self.stream, st)) for m, st in zip(managers, states)]
             ev = torch.cuda.Event()
             ev.record(self.stream)
         self.pending[key] = (out, ev)
@@ -124,7 +129,7 @@ class Zero3ParamManager:
     """zero3.py:25-52: tracks one parameter's dim-0 shard and gathers / releases the full tensor."""
 
     def __init__(self, param, shard_idx, world_size, shard_dim=0, *, runtime=None, shard=None,
-                 full_shape=None, keep_full_grad=False):
+                 full_shape=None, keep_full_grad=False, gather_dtype=None):
         if shard_dim != 0:
             raise NotImplementedError("zero_amd ZeRO-3 shards along dim 0 (as zero3.py:106)")
         self.param = param
@@ -141,16 +146,48 @@ class Zero3ParamManager:
         self.cs, self.r0, self.r1 = _chunk_geom(d0, world_size, shard_idx)
         self.S = self.cs * self.row  # padded chunk elements (equal on every rank)
         self.numel = int(np.prod(self.full_shape)) if self.full_shape else 1
+        if gather_dtype not in (None, "fp8"):
+            raise ValueError(f"gather_dtype must be None or 'fp8' (got {gather_dtype!r})")
+        # fp8 only for matrices (row-wise scales); vectors (biases, norms) gather as they are
+        self.fp8 = gather_dtype == "fp8" and len(self.full_shape) >= 2
 
     # -- gather ----------------------------------------------------------------------------------
-    def _gather_into_new(self, comm, stream):
-        full = torch.empty(self.world_size * self.S, dtype=self.shard.dtype, device=self.shard.device)
+    # Three phases so a module's managers share one RCCL group: prepare (kernels on the side
+    # stream), issue (collectives, inside the group), finish (kernels after the group).
+    def _gather_prepare(self, stream):
+        dev, ws = self.shard.device, self.world_size
+        rows = self.r1 - self.r0
+        if self.fp8:  # 1 byte per element + one fp32 scale per row
+            q = torch.zeros(self.S, dtype=torch.uint8, device=dev)
+            sc = torch.ones(self.cs, dtype=torch.float32, device=dev)
+            if rows:
+                _lib.call("zs_fp8_quantize_rows", self.shard.data_ptr(), zs_dtype(self.shard.dtype),
+                          q.data_ptr(), sc.data_ptr(), rows, self.row, stream_handle(stream))
+            return (q, sc, torch.empty(ws * self.S, dtype=torch.uint8, device=dev),
+                    torch.empty(ws * self.cs, dtype=torch.float32, device=dev))
         send = self.shard.reshape(-1)
         if send.numel() != self.S:  # short / empty last chunks: pad so every rank sends S elements
-            pad = torch.zeros(self.S, dtype=send.dtype, device=send.device)
+            pad = torch.zeros(self.S, dtype=send.dtype, device=dev)
             pad[:send.numel()].copy_(send)
             send = pad
-        comm.all_gather(send, full, stream)
+        return (send, torch.empty(ws * self.S, dtype=self.shard.dtype, device=dev))
+
+    def _gather_issue(self, comm, stream, st):
+        if self.fp8:
+            q, sc, full_q, full_sc = st
+            comm.all_gather(q, full_q, stream)
+            comm.all_gather(sc, full_sc, stream)
+        else:
+            send, full = st
+            comm.all_gather(send, full, stream)
+
+    def _gather_finish(self, stream, st):
+        if not self.fp8:
+            return st[1]
+        _, _, full_q, full_sc = st
+        full = torch.empty(self.world_size * self.S, dtype=self.shard.dtype, device=self.shard.device)
+        _lib.call("zs_fp8_dequantize_rows", full_q.data_ptr(), full_sc.data_ptr(), full.data_ptr(),
+                  zs_dtype(full.dtype), self.world_size * self.cs, self.row, stream_handle(stream))
         return full
 
     def _install_full(self, full):
@@ -225,7 +262,8 @@ def register_zero3_hooks(model, param_managers):
 class ShardedOptimizer:
     """zero3.py:81-168 with ``update`` selecting reference (no-op) or real ZeRO-3 updates."""
 
-    def __init__(self, optimizer: Optimizer, *, update: bool = False, comm=None, sync: bool = True):
+    def __init__(self, optimizer: Optimizer, *, update: bool = False, comm=None, sync: bool = True,
+                 gather_dtype=None):
         if not isinstance(optimizer, torch.optim.Adam):
             raise TypeError("zero_amd ShardedOptimizer wraps torch.optim.Adam / AdamW")
         self.optimizer = optimizer
@@ -264,7 +302,7 @@ class ShardedOptimizer:
             param.data = shard
             self.param_managers[param] = Zero3ParamManager(
                 param, rank, world_size, 0, runtime=self.runtime, shard=shard,
-                full_shape=full_shape, keep_full_grad=self.update)
+                full_shape=full_shape, keep_full_grad=self.update, gather_dtype=gather_dtype)
         for group in self.optimizer.param_groups:  # zero3.py:114-115
             group["params"] = [p for p in group["params"] if p in self.local_params]
         self.grad_hooks = {}
@@ -312,12 +350,19 @@ class ShardedOptimizer:
             man = self.param_managers[param]
             if g.shape != param.data.shape:  # zero3.py:141-143
                 g = g.reshape(man.full_shape)[man.r0:man.r1].contiguous()
-            shards.append(g)
+            n = g.numel()
+            if n != man.S:  # uneven torch.chunk: every rank all-reduces S elements (the
+                pad = torch.zeros(man.S, dtype=g.dtype, device=g.device)  # reference deadlocks)
+                pad[:n].copy_(g.reshape(-1))
+                shards.append((pad, n, g.shape))
+            else:
+                shards.append((g, n, g.shape))
         grp = getattr(self.comm, "group", None)
         with (grp() if grp is not None else contextlib.nullcontext()):
-            for g in shards:
-                self.comm.all_reduce(g, cur)
-        self.last_reduced_grads = [g.div_(self.world_size) for g in shards]
+            for buf, _, _ in shards:
+                self.comm.all_reduce(buf, cur)
+        self.last_reduced_grads = [buf.reshape(-1)[:n].view(shp).div_(self.world_size)
+                                   for buf, n, shp in shards]
         for param in self.params:  # zero3.py:150-153 for-else: every grad is dropped
             param.grad = None
 

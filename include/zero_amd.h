@@ -34,7 +34,7 @@ enum zs_status {
   ZS_ERR_NOMEM = 4
 };
 
-enum zs_dtype { ZS_F32 = 0, ZS_BF16 = 1 };
+enum zs_dtype { ZS_F32 = 0, ZS_BF16 = 1, ZS_U8 = 2 /* raw bytes (fp8 payloads); collectives only */ };
 
 /* Shard layouts (SURVEY.md §7 "Two shard layouts"). */
 enum zs_layout {
@@ -121,6 +121,17 @@ int zs_copyset_destroy(zs_copyset* cs);
  * whole all-reduced gradient bucket.  fp32: IEEE division (reciprocal multiply when div is a power
  * of two, which is exact); bf16: computed in fp32, rounded to nearest even. */
 int zs_scale(void* x, int64_t n, int dtype, double div, uintptr_t stream);
+
+/* Row-wise fp8 (OCP E4M3, the gfx950 format) quantisation for the low-precision parameter
+ * all-gather (the reference's torchao float8 all-gather, fp8/fp8_benchmark.py:79-81).
+ * Row r of src (row_len elements, dtype ZS_F32 / ZS_BF16): amax = max|x|, inv = 448/amax,
+ * dst[r, i] = e4m3(RNE(clamp(x * inv, ±448))), scales[r] = amax/448 (amax == 0: inv = scale = 1).
+ * Dequantise: dst[r, i] = (float(q) * scales[r]) rounded to dst_dtype.  Replaces gathering the
+ * bf16/fp32 shard in zero3.py:36-41 with 1 byte/element + 4 bytes/row. */
+int zs_fp8_quantize_rows(const void* src, int src_dtype, void* dst, float* scales, int64_t rows,
+                         int64_t row_len, uintptr_t stream);
+int zs_fp8_dequantize_rows(const void* src, const float* scales, void* dst, int dst_dtype,
+                           int64_t rows, int64_t row_len, uintptr_t stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Fused Adam / AdamW.  Replaces torch.optim.Adam.step on the owned shard (zero1.py:88,          */

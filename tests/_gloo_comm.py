@@ -29,12 +29,11 @@ class GlooStagedComm:
     def all_gather(self, send, recv, stream):
         stream.synchronize()
         h = send.detach().to("cpu")
-        if h.dtype == torch.bfloat16:
-            h = h.view(torch.int16)
-        out = torch.empty(recv.numel(), dtype=h.dtype)
+        if h.dtype != torch.float32:  # a gather is a byte copy: move bf16 / uint8 as int8 bytes
+            h = h.view(torch.int8)
+        out = torch.empty(recv.numel() * recv.element_size() // h.element_size(), dtype=h.dtype)
         dist.all_gather_into_tensor(out, h, group=self.group)
-        if recv.dtype == torch.bfloat16:
-            out = out.view(torch.bfloat16)
+        out = out.view(recv.dtype)
         with torch.cuda.stream(stream):
             recv.copy_(out.to(recv.device))
         self.calls.append(("ag", recv.numel()))
@@ -54,11 +53,10 @@ class GlooStagedComm:
     def broadcast(self, t, root, stream):
         stream.synchronize()
         h = t.detach().to("cpu")
-        if h.dtype == torch.bfloat16:
-            h = h.view(torch.int16)
+        if h.dtype != torch.float32:
+            h = h.view(torch.int8)
         dist.broadcast(h, src=self._root(root), group=self.group)
-        if t.dtype == torch.bfloat16:
-            h = h.view(torch.bfloat16)
+        h = h.view(t.dtype)
         with torch.cuda.stream(stream):
             t.copy_(h.to(t.device))
         self.calls.append(("bcast", t.numel()))
@@ -80,16 +78,12 @@ class GlooStagedComm:
     def broadcast_v(self, buf, win_off, win_len, stream):
         stream.synchronize()
         h = buf.detach().to("cpu")
-        if h.dtype == torch.bfloat16:
-            h = h.view(torch.int16)
         for root, (off, n) in enumerate(zip(win_off, win_len)):
             if n:
                 part = h[int(off):int(off) + int(n)].clone()
-                dist.broadcast(part, src=dist.get_global_rank(self.group, root) if self.group else root,
-                               group=self.group)
-                h[int(off):int(off) + int(n)] = part
-        if buf.dtype == torch.bfloat16:
-            h = h.view(torch.bfloat16)
+                raw = part if part.dtype == torch.float32 else part.view(torch.int8)
+                dist.broadcast(raw, src=self._root(root), group=self.group)
+                h[int(off):int(off) + int(n)] = raw.view(part.dtype)
         with torch.cuda.stream(stream):
             buf.copy_(h.to(buf.device))
         self.calls.append(("agv", int(sum(win_len))))

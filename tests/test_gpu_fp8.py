@@ -1,0 +1,121 @@
+"""Low-precision (fp8 E4M3, row-wise scaled) ZeRO-3 parameter all-gather.
+
+Kernels: bit-exact against a numpy/torch restatement (float32 scaling in the same order, torch's
+float8_e4m3fn round-to-nearest-even for the cast).  ZeRO-3: every rank's materialised full
+parameter equals that restatement applied row by row to the full original parameter — rows are
+scaled independently, so where the dim-0 chunk boundaries fall does not matter.
+"""
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from _zero_run import init_pg
+
+pytestmark = pytest.mark.gpu
+
+
+def fp8_rows_oracle(x: torch.Tensor):
+    """(q bytes, scales, dequantised float32) of a 2-D float tensor (CPU)."""
+    x = x.float().numpy()
+    amax = np.max(np.abs(x), axis=1).astype(np.float32)
+    inv = np.where(amax > 0, np.float32(448.0) / np.where(amax > 0, amax, 1), np.float32(1)).astype(np.float32)
+    v = np.clip((x * inv[:, None]).astype(np.float32), np.float32(-448), np.float32(448))
+    q = torch.from_numpy(v).to(torch.float8_e4m3fn)
+    sc = np.where(amax > 0, amax / np.float32(448.0), np.float32(1)).astype(np.float32)
+    deq = (q.float().numpy() * sc[:, None]).astype(np.float32)
+    return q.view(torch.uint8).numpy(), sc, deq
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("rows,row_len", [(5, 64), (3, 37), (17, 12800), (4, 8), (1, 11008)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_fp8_rows_kernels_bit_exact(gpu, rows, row_len, dtype):
+    from zero_amd import _lib
+    from zero_amd.comm import zs_dtype
+
+    g = torch.Generator().manual_seed(rows * row_len)
+    x = (torch.randn(rows, row_len, generator=g) * torch.logspace(-3, 2, rows)[:, None]).to(dtype)
+    if rows >= 4:
+        x[2] = 0  # all-zero row: scale 1
+        x[3, : min(5, row_len)] = 1e-30  # deep subnormal territory after scaling
+    q_want, sc_want, deq_want = fp8_rows_oracle(x)
+    d = x.to(gpu)
+    q = torch.empty(rows, row_len, dtype=torch.uint8, device=gpu)
+    sc = torch.empty(rows, dtype=torch.float32, device=gpu)
+    st = torch.cuda.current_stream().cuda_stream
+    _lib.call("zs_fp8_quantize_rows", d.data_ptr(), zs_dtype(dtype), q.data_ptr(), sc.data_ptr(),
+              rows, row_len, st)
+    y = torch.empty(rows, row_len, dtype=dtype, device=gpu)
+    _lib.call("zs_fp8_dequantize_rows", q.data_ptr(), sc.data_ptr(), y.data_ptr(), zs_dtype(dtype),
+              rows, row_len, st)
+    torch.cuda.synchronize()
+    assert np.array_equal(sc.cpu().numpy(), sc_want)
+    assert np.array_equal(q.cpu().numpy(), q_want)
+    want = torch.from_numpy(deq_want).to(dtype)
+    assert torch.equal(y.cpu(), want)
+
+
+def _check_materialize(rank, ws, dtype, comm=None):
+    from zero_amd import zero3
+
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(40, 24), torch.nn.ReLU(), torch.nn.Linear(24, 10)).to(dev).to(dtype)
+    full = [p.detach().cpu().clone() for p in model.parameters()]
+    kw = {"comm": comm} if comm is not None else {}
+    opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), gather_dtype="fp8", **kw)
+    for p, f in zip(model.parameters(), full):
+        man = opt.param_managers[p]
+        man.materialize()
+        torch.cuda.synchronize()
+        got = p.detach().cpu()
+        if f.dim() >= 2:
+            assert man.fp8
+            want = torch.from_numpy(fp8_rows_oracle(f)[2]).to(dtype)
+        else:
+            want = f
+        assert torch.equal(got, want), (rank, tuple(f.shape))
+        man.release()
+    # a hooked training iteration runs on fp8-gathered weights
+    zero3.register_zero3_hooks(model, opt.param_managers)
+    x = torch.randn(8, 40, device=dev).to(dtype)
+    loss = model(x).float().pow(2).mean()
+    loss.backward()
+    opt.step()
+    assert torch.isfinite(loss)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_zero3_fp8_gather_ws1(gpu, dtype):
+    init_pg(0, 1, _port())
+    try:
+        _check_materialize(0, 1, dtype)
+    finally:
+        dist.destroy_process_group()
+
+
+def _mr(rank, ws, port):
+    from conftest import PKG, REPO  # noqa: F401
+    from _gloo_comm import GlooStagedComm
+
+    torch.cuda.set_device(0)
+    init_pg(rank, ws, port)
+    _check_materialize(rank, ws, torch.bfloat16, comm=GlooStagedComm())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws", [2, 3])
+def test_zero3_fp8_gather_multirank(gpu, ws):
+    mp.spawn(_mr, args=(ws, _port()), nprocs=ws, join=True)
