@@ -168,6 +168,40 @@ def comm_sweep(comm, arena, world, red_dev, sizes_mb=(4, 16, 64, 256), iters=5):
     return rows
 
 
+def cpu_reference_adam(shapes, sample_elems: int, min_seconds: float = 8.0):
+    """The reference's own inner optimizer on the host: torch.optim.Adam on CPU (the math
+    zero2.py:120 runs on its owned params; single-tensor CPU path of torch/optim/adam.py) over the
+    same leading tensors as cpu_baseline, fp32 params + grads (the reference is fp32-only)."""
+    import numpy as np
+    import torch
+
+    n = 0
+    sel = []
+    for s in shapes:
+        k = int(np.prod(s))
+        if n + k > sample_elems and sel:
+            break
+        n += k
+        sel.append(s)
+    g = torch.Generator().manual_seed(0)
+    ps = [torch.nn.Parameter(torch.randn(s, generator=g) * 0.02) for s in sel]
+    for p in ps:
+        p.grad = torch.randn(p.shape, generator=g) * 1e-3
+    opt = torch.optim.Adam(ps, lr=1e-3)
+    opt.step()  # state allocation outside the timing
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        opt.step()
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= min_seconds or steps >= 100:
+            break
+    return dict(value=n * steps / el, unit="params/s", cores=torch.get_num_threads(),
+                kind="reference-inner-optimizer",
+                sample=f"torch.optim.Adam (CPU, fp32) over the first {n:,} params "
+                       f"({len(sel)} tensors), {steps} steps, {el:.1f} s; torch {torch.__version__}")
+
+
 class _NoComm:
     """Timing-only stand-in for the collectives (--simulate-ws): leaves buffers untouched."""
 
@@ -531,6 +565,7 @@ def main():
             out["copy_kernels"] = copy_kernels
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(shapes, args.cpu_sample)
+            out["cpu_reference_adam"] = cpu_reference_adam(shapes, args.cpu_sample)
         print(json.dumps(out), flush=True)
     dist.destroy_process_group()
 

@@ -124,3 +124,49 @@ def test_multirank_padded_buckets(gpu, variant):
 def test_multirank_ws8_ragged(gpu):
     """ws=8 over the 12-param MLP: most buckets are ragged (one reduce / broadcast per owner)."""
     mp.spawn(_mr_worker, args=(8, _port(), 2, "traj_z2_ws8_d16_distinct.npz"), nprocs=8, join=True)
+
+
+def _edge_worker(rank, ws, port, variant, buckets):
+    import sys
+    from conftest import PKG, REPO  # noqa: F401
+    from _gloo_comm import GlooStagedComm
+    from _zero_run import module_for
+    from oracle import zero_oracle as zo
+
+    torch.cuda.set_device(0)
+    init_pg(rank, ws, port)
+    dev = torch.device("cuda:0")
+    shapes = [(33,), (0,), (7, 5)]  # fewer params than ranks (rank 3 owns nothing), a 0-size param
+    g = torch.Generator().manual_seed(5)
+    init = [torch.randn(s, generator=g).numpy() for s in shapes]
+    steps = 3
+    lg = {(t, r, i): (torch.randn(s, generator=torch.Generator().manual_seed(100 * t + 10 * r + i))
+                      * 1e-2).numpy() for t in range(steps) for r in range(ws) for i, s in enumerate(shapes)}
+    want = zo.simulate(variant, ws, init, steps=steps, local_grads=lambda t, r, i: lg[(t, r, i)])
+    params = [torch.nn.Parameter(torch.from_numpy(a.copy()).to(dev)) for a in init]
+    opt = module_for(variant).ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=GlooStagedComm(),
+                                               bucket_mb=ws * 64 * 4 / (1 << 20), buckets=buckets)
+    if rank == 3:
+        assert opt.local_param_indices == []
+    for t in range(steps):
+        opt.zero_grad()
+        for i, p in enumerate(params):
+            p.grad = torch.from_numpy(lg[(t, rank, i)].copy()).to(dev)
+        opt.step()
+        for i, p in enumerate(params):
+            ref = want["params"][t][rank][i]
+            got = p.detach().cpu().numpy()
+            assert got.shape == ref.shape
+            if ref.size:
+                assert rel(got, ref) <= 1e-6, (variant, rank, t, i)
+    dist.barrier()
+    dist.destroy_process_group()
+    sys.stdout.flush()
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("buckets", ["ragged", "padded"])
+def test_multirank_fewer_params_than_ranks(gpu, variant, buckets):
+    """Edge cases of the reference's ownership rule on the device path: n < ws (empty ranks) and a
+    zero-element parameter, against the oracle's restatement of the reference."""
+    mp.spawn(_edge_worker, args=(4, _port(), variant, buckets), nprocs=4, join=True)
