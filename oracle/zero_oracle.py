@@ -131,13 +131,15 @@ def _sum_ranks(arrs):
 
 
 def simulate(variant: int, ws: int, init, xs=None, ys=None, steps: int = 10, lr: float = 1e-3,
-             local_grads=None):
+             local_grads=None, adam_kw=None):
     """Restate a ``steps``-long run of reference ZeRO-``variant`` at world size ``ws``.
 
     init: list of fp32 param arrays (identical on every rank, torch.manual_seed(0) in the fixture).
     xs, ys: per-rank inputs (used when local_grads is None: grads come from ``mlp_grads``).
     local_grads: optional callable (t, rank, i) -> that rank's local grad of param i at step t
                  (from the fixture), replacing the forward/backward.
+    adam_kw: optional callable i -> keyword arguments of ``adam_update`` for param i (its param
+             group's lr / betas / eps / weight_decay / amsgrad / maximize / decoupled).
     Returns dict with per-step params per rank, per-step reduced grads per rank (list in the
     reference's collective order), and final Adam state per rank.
     """
@@ -202,11 +204,13 @@ def simulate(variant: int, ws: int, init, xs=None, ys=None, steps: int = 10, lr:
             for r in range(ws):
                 s, e = owner_range(n, ws, r)
                 for i in range(s, e):
-                    st, m, v = state[r].get(i, (0, np.zeros_like(init[i]), np.zeros_like(init[i])))
+                    z0 = np.zeros_like(init[i])
+                    st, m, v, vm = state[r].get(i, (0, z0, z0, z0))
                     st += 1
-                    p, m, v, _ = adam_update(params[r][i], grads_for(r, i), m, v, st, lr=lr)
+                    kw = dict(lr=lr) if adam_kw is None else dict(adam_kw(i))
+                    p, m, v, vm = adam_update(params[r][i], grads_for(r, i), m, v, st, vmax=vm, **kw)
                     params[r][i] = p
-                    state[r][i] = (st, m, v)
+                    state[r][i] = (st, m, v, vm)
             for i in range(n):  # broadcast from owner (zero1.py:91-102 / zero2.py:122-133)
                 o = owner_of(n, ws, i)
                 for r in range(ws):

@@ -170,3 +170,66 @@ def test_multirank_fewer_params_than_ranks(gpu, variant, buckets):
     """Edge cases of the reference's ownership rule on the device path: n < ws (empty ranks) and a
     zero-element parameter, against the oracle's restatement of the reference."""
     mp.spawn(_edge_worker, args=(4, _port(), variant, buckets), nprocs=4, join=True)
+
+
+HP_CASES = {
+    "adamw_amsgrad_2groups": (torch.optim.AdamW, [dict(lr=1e-3, weight_decay=0.05, amsgrad=True),
+                                                  dict(lr=3e-3, weight_decay=0.0, amsgrad=True)]),
+    "adam_l2_maximize": (torch.optim.Adam, [dict(lr=2e-3, weight_decay=0.01, maximize=True)]),
+}
+
+
+def _hp_worker(rank, ws, port, variant, case):
+    import sys
+    from conftest import PKG, REPO  # noqa: F401
+    from _gloo_comm import GlooStagedComm
+    from _zero_run import module_for
+    from oracle import zero_oracle as zo
+
+    torch.cuda.set_device(0)
+    init_pg(rank, ws, port)
+    dev = torch.device("cuda:0")
+    cls, groups = HP_CASES[case]
+    shapes = [(48, 8), (48,), (20, 9), (20,), (7,), (64, 3)]
+    g = torch.Generator().manual_seed(9)
+    init = [torch.randn(s, generator=g).numpy() for s in shapes]
+    steps = 4
+    lg = {(t, r, i): (torch.randn(s, generator=torch.Generator().manual_seed(1000 * t + 10 * r + i))
+                      * 1e-2).numpy() for t in range(steps) for r in range(ws) for i, s in enumerate(shapes)}
+    group_of = [0 if i < 3 or len(groups) == 1 else 1 for i in range(len(shapes))]
+
+    def kw_of(i):
+        h = groups[group_of[i]]
+        return dict(lr=h["lr"], weight_decay=h.get("weight_decay", 0.0), amsgrad=h.get("amsgrad", False),
+                    maximize=h.get("maximize", False), decoupled=cls is torch.optim.AdamW)
+
+    want = zo.simulate(variant, ws, init, steps=steps, local_grads=lambda t, r, i: lg[(t, r, i)],
+                       adam_kw=kw_of)
+    params = [torch.nn.Parameter(torch.from_numpy(a.copy()).to(dev)) for a in init]
+    pg = [dict(params=[p for p, gi in zip(params, group_of) if gi == k], **h) for k, h in enumerate(groups)]
+    opt = module_for(variant).ShardedOptimizer(cls(pg), comm=GlooStagedComm(),
+                                               bucket_mb=ws * 128 * 4 / (1 << 20))
+    for t in range(steps):
+        opt.zero_grad()
+        for i, p in enumerate(params):
+            p.grad = torch.from_numpy(lg[(t, rank, i)].copy()).to(dev)
+        opt.step()
+        for i, p in enumerate(params):
+            assert rel(p.detach().cpu().numpy(), want["params"][t][rank][i]) <= 1e-6, (case, rank, t, i)
+    for i, (st, m, v, vm) in want["state"][rank].items():
+        s = opt.optimizer.state[params[i]]
+        assert int(s["step"].item()) == st
+        assert rel(s["exp_avg"].cpu().numpy(), m) <= 1e-6
+        if kw_of(i)["amsgrad"]:
+            assert rel(s["max_exp_avg_sq"].cpu().numpy(), vm) <= 1e-6
+    dist.barrier()
+    dist.destroy_process_group()
+    sys.stdout.flush()
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("case", sorted(HP_CASES))
+def test_multirank_hyperparameters(gpu, variant, case):
+    """AdamW / L2 weight decay / amsgrad / maximize and per-group lr through the bucketed ws=3
+    path (ragged buckets included) against the oracle's restatement of the reference."""
+    mp.spawn(_hp_worker, args=(3, _port(), variant, case), nprocs=3, join=True)

@@ -104,7 +104,7 @@ def test_simulate_with_fixture_grads(golden, variant):
                 for i in range(12):
                     assert rel(out["params"][t][r][i], z[f"r{r}_t{t}_p{i}"]) <= 1e-6, (name, t, r, i)
         for r in range(ws):  # final Adam state of owned params
-            for i, (st, m, v) in out["state"][r].items():
+            for i, (st, m, v, _) in out["state"][r].items():
                 assert int(z[f"r{r}_state_{i}_step"]) == st
                 assert rel(m, z[f"r{r}_state_{i}_exp_avg"]) <= 1e-6
                 assert rel(v, z[f"r{r}_state_{i}_exp_avg_sq"]) <= 1e-6
