@@ -511,6 +511,18 @@ def main():
             traffic_src = str(tj.relative_to(REPO) if tj.is_absolute() else tj)
 
     copy_kernels = copy_summary(copy_events, args.steps, world, red_dev) if copy_events else None
+    # step roofline: this rank's HBM bytes (Adam + pack + unpack) at 8 TB/s plus its bus bytes at
+    # the 7-link xGMI aggregate, no overlap credit; the slowest rank's sum vs the measured step
+    hbm_b = (adam_bytes + sum(b for *_, b in (copy_events or []))) / args.steps
+    bus_b = sum(ev[-1] for ev in (comm_events or [])) / args.steps
+    ideal = torch.tensor([hbm_b / (HBM_PEAK_GBS * 1e9) * 1e3 + bus_b / (XGMI_LINK_GBS * XGMI_LINKS * 1e9) * 1e3,
+                          hbm_b, bus_b], dtype=torch.float64, device=red_dev)
+    if world > 1:
+        dist.all_reduce(ideal, op=dist.ReduceOp.MAX)
+    step_roofline = {"ideal_ms": float(ideal[0]), "frac": float(ideal[0]) / ms,
+                     "hbm_gb_per_step": float(ideal[1]) / 1e9, "bus_gb_per_step": float(ideal[2]) / 1e9,
+                     "model": "per rank: (Adam + pack + unpack algorithmic bytes) / 8 TB/s + bus bytes "
+                              "/ (7 x 153 GB/s), no overlap credit; max over ranks"}
     collectives = None
     if world > 1:
         collectives = collective_summary(comm_events, args.steps, world, red_dev)
@@ -559,6 +571,7 @@ def main():
                 "traffic_source": traffic_src,
             },
         }
+        out["step_roofline"] = step_roofline
         if collectives is not None:
             out["collectives"] = collectives
         if copy_kernels is not None:
