@@ -475,6 +475,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    host_ms = (time.perf_counter() - t0) / args.steps * 1e3  # enqueue only: nothing waits
     torch.cuda.synchronize()
     dist.barrier()
     el = time.perf_counter() - t0
@@ -535,6 +536,7 @@ def main():
                           "ms_per_step": ms, "adam_achieved_gbs": achieved,
                           "adam_ms_per_step": adam_ms / args.steps, "buckets": eng.K,
                           "window_elems": eng.W, "stream_elems": eng.L,
+                          "host_enqueue_ms_per_step": host_ms,
                           "copy_kernels": copy_kernels}), flush=True)
         dist.destroy_process_group()
         return
@@ -572,6 +574,7 @@ def main():
             },
         }
         out["step_roofline"] = step_roofline
+        out["host_enqueue_ms_per_step"] = host_ms  # rank 0's Python + launch time per step
         if collectives is not None:
             out["collectives"] = collectives
         if copy_kernels is not None:
