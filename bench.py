@@ -128,6 +128,45 @@ def copy_summary(events, steps, world, red_dev):
     return out
 
 
+def comm_selfcheck(comm, world, rank, dev):
+    """Closed-form check of the RCCL communicator at this N (run before timing): in-place
+    reduce-scatter / all-gather, and the ragged bucket's grouped reduce / broadcast per owner.
+    Rank r contributes x_r[i] = r + i/1024 (exact in fp32); every result is an exact fp32 value."""
+    import torch
+
+    st = torch.cuda.Stream(device=dev)
+    n = 4096
+    i = torch.arange(world * n, device=dev, dtype=torch.float32)
+    out = {}
+    buf = rank + i / 1024
+    comm.reduce_scatter(buf, buf[rank * n:(rank + 1) * n], st)
+    st.synchronize()
+    want = world * (world - 1) / 2 + i[rank * n:(rank + 1) * n] * world / 1024
+    out["reduce_scatter"] = bool(torch.equal(buf[rank * n:(rank + 1) * n], want))
+    buf = torch.full((world * n,), -1.0, device=dev)
+    buf[rank * n:(rank + 1) * n] = rank + i[:n] / 1024
+    comm.all_gather(buf[rank * n:(rank + 1) * n], buf, st)
+    st.synchronize()
+    out["all_gather"] = bool(torch.equal(buf, (i // n) + (i % n) / 1024))
+    lens = [(r % 3 + 1) * 64 for r in range(world)]  # ragged windows, 64-element aligned
+    offs = [sum(lens[:r]) for r in range(world)]
+    tot = sum(lens)
+    buf = rank + torch.arange(tot, device=dev, dtype=torch.float32) / 1024
+    comm.reduce_v(buf, offs, lens, st)
+    st.synchronize()
+    o, m = offs[rank], lens[rank]
+    want = world * (world - 1) / 2 + torch.arange(o, o + m, device=dev, dtype=torch.float32) * world / 1024
+    out["reduce_v"] = bool(torch.equal(buf[o:o + m], want))
+    buf = torch.full((tot,), -1.0, device=dev)
+    buf[o:o + m] = rank + 0.5
+    comm.broadcast_v(buf, offs, lens, st)
+    st.synchronize()
+    want = torch.cat([torch.full((lens[r],), r + 0.5, device=dev) for r in range(world)])
+    out["broadcast_v"] = bool(torch.equal(buf, want))
+    out["ok"] = all(out.values())
+    return out
+
+
 def comm_sweep(comm, arena, world, red_dev, sizes_mb=(4, 16, 64, 256), iters=5):
     """Bucket-size sweep of in-place RCCL reduce-scatter / all-gather on the bf16 arena (the C5
     sweep of BASELINE.json, run on whatever N the bench runs): busBW = bytes*(ws-1)/ws / time."""
@@ -458,6 +497,18 @@ def main():
             else real_get(what, dm)
     opt = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), layout=args.layout,
                                bucket_mb=args.bucket_mb, sync=False, buckets=args.buckets, **kw)
+    selfcheck = None
+    if world > 1 and args.comm == "rccl":
+        from zero_amd.comm import RcclComm
+
+        probe = RcclComm()
+        selfcheck = comm_selfcheck(probe, world, rank, dev)
+        probe.close()
+        ok = torch.tensor([1.0 if selfcheck["ok"] else 0.0], device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        selfcheck["all_ranks_ok"] = bool(ok.item() == 1.0)
+        if not selfcheck["all_ranks_ok"]:
+            log(f"rank {rank}: RCCL self-check FAILED: {selfcheck}")
 
     def step():
         for p, g in zip(params, grads):
@@ -574,6 +625,8 @@ def main():
             },
         }
         out["step_roofline"] = step_roofline
+        if selfcheck is not None:
+            out["rccl_selfcheck"] = selfcheck
         out["host_enqueue_ms_per_step"] = host_ms  # rank 0's Python + launch time per step
         if collectives is not None:
             out["collectives"] = collectives

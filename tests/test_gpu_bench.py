@@ -63,3 +63,29 @@ def test_bench_zero3_training_iteration(gpu):
                 "--steps", "3", "--warmup", "1", "--no-cpu-baseline"])
     assert out["config"]["zero"] == 3 and out["value"] > 0
     assert out["roofline"]["launches_per_step"] >= 1 and out["zero3"]["gathers_per_step"] > 0
+
+
+def _selfcheck_worker(rank, ws, port):
+    import torch
+    import torch.distributed as dist
+
+    from conftest import PKG, REPO  # noqa: F401
+    from _gloo_comm import GlooStagedComm
+    from _zero_run import init_pg
+    import bench
+
+    torch.cuda.set_device(0)
+    init_pg(rank, ws, port)
+    out = bench.comm_selfcheck(GlooStagedComm(), ws, rank, torch.device("cuda:0"))
+    assert out["ok"], out
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws", [2, 3])
+def test_comm_selfcheck_logic(gpu, ws):
+    """bench.comm_selfcheck's closed-form expectations hold for a correct communicator (the
+    test-only gloo-staged one here; RCCL at N>1 in the driver's multi-GPU runs)."""
+    import torch.multiprocessing as mp
+
+    mp.spawn(_selfcheck_worker, args=(ws, _port()), nprocs=ws, join=True)
