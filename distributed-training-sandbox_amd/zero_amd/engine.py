@@ -32,6 +32,7 @@ from __future__ import annotations
 
 import numpy as np
 import torch
+from torch.profiler import record_function  # the reference's step() ranges (zero1.py:80-91)
 
 from . import _lib
 from .comm import comm_stream, zs_dtype
@@ -246,7 +247,8 @@ class ShardEngine:
         else:
             p = pptr + po.astype(np.uint64) * np.uint64(4)
             rows = self._adam_rows(idx, g, p, p, 0, so, n)
-        self._run_adam("local", rows, idx, hparams_of, stream)
+        with record_function("optimizer_step"):  # zero1.py:88
+            self._run_adam("local", rows, idx, hparams_of, stream)
 
     def _run_copy(self, kind, cs, stream):
         """Launch a pack / unpack CopySet; with timing on, bracket it with HIP events (algorithmic
@@ -298,56 +300,59 @@ class ShardEngine:
         r = self.rank
         cs = self.comm_stream
         self.ev_c0.record(cs)
-        for k in range(self.K):  # pack every bucket on the compute stream
-            s, b = self.segs[k], self.buckets[k]
-            src = np.where(has[s.param], gptr[s.param] + s.param_off.astype(np.uint64) * es, 0)
-            dst = base + np.uint64(b.arena_off) * es + s.buf_off.astype(np.uint64) * es
-            nb = s.length * self.es
-            sig = src.tobytes() + dst.tobytes()
-            self._run_copy("pack", self._cached(("pack", k), sig, lambda: CopySet(src, dst, nb)),
-                           stream)
-            self.ev_pack[k].record(stream)
-        for k in range(self.K):  # in-place reduce-scatter (-v) of each bucket
-            cs.wait_event(self.ev_pack[k])
-            self._collective(k, "rs")
-            self.ev_rs[k].record(cs)
-        for k in range(self.K):  # fused Adam on this rank's window
-            stream.wait_event(self.ev_rs[k])
-            s, b = self.segs[k], self.buckets[k]
-            own = np.nonzero(s.rank == r)[0]
-            idx = s.param[own]
-            slot = base + np.uint64(b.arena_off) * es + s.buf_off[own].astype(np.uint64) * es
-            so = (s.buf_off[own] - int(b.win_off[r])) + int(b.win_stream[r])
-            ln = s.length[own]
-            po = s.param_off[own].astype(np.uint64)
-            live = has[idx]
-            if self.mixed:
-                mst = np.uint64(self.master.data_ptr()) + so.astype(np.uint64) * np.uint64(4)
-                rows = self._adam_rows(idx, slot, mst, mst, slot, so, ln)
-            else:
-                p = pptr[idx] + po * np.uint64(4)
-                rows = self._adam_rows(idx, slot, p, slot, 0, so, ln)
-            self._run_adam(("bucket", k), rows[live], idx[live], hparams_of, stream)
-            if not live.all():  # params without a grad keep their value: copy it into the slot
-                dead = np.nonzero(~live)[0]
-                src = pptr[idx[dead]] + po[dead] * es
-                nb = ln[dead] * self.es
-                self._cached(("pass", k), src.tobytes() + slot[dead].tobytes(),
-                             lambda: CopySet(src, slot[dead], nb)).run(stream)
-            self.ev_adam[k].record(stream)
-        for k in range(self.K):  # in-place all-gather (-v) of the updated windows
-            cs.wait_event(self.ev_adam[k])
-            self._collective(k, "ag")
-            self.ev_ag[k].record(cs)
-        self.ev_c1.record(cs)
-        for k in range(self.K):  # scatter every bucket back into module storage
-            stream.wait_event(self.ev_ag[k])
-            s, b = self.segs[k], self.buckets[k]
-            src = base + np.uint64(b.arena_off) * es + s.buf_off.astype(np.uint64) * es
-            dst = pptr[s.param] + s.param_off.astype(np.uint64) * es
-            self._run_copy("unpack", self._cached(("unpack", k), dst.tobytes(),
-                                                  lambda: CopySet(src, dst, s.length * self.es)),
-                           stream)
+        with record_function("all_reduce_gradients"):  # zero1.py:80-84: pack + reduce-scatter
+            for k in range(self.K):  # pack every bucket on the compute stream
+                s, b = self.segs[k], self.buckets[k]
+                src = np.where(has[s.param], gptr[s.param] + s.param_off.astype(np.uint64) * es, 0)
+                dst = base + np.uint64(b.arena_off) * es + s.buf_off.astype(np.uint64) * es
+                nb = s.length * self.es
+                sig = src.tobytes() + dst.tobytes()
+                pack = self._cached(("pack", k), sig, lambda: CopySet(src, dst, nb))
+                self._run_copy("pack", pack, stream)
+                self.ev_pack[k].record(stream)
+            for k in range(self.K):  # in-place reduce-scatter (-v) of each bucket
+                cs.wait_event(self.ev_pack[k])
+                self._collective(k, "rs")
+                self.ev_rs[k].record(cs)
+        with record_function("optimizer_step"):  # zero1.py:88
+            for k in range(self.K):  # fused Adam on this rank's window
+                stream.wait_event(self.ev_rs[k])
+                s, b = self.segs[k], self.buckets[k]
+                own = np.nonzero(s.rank == r)[0]
+                idx = s.param[own]
+                slot = base + np.uint64(b.arena_off) * es + s.buf_off[own].astype(np.uint64) * es
+                so = (s.buf_off[own] - int(b.win_off[r])) + int(b.win_stream[r])
+                ln = s.length[own]
+                po = s.param_off[own].astype(np.uint64)
+                live = has[idx]
+                if self.mixed:
+                    mst = np.uint64(self.master.data_ptr()) + so.astype(np.uint64) * np.uint64(4)
+                    rows = self._adam_rows(idx, slot, mst, mst, slot, so, ln)
+                else:
+                    p = pptr[idx] + po * np.uint64(4)
+                    rows = self._adam_rows(idx, slot, p, slot, 0, so, ln)
+                self._run_adam(("bucket", k), rows[live], idx[live], hparams_of, stream)
+                if not live.all():  # params without a grad keep their value: copy it into the slot
+                    dead = np.nonzero(~live)[0]
+                    src = pptr[idx[dead]] + po[dead] * es
+                    nb = ln[dead] * self.es
+                    self._cached(("pass", k), src.tobytes() + slot[dead].tobytes(),
+                                 lambda: CopySet(src, slot[dead], nb)).run(stream)
+                self.ev_adam[k].record(stream)
+        with record_function("broadcast_parameters"):  # zero1.py:91-102: all-gather + unpack
+            for k in range(self.K):  # in-place all-gather (-v) of the updated windows
+                cs.wait_event(self.ev_adam[k])
+                self._collective(k, "ag")
+                self.ev_ag[k].record(cs)
+            self.ev_c1.record(cs)
+            for k in range(self.K):  # scatter every bucket back into module storage
+                stream.wait_event(self.ev_ag[k])
+                s, b = self.segs[k], self.buckets[k]
+                src = base + np.uint64(b.arena_off) * es + s.buf_off.astype(np.uint64) * es
+                dst = pptr[s.param] + s.param_off.astype(np.uint64) * es
+                unpack = self._cached(("unpack", k), dst.tobytes(),
+                                      lambda: CopySet(src, dst, s.length * self.es))
+                self._run_copy("unpack", unpack, stream)
 
     # ------------------------------------------------------------------------------------------
     # backward-overlapped mode: grads reduced to their owner from

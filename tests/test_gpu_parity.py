@@ -233,3 +233,18 @@ def test_multirank_hyperparameters(gpu, variant, case):
     """AdamW / L2 weight decay / amsgrad / maximize and per-group lr through the bucketed ws=3
     path (ragged buckets included) against the oracle's restatement of the reference."""
     mp.spawn(_hp_worker, args=(3, _port(), variant, case), nprocs=3, join=True)
+
+
+def test_profiler_ranges_match_reference_names(gpu, pg1):
+    """torch.profiler shows the reference's step() ranges (zero1.py:80-91) around the native work."""
+    from torch.profiler import ProfilerActivity, profile
+    from zero_amd import zero2
+
+    ps = [torch.nn.Parameter(torch.randn(256, 64, device=gpu)) for _ in range(3)]
+    opt = zero2.ShardedOptimizer(torch.optim.Adam(ps, lr=1e-3))
+    for p in ps:
+        p.grad = torch.randn_like(p)
+    with profile(activities=[ProfilerActivity.CPU]) as prof:
+        opt.step()
+    names = {e.name for e in prof.events()}
+    assert "optimizer_step" in names
