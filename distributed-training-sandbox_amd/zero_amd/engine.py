@@ -397,15 +397,18 @@ class ShardEngine:
                 slot = base + gb.slot[idx].astype(np.uint64) * es
                 so = np.array([self._so_of[int(i)] for i in idx], np.int64)
                 ln = np.array([self.params[int(i)].numel() for i in idx], np.int64)
+                p = np.fromiter((_ptr(self.params[int(i)]) for i in idx), np.uint64, len(idx))
+                # ws > 1: the updated params go into the slot, which the broadcast sends; ws == 1:
+                # straight into module storage (no broadcast, no unpack)
+                out = slot if self.ws > 1 else p
                 if self.mixed:
                     mst = np.uint64(self.master.data_ptr()) + so.astype(np.uint64) * np.uint64(4)
-                    rows = self._adam_rows(idx, slot, mst, mst, slot, so, ln)
+                    rows = self._adam_rows(idx, slot, mst, mst, out, so, ln)
                 else:
-                    p = np.fromiter((_ptr(self.params[int(i)]) for i in idx), np.uint64, len(idx))
-                    rows = self._adam_rows(idx, slot, p, slot, 0, so, ln)
+                    rows = self._adam_rows(idx, slot, p, out, 0, so, ln)
                 self._run_adam(("overlap", k), rows, idx, hparams_of, stream)
             dead = [i for i in gb.groups[k] if not has[i]]
-            if dead:  # params without a grad keep their value: copy it into the slot
+            if dead and self.ws > 1:  # params without a grad keep their value: copy into the slot
                 src = [_ptr(self.params[i]) for i in dead]
                 dst = [int(base) + int(gb.slot[i]) * self.es for i in dead]
                 self._cached(("opass", k), np.array(src + dst, np.uint64).tobytes(),
@@ -426,11 +429,8 @@ class ShardEngine:
                     self.comm_events.append(("ag", False, e0, e1, region.numel() * self.es))
                 self.ev_obc[k].record(cs)
             self.ev_c1.record(cs)
-        for k in range(gb.K):  # unpack updated params into module storage
-            if self.ws > 1:
-                stream.wait_event(self.ev_obc[k])
-            elif gb.key[k] != r:
-                continue
+        for k in range(gb.K if self.ws > 1 else 0):  # unpack updated params into module storage
+            stream.wait_event(self.ev_obc[k])
             g = gb.groups[k]
             src = [int(base) + int(gb.slot[i]) * self.es for i in g]
             dst = [_ptr(self.params[i]) for i in g]

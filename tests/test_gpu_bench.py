@@ -2,13 +2,12 @@
 one GPU through the test-only gloo-staged communicator) and the ws=8 bucket path at scale."""
 import json
 import os
-import socket
 import subprocess
 import sys
 
 import pytest
 
-from conftest import REPO
+from conftest import REPO, free_port
 
 pytestmark = pytest.mark.gpu
 
@@ -26,11 +25,7 @@ def _run(cmd, timeout=240):
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    return free_port()
 
 
 def test_bench_json_line_n1(gpu):

@@ -5,7 +5,6 @@ float8_e4m3fn round-to-nearest-even for the cast).  ZeRO-3: every rank's materia
 parameter equals that restatement applied row by row to the full original parameter — rows are
 scaled independently, so where the dim-0 chunk boundaries fall does not matter.
 """
-import socket
 
 import numpy as np
 import pytest
@@ -13,6 +12,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from conftest import free_port
 from _zero_run import init_pg
 
 pytestmark = pytest.mark.gpu
@@ -31,11 +31,7 @@ def fp8_rows_oracle(x: torch.Tensor):
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    return free_port()
 
 
 @pytest.mark.parametrize("rows,row_len", [(5, 64), (3, 37), (17, 12800), (4, 8), (1, 11008)])

@@ -6,7 +6,6 @@ ZeRO: the reference trajectories (tests/golden) are replayed through a real back
 cases share the one GPU through the test-only gloo-staged communicator, as in test_gpu_parity.
 DDP: every rank's averaged grads against numpy (sum over ranks in rank order, then / ws).
 """
-import socket
 
 import numpy as np
 import pytest
@@ -14,18 +13,14 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from conftest import GOLDEN
+from conftest import GOLDEN, free_port
 from _zero_run import init_pg, run_backward
 
 pytestmark = pytest.mark.gpu
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    return free_port()
 
 
 @pytest.fixture

@@ -5,7 +5,6 @@ Multi-rank cases run ws processes on the one GPU of the box: pack / fused Adam /
 real HIP kernels, the exchange goes through tests/_gloo_comm.py (RCCL cannot put two ranks of a
 communicator on one device).  Tolerance: 1e-6 normwise relative (north star), every step.
 """
-import socket
 
 import numpy as np
 import pytest
@@ -13,18 +12,14 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from conftest import GOLDEN
+from conftest import GOLDEN, free_port
 from _zero_run import init_pg, rel, run_injected
 
 pytestmark = pytest.mark.gpu
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    return free_port()
 
 
 @pytest.fixture

@@ -1,6 +1,5 @@
 """ZeRO-3 drop-in on the MI355X vs the reference (tests/golden/traj_z3_*) and, in update mode,
 vs data-parallel Adam (the ZeRO-2 fixtures, sliced to each rank's dim-0 chunk)."""
-import socket
 
 import numpy as np
 import pytest
@@ -8,18 +7,14 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from conftest import GOLDEN
+from conftest import GOLDEN, free_port
 from _zero_run import init_pg, rel
 
 pytestmark = pytest.mark.gpu
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    return free_port()
 
 
 def _model(z, dev):

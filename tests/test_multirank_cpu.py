@@ -7,7 +7,6 @@ the rank-major buffer so each rank receives its own window (ragged buckets: one 
 the ZeRO-1 carry folded in), write the updated params into the window, all-gather, unpack.  The
 device kernels themselves are covered by the -m gpu tests.
 """
-import socket
 
 import numpy as np
 import pytest
@@ -15,15 +14,11 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from conftest import GOLDEN
+from conftest import GOLDEN, free_port
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    return free_port()
 
 
 def _worker(rank, ws, port, variant, name, window, buckets="ragged"):
