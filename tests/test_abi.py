@@ -67,3 +67,30 @@ def test_invalid_step_rejected():
 
     with pytest.raises(ZeroAmdError):
         adam_hparams(1e-3, 0.9, 0.999, 1e-8, 0.0, 0)
+
+
+def test_new_entry_points_validate_arguments():
+    """ABI v2 entry points reject bad arguments with ZS_ERR_INVALID and a message, without a GPU."""
+    from zero_amd import _lib
+
+    lib = _lib.lib
+    h = ctypes.c_void_p()
+    numels = (ctypes.c_int64 * 2)(4, 4)
+    assert lib.zs_plan_create(2, numels, None, 2, 0, 0, 64, 0, 7, ctypes.byref(h)) == _lib.ZS_ERR_INVALID
+    assert b"bucket_mode" in lib.zs_last_error()
+    assert lib.zs_scale(None, 16, 9, 2.0, 0) == _lib.ZS_ERR_INVALID
+    assert lib.zs_scale(None, 16, _lib.ZS_F32, 0.0, 0) == _lib.ZS_ERR_INVALID
+    assert lib.zs_scale(None, 0, _lib.ZS_F32, 2.0, 0) == _lib.ZS_OK  # empty: nothing to launch
+    assert lib.zs_fp8_quantize_rows(None, 9, None, None, 1, 8, 0) == _lib.ZS_ERR_INVALID
+    assert lib.zs_fp8_dequantize_rows(None, None, None, _lib.ZS_BF16, 1, 8, 0) == _lib.ZS_ERR_INVALID
+    assert b"NULL" in lib.zs_last_error()
+    assert lib.zs_fp8_quantize_rows(None, _lib.ZS_BF16, None, None, 0, 8, 0) == _lib.ZS_OK
+    assert lib.zs_reduce(None, None, None, 4, _lib.ZS_F32, 0, 0) == _lib.ZS_ERR_INVALID
+    assert lib.zs_broadcast(None, None, None, 4, _lib.ZS_F32, 0, 0) == _lib.ZS_ERR_INVALID
+    from zero_amd.plan import Plan
+
+    plan = Plan([100, 300, 5], 2, 0, window_elems=64)
+    ao, el, ev = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int()
+    arr = (ctypes.c_int64 * 2)()
+    assert lib.zs_plan_bucket(plan._h, plan.num_buckets, ctypes.byref(ao), ctypes.byref(el),
+                              ctypes.byref(ev), arr, arr, arr) == _lib.ZS_ERR_INVALID
