@@ -243,3 +243,20 @@ def test_profiler_ranges_match_reference_names(gpu, pg1):
         opt.step()
     names = {e.name for e in prof.events()}
     assert "optimizer_step" in names
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3])
+def test_reference_harness_runs(gpu, variant):
+    """zero_amd.harness: the reference's train() / test_zeroN() experiment (shrunken) on one GPU,
+    through the same CLI a user would call; the sharded run reports its timing summary."""
+    import subprocess
+    import sys
+
+    from conftest import PKG
+
+    env = dict(__import__("os").environ, MASTER_PORT=str(_port()), PYTHONPATH=str(PKG))
+    r = subprocess.run([sys.executable, "-m", "zero_amd.harness", "--zero", str(variant),
+                        "--width", "512", "--steps", "3"], capture_output=True, text=True,
+                       timeout=180, env=env, cwd=str(PKG))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "Memory Usage Summary" in r.stdout and "Average step time" in r.stdout
