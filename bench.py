@@ -434,8 +434,10 @@ def main():
                     help="DIAGNOSTIC (N=1 only): run the ws>1 bucket path of rank 0 of a ws-rank job "
                          "with the collectives replaced by no-ops, to time pack / Adam / unpack "
                          "at that layout; prints a diagnostic line, not the metric")
-    ap.add_argument("--comm", default="rccl", choices=["rccl", "gloo-staged"],
-                    help="gloo-staged = TEST ONLY (tests/_gloo_comm.py): N ranks sharing one GPU")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "c10d", "gloo-staged"],
+                    help="rccl: the library's own RCCL communicator; c10d: the same RCCL through "
+                         "torch.distributed (A/B); gloo-staged = TEST ONLY (tests/_gloo_comm.py): "
+                         "N ranks sharing one GPU")
     ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "r01_c4_n1_adam_pmc.json"),
                     help="PMC HBM-bytes summary (profiles/*.json) for the roofline 'traffic' field")
     args = ap.parse_args()
@@ -458,7 +460,7 @@ def main():
     dev = torch.device("cuda", local)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29531")
-    use_nccl = world > 1 and args.comm == "rccl"
+    use_nccl = world > 1 and args.comm in ("rccl", "c10d")
     dist.init_process_group("nccl" if use_nccl else "gloo", rank=rank, world_size=world,
                             device_id=dev if use_nccl else None)
 
@@ -483,11 +485,24 @@ def main():
     torch.cuda.synchronize()
     mod = zero1 if args.zero == 1 else zero2
     kw = {}
+    comm_used = None
     if args.comm == "gloo-staged" and world > 1:
         sys.path.insert(0, str(REPO / "tests"))
         from _gloo_comm import GlooStagedComm
 
         kw["comm"] = GlooStagedComm()
+        comm_used = "gloo-staged (test only)"
+    elif world > 1:
+        from zero_amd.comm import C10dComm, RcclComm
+
+        if args.comm == "c10d":
+            kw["comm"], comm_used = C10dComm(), "c10d"
+        else:
+            try:
+                kw["comm"], comm_used = RcclComm(), "rccl"
+            except Exception as e:  # keep measuring on the same RCCL, through torch's communicator
+                log(f"rank {rank}: RcclComm failed ({e}); falling back to C10dComm")
+                kw["comm"], comm_used = C10dComm(), f"c10d (RcclComm failed: {e})"
     if args.simulate_ws > 1:
         assert world == 1, "--simulate-ws is a single-GPU diagnostic"
         kw["comm"] = _NoComm(args.simulate_ws)
@@ -498,12 +513,8 @@ def main():
     opt = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), layout=args.layout,
                                bucket_mb=args.bucket_mb, sync=False, buckets=args.buckets, **kw)
     selfcheck = None
-    if world > 1 and args.comm == "rccl":
-        from zero_amd.comm import RcclComm
-
-        probe = RcclComm()
-        selfcheck = comm_selfcheck(probe, world, rank, dev)
-        probe.close()
+    if world > 1 and args.comm in ("rccl", "c10d"):
+        selfcheck = comm_selfcheck(kw["comm"], world, rank, dev)
         ok = torch.tensor([1.0 if selfcheck["ok"] else 0.0], device=dev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         selfcheck["all_ranks_ok"] = bool(ok.item() == 1.0)
@@ -578,7 +589,7 @@ def main():
     collectives = None
     if world > 1:
         collectives = collective_summary(comm_events, args.steps, world, red_dev)
-        if args.comm == "rccl" and not args.no_comm_sweep:
+        if args.comm in ("rccl", "c10d") and not args.no_comm_sweep:
             collectives["sweep"] = comm_sweep(opt._comm, eng.arena, world, red_dev)
 
     if rank == 0 and args.simulate_ws > 1:
@@ -613,7 +624,7 @@ def main():
                 "state_dtype": "fp32 (master, exp_avg, exp_avg_sq)",
                 "zero": args.zero, "layout": args.layout, "bucket_mb": args.bucket_mb,
                 "bucket_mode": args.buckets,
-                "buckets": eng.K, "parallelism": f"dp{world}",
+                "buckets": eng.K, "parallelism": f"dp{world}", "comm": comm_used,
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -124,3 +124,67 @@ class RcclComm:
     def all_reduce(self, t: torch.Tensor, stream) -> None:
         _lib.call("zs_all_reduce", self._h, t.data_ptr(), t.data_ptr(), t.numel(),
                   zs_dtype(t.dtype), stream_handle(stream))
+
+
+class C10dComm:
+    """The same interface over torch.distributed's own communicator of ``group`` (RCCL under the
+    "nccl" backend): every call is issued with ``stream`` as torch's current stream, so c10d
+    orders its internal collective stream after the caller's work and the caller's later work
+    after the collective.  An A/B baseline for RcclComm (one extra stream hop per call), and the
+    bench's fallback if a dedicated communicator cannot be created."""
+
+    def __init__(self, group=None):
+        self.group_ = group
+        self.ws = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+
+    def _root(self, r):
+        return dist.get_global_rank(self.group_, r) if self.group_ is not None else r
+
+    @contextlib.contextmanager
+    def group(self):
+        yield  # c10d collectives are issued one by one
+
+    def reduce_scatter(self, send, recv, stream):
+        with torch.cuda.stream(stream):
+            if recv.data_ptr() == send.data_ptr() + self.rank * recv.numel() * recv.element_size():
+                out = torch.empty_like(recv)  # c10d has no in-place reduce-scatter
+                dist.reduce_scatter_tensor(out, send, group=self.group_)
+                recv.copy_(out)
+            else:
+                dist.reduce_scatter_tensor(recv, send, group=self.group_)
+
+    def all_gather(self, send, recv, stream):
+        with torch.cuda.stream(stream):
+            dist.all_gather_into_tensor(recv, send.clone() if _overlaps(send, recv) else send,
+                                        group=self.group_)
+
+    def all_reduce(self, t, stream):
+        with torch.cuda.stream(stream):
+            dist.all_reduce(t, group=self.group_)
+
+    def reduce(self, t, root, stream):
+        with torch.cuda.stream(stream):
+            dist.reduce(t, dst=self._root(root), group=self.group_)
+
+    def broadcast(self, t, root, stream):
+        with torch.cuda.stream(stream):
+            dist.broadcast(t, src=self._root(root), group=self.group_)
+
+    def reduce_v(self, buf, win_off, win_len, stream):
+        for root, (off, n) in enumerate(zip(win_off, win_len)):
+            if n:
+                self.reduce(buf[int(off):int(off) + int(n)], root, stream)
+
+    def broadcast_v(self, buf, win_off, win_len, stream):
+        for root, (off, n) in enumerate(zip(win_off, win_len)):
+            if n:
+                self.broadcast(buf[int(off):int(off) + int(n)], root, stream)
+
+    def close(self):
+        pass
+
+
+def _overlaps(a: torch.Tensor, b: torch.Tensor) -> bool:
+    a0, b0 = a.data_ptr(), b.data_ptr()
+    return a0 < b0 + b.numel() * b.element_size() and b0 < a0 + a.numel() * a.element_size()

@@ -84,3 +84,25 @@ def test_comm_selfcheck_logic(gpu, ws):
     import torch.multiprocessing as mp
 
     mp.spawn(_selfcheck_worker, args=(ws, _port()), nprocs=ws, join=True)
+
+
+def test_comm_backends_selfcheck_ws1(gpu):
+    """RcclComm and the C10dComm A/B backend pass the bench's closed-form self-check on an "nccl"
+    (RCCL) process group of one rank."""
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    from zero_amd.comm import C10dComm, RcclComm
+
+    import os
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        for comm in (RcclComm(), C10dComm()):
+            out = bench.comm_selfcheck(comm, 1, 0, torch.device("cuda:0"))
+            assert out["ok"], (type(comm).__name__, out)
+            comm.close()
+    finally:
+        dist.destroy_process_group()
