@@ -166,6 +166,8 @@ class Zero3ParamManager:
             return (q, sc, torch.empty(ws * self.S, dtype=torch.uint8, device=dev),
                     torch.empty(ws * self.cs, dtype=torch.float32, device=dev))
         send = self.shard.reshape(-1)
+        if ws == 1:  # the shard is the whole parameter: nothing to gather
+            return (send, send)
         if send.numel() != self.S:  # short / empty last chunks: pad so every rank sends S elements
             pad = torch.zeros(self.S, dtype=send.dtype, device=dev)
             pad[:send.numel()].copy_(send)
@@ -179,7 +181,8 @@ class Zero3ParamManager:
             comm.all_gather(sc, full_sc, stream)
         else:
             send, full = st
-            comm.all_gather(send, full, stream)
+            if full is not send:
+                comm.all_gather(send, full, stream)
 
     def _gather_finish(self, stream, st):
         if not self.fp8:
