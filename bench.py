@@ -636,6 +636,8 @@ def main():
             },
         }
         out["step_roofline"] = step_roofline
+        out["placement"] = {"state": eng.placement,
+                            "arena": getattr(eng, "arena_placement", None)}
         if selfcheck is not None:
             out["rccl_selfcheck"] = selfcheck
         out["host_enqueue_ms_per_step"] = host_ms  # rank 0's Python + launch time per step

@@ -46,10 +46,52 @@ def _ptr(t: torch.Tensor | None) -> int:
     return 0 if t is None else int(t.data_ptr())
 
 
+PROBE_MIN_BYTES = 1 << 30
+
+
+def probed_zeros(n: int, dtype, device, tries: int = 3):
+    """A zero-filled buffer for a long-lived, bandwidth-bound stream, placed by measurement.
+
+    The same C4 Adam launch over different allocations of its state measured 13.9 ms on some and
+    15.1-15.6 ms on others in one process, and an in-place copy over the allocation alone predicts
+    which (6.26 vs 5.3-5.7 TB/s; profiles/r01_alloc_probe.log).  So for buffers of 1 GiB or more,
+    up to ``tries`` candidates are allocated (each while the previous ones are still held, so each
+    is new memory), streamed once with the gfx950 copy kernel in place, and the fastest is kept;
+    the others go back to torch's caching allocator.  Skipped when free memory is short.
+    Returns (buffer, info dict)."""
+    nbytes = n * torch.empty((), dtype=dtype).element_size()
+    info = {"tries": 1, "gbs": []}
+    if tries <= 1 or nbytes < PROBE_MIN_BYTES:
+        return torch.zeros(n, dtype=dtype, device=device), info
+    free, _ = torch.cuda.mem_get_info(device)
+    tries = int(min(tries, max(1, (free - (2 << 30)) // nbytes)))
+    if tries <= 1:
+        return torch.zeros(n, dtype=dtype, device=device), info
+    stream = torch.cuda.current_stream(device)
+    cands = []
+    for _ in range(tries):
+        buf = torch.zeros(n, dtype=dtype, device=device)
+        probe = CopySet([buf.data_ptr()], [buf.data_ptr()], [nbytes])  # read + write, unchanged
+        probe.run(stream)  # warm (first touch)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        probe.run(stream)
+        e1.record(stream)
+        e1.synchronize()
+        gbs = 2 * nbytes / (e0.elapsed_time(e1) / 1e3) / 1e9
+        cands.append((gbs, buf))
+        info["gbs"].append(round(gbs, 1))
+    best = max(range(len(cands)), key=lambda i: cands[i][0])
+    buf = cands[best][1]
+    del cands
+    info.update(tries=tries, chosen=best)
+    return buf, info
+
+
 class ShardEngine:
     def __init__(self, params, group_of, ws: int, rank: int, *, layout="reference", carry=False,
                  comm=None, bucket_bytes: int = 256 << 20, align: int = ALIGN_ELEMS,
-                 buckets: str = "ragged"):
+                 buckets: str = "ragged", placement_tries: int = 3):
         if not params:
             raise ValueError("ShardEngine: no parameters")
         dev = params[0].device
@@ -83,17 +125,19 @@ class ShardEngine:
         self.L = self.plan.stream_len(rank)
         self.pieces = self.plan.pieces(rank)
 
-        f32 = dict(dtype=torch.float32, device=dev)
-        self.m = torch.zeros(self.L, **f32)
-        self.v = torch.zeros(self.L, **f32)
+        # exp_avg, exp_avg_sq (+ fp32 master, + ZeRO-1 carry): one allocation, placed by probe
+        nbuf = 2 + int(self.mixed) + int(bool(carry))
+        self.state, self.placement = probed_zeros(nbuf * self.L, torch.float32, dev, placement_tries)
+        views = iter(self.state.split(self.L) if self.L else [self.state] * nbuf)
+        self.m, self.v = next(views), next(views)
         self.vmax = None
-        self.carry = torch.zeros(self.L, **f32) if carry else None
-        self.master = None
+        self.master = next(views) if self.mixed else None
+        self.carry = next(views) if carry else None
         if self.mixed:
-            self.master = torch.zeros(self.L, **f32)
             for i, po, so, n in zip(*self._piece_cols()):
                 self.master[so:so + n].copy_(params[i].detach().reshape(-1)[po:po + n])
         self.arena = None  # allocated on the first bucketed step (not at all in overlap mode)
+        self.placement_tries = placement_tries
         if ws > 1:
             self.buckets = [self.plan.bucket(k) for k in range(self.K)]
             self.segs = [self.plan.segments(k) for k in range(self.K)]
@@ -293,7 +337,8 @@ class ShardEngine:
 
     def _step_buckets(self, gptr, has, hparams_of, stream):
         if self.arena is None:
-            self.arena = torch.zeros(self.plan.arena_elems, dtype=self.dtype, device=self.device)
+            self.arena, self.arena_placement = probed_zeros(self.plan.arena_elems, self.dtype,
+                                                            self.device, self.placement_tries)
         es = np.uint64(self.es)
         pptr = np.fromiter((_ptr(p) for p in self.params), np.uint64, len(self.params))
         base = np.uint64(self.arena.data_ptr())
