@@ -88,7 +88,9 @@ class GradBuckets:
                                               self.es, order=order, align=align)
         self.K = len(self.groups)
         off = int(self.bucket_off[-1] + self.bucket_len[-1])
-        self.buf = torch.zeros(max(off, align), dtype=self.dtype, device=self.device)
+        from .engine import probed_zeros  # grads stream through Adam every step: place by probe
+
+        self.buf, self.placement = probed_zeros(max(off, align), self.dtype, self.device)
         self.comm_stream = comm_stream(self.device)
         self.ev_ready = [torch.cuda.Event() for _ in range(self.K)]
         self.ev_done = [torch.cuda.Event() for _ in range(self.K)]

@@ -36,7 +36,7 @@ from torch.optim import Optimizer
 from . import _lib
 from .comm import RcclComm, comm_stream, zs_dtype
 from .kernels import stream_handle
-from .engine import ALIGN_ELEMS
+from .engine import ALIGN_ELEMS, probed_zeros
 from .kernels import AdamSet, adam_hparams
 from .plan import Plan
 from ._sharded import adam_group_hparams
@@ -324,13 +324,15 @@ class ShardedOptimizer:
         plan = Plan(numels, self.world_size, self.rank, "chunk", dim0=dim0, align_elems=ALIGN_ELEMS)
         L = plan.stream_len(self.rank)
         pc = plan.pieces(self.rank)
-        eng = dict(plan=plan, pieces=pc, L=L, dtype=dtype,
-                   m=torch.zeros(L, dtype=torch.float32, device=dev),
-                   v=torch.zeros(L, dtype=torch.float32, device=dev),
+        nbuf = 3 if dtype == torch.bfloat16 else 2  # exp_avg, exp_avg_sq (+ fp32 master)
+        state, placement = probed_zeros(nbuf * L, torch.float32, dev)
+        views = list(state.split(L)) if L else [state] * nbuf
+        eng = dict(plan=plan, pieces=pc, L=L, dtype=dtype, state=state, placement=placement,
+                   m=views[0], v=views[1],
                    vmax=None, gshard=torch.zeros(L, dtype=dtype, device=dev), master=None,
                    steps=np.zeros(len(self.params), np.int64), cache={}, retired=[])
         if dtype == torch.bfloat16:
-            eng["master"] = torch.zeros(L, dtype=torch.float32, device=dev)
+            eng["master"] = views[2]
             for i, so, ln in zip(pc.param, pc.stream_off, pc.length):
                 if ln:
                     eng["master"][so:so + ln].copy_(self.param_managers[self.params[i]].shard.reshape(-1).float())
