@@ -49,7 +49,7 @@ def _ptr(t: torch.Tensor | None) -> int:
 PROBE_MIN_BYTES = 1 << 30
 
 
-def probed_zeros(n: int, dtype, device, tries: int = 3):
+def probed_zeros(n: int, dtype, device, tries: int = 5):
     """A zero-filled buffer for a long-lived, bandwidth-bound stream, placed by measurement.
 
     The same C4 Adam launch over different allocations of its state measured 13.9 ms on some and
@@ -63,8 +63,9 @@ def probed_zeros(n: int, dtype, device, tries: int = 3):
     info = {"tries": 1, "gbs": []}
     if tries <= 1 or nbytes < PROBE_MIN_BYTES:
         return torch.zeros(n, dtype=dtype, device=device), info
-    free, _ = torch.cuda.mem_get_info(device)
-    tries = int(min(tries, max(1, (free - (2 << 30)) // nbytes)))
+    free, total = torch.cuda.mem_get_info(device)
+    # candidates are held together: keep a quarter of the device (and 2 GiB) out of it
+    tries = int(min(tries, max(1, (free - max(total // 4, 2 << 30)) // nbytes)))
     if tries <= 1:
         return torch.zeros(n, dtype=dtype, device=device), info
     stream = torch.cuda.current_stream(device)
@@ -91,7 +92,7 @@ def probed_zeros(n: int, dtype, device, tries: int = 3):
 class ShardEngine:
     def __init__(self, params, group_of, ws: int, rank: int, *, layout="reference", carry=False,
                  comm=None, bucket_bytes: int = 256 << 20, align: int = ALIGN_ELEMS,
-                 buckets: str = "ragged", placement_tries: int = 3):
+                 buckets: str = "ragged", placement_tries: int = 5):
         if not params:
             raise ValueError("ShardEngine: no parameters")
         dev = params[0].device
