@@ -188,6 +188,7 @@ def comm_sweep(comm, arena, world, red_dev, sizes_mb=(4, 16, 64, 256), iters=5):
                 (lambda: comm.all_gather(mine, buf, st))
             op()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()  # nothing of ours in flight while c10d's barrier runs
             dist.barrier()
             torch.cuda.synchronize()
             e0.record(st)
@@ -303,6 +304,7 @@ def bench_zero3(args, world, rank, dev, use_nccl):
     for _ in range(args.warmup):
         step()
     opt.timing_events = []
+    torch.cuda.synchronize()  # warmup drained first: no collective of ours beside c10d's barrier
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -366,6 +368,7 @@ def bench_train_smollm3(args, world, rank, dev, use_nccl):
     opt.zero_grad()
     for _ in range(args.warmup):
         sm.train_step(model, opt, ids)
+    torch.cuda.synchronize()  # warmup drained first: no collective of ours beside c10d's barrier
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -532,6 +535,7 @@ def main():
     eng.timing_events = []
     eng.comm_events = [] if world > 1 or args.simulate_ws > 1 else None
     eng.copy_events = [] if world > 1 or args.simulate_ws > 1 else None
+    torch.cuda.synchronize()  # warmup drained first: no collective of ours beside c10d's barrier
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
