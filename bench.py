@@ -167,6 +167,37 @@ def comm_selfcheck(comm, world, rank, dev):
     return out
 
 
+def _checked_comm(kw, world, rank, dev):
+    """Run comm_selfcheck on kw["comm"] (AND-ed over ranks) before anything is measured.  If the
+    library's own communicator gets any closed-form result wrong on any rank, every rank switches
+    to the same RCCL through torch.distributed (C10dComm) — a wrong exchange is never timed — and
+    the check is repeated there.  Returns the report (incl. "comm_used" when it switched)."""
+    import torch
+    import torch.distributed as dist
+
+    from zero_amd.comm import C10dComm, RcclComm
+
+    def check(comm):
+        out = comm_selfcheck(comm, world, rank, dev)
+        ok = torch.tensor([1.0 if out["ok"] else 0.0], device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        out["all_ranks_ok"] = bool(ok.item() == 1.0)
+        return out
+
+    out = check(kw["comm"])
+    if not out["all_ranks_ok"] and isinstance(kw["comm"], RcclComm):
+        log(f"rank {rank}: RcclComm self-check FAILED ({out}); measuring through C10dComm")
+        kw["comm"].close()
+        kw["comm"] = C10dComm()
+        failed = out
+        out = check(kw["comm"])
+        out["rccl_comm_failed"] = failed
+        out["comm_used"] = "c10d (RcclComm failed its self-check)"
+    elif not out["all_ranks_ok"]:
+        log(f"rank {rank}: communicator self-check FAILED: {out}")
+    return out
+
+
 def comm_sweep(comm, arena, world, red_dev, sizes_mb=(4, 16, 64, 256), iters=5):
     """Bucket-size sweep of in-place RCCL reduce-scatter / all-gather on the bf16 arena (the C5
     sweep of BASELINE.json, run on whatever N the bench runs): busBW = bytes*(ws-1)/ws / time."""
@@ -411,8 +442,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C4", choices=["C2", "C3", "C4", "C5"])
     ap.add_argument("--zero", type=int, default=2, choices=[1, 2, 3],
-                    help="3 = a ZeRO-3 training iteration (hooked forward/backward + update-mode "
-                         "step) of the MLP configs C2/C3 (BASELINE.json configs[2])")
+                    help="3 on C2/C3 = a ZeRO-3 training iteration (hooked forward/backward + "
+                         "update-mode step) of the MLP (BASELINE.json configs[2]); 3 on C4/C5 = the "
+                         "parameter-set ZeRO-3 step (configs[4]): dim-0-chunk (Layout Z) buckets, "
+                         "RS of the full grads -> fused Adam on the chunks -> AG of the updated "
+                         "chunks, i.e. one parameter gather per iteration")
     ap.add_argument("--batch", type=int, default=None,
                     help="ZeRO-3 MLP batch (default 16, zero1.py:144) / --train batch (default 1)")
     ap.add_argument("--gather", default=None, choices=["fp8"],
@@ -423,7 +457,10 @@ def main():
     ap.add_argument("--seq", type=int, default=8192, help="--train sequence length "
                     "(fsdp/train_fsdp.py:44: 8192)")
     ap.add_argument("--train-layers", type=int, default=None, help="--train: fewer decoder layers")
-    ap.add_argument("--layout", default="reference", choices=["reference", "flat"])
+    ap.add_argument("--layout", default="reference", choices=["reference", "flat", "chunk"],
+                    help="optimizer-shard layout: reference = whole params by index (zero1.py:55-62, "
+                         "ZeRO-1/2); chunk = dim-0 chunks of every param (zero3.py:107-108, forced "
+                         "by --zero 3 on C4/C5); flat = balanced 1/N slices (ablation)")
     ap.add_argument("--bucket-mb", type=float, default=256.0)
     ap.add_argument("--buckets", default="ragged", choices=["ragged", "padded"],
                     help="ragged: equal-count RS/AG over the shortest stream + one grouped "
@@ -469,8 +506,10 @@ def main():
 
     if args.train == "smollm3":
         return bench_train_smollm3(args, world, rank, dev, use_nccl)
-    if args.zero == 3:
+    if args.zero == 3 and args.config in ("C2", "C3"):
         return bench_zero3(args, world, rank, dev, use_nccl)
+    if args.zero == 3:  # parameter-set ZeRO-3 (BASELINE.json configs[4]): Layout Z buckets
+        args.layout = "chunk"
     name, shape_fn = CONFIGS[args.config]
     shapes = shape_fn()
     total = int(sum(int(np.prod(s)) for s in shapes))
@@ -486,7 +525,7 @@ def main():
     for s in shapes:
         grads.append((torch.empty(s, dtype=torch.float32, device=dev).normal_(generator=gen) * 1e-3).to(dt))
     torch.cuda.synchronize()
-    mod = zero1 if args.zero == 1 else zero2
+    mod = zero1 if args.zero == 1 else zero2  # zero=3 here: zero2's engine over Layout Z
     kw = {}
     comm_used = None
     if args.comm == "gloo-staged" and world > 1:
@@ -513,16 +552,12 @@ def main():
         sim_ws, real_get = args.simulate_ws, sh.get
         sh.get = lambda what, dm=None: {"ws": sim_ws, "rank": 0}.get(what) if what in ("ws", "rank") \
             else real_get(what, dm)
-    opt = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), layout=args.layout,
-                               bucket_mb=args.bucket_mb, sync=False, buckets=args.buckets, **kw)
     selfcheck = None
     if world > 1 and args.comm in ("rccl", "c10d"):
-        selfcheck = comm_selfcheck(kw["comm"], world, rank, dev)
-        ok = torch.tensor([1.0 if selfcheck["ok"] else 0.0], device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        selfcheck["all_ranks_ok"] = bool(ok.item() == 1.0)
-        if not selfcheck["all_ranks_ok"]:
-            log(f"rank {rank}: RCCL self-check FAILED: {selfcheck}")
+        selfcheck = _checked_comm(kw, world, rank, dev)
+        comm_used = selfcheck.pop("comm_used", comm_used)
+    opt = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), layout=args.layout,
+                               bucket_mb=args.bucket_mb, sync=False, buckets=args.buckets, **kw)
 
     def step():
         for p, g in zip(params, grads):
@@ -621,8 +656,12 @@ def main():
             "dtype": "fp32",
             "data": "synthetic",
             "config": {
-                "workload": f"{args.config} {name} synthetic parameter set: ZeRO-{args.zero} "
-                            f"ShardedOptimizer(Adam lr=1e-3).step(), grads resident in HBM",
+                "workload": (f"{args.config} {name} synthetic parameter set: ZeRO-{args.zero} "
+                             f"ShardedOptimizer(Adam lr=1e-3).step(), grads resident in HBM")
+                if args.zero != 3 else
+                            (f"{args.config} {name} synthetic parameter set: ZeRO-3 step on dim-0 "
+                             f"chunks (zero3.py:107-108): bucketed RS of the full grads, fused Adam "
+                             f"on the chunks, AG of the updated chunks (one gather per iteration)"),
                 "params": total, "tensors": len(shapes),
                 "param_dtype": args.dtype, "grad_dtype": args.dtype,
                 "state_dtype": "fp32 (master, exp_avg, exp_avg_sq)",

@@ -52,6 +52,15 @@ def test_bench_simulated_ws8_bucket_path(gpu):
     assert "diagnostic" in out and out["buckets"] > 1 and out["ms_per_step"] > 0
 
 
+def test_bench_zero3_parameter_set_simulated_ws8(gpu):
+    """--zero 3 on C4: the Layout Z (dim-0 chunk) bucket path of rank 0 of 8 at full scale."""
+    out = _run([sys.executable, "bench.py", "--config", "C4", "--zero", "3", "--steps", "3",
+                "--warmup", "1", "--simulate-ws", "8", "--no-cpu-baseline"])
+    assert "diagnostic" in out and out["buckets"] > 1
+    # Layout Z is balanced: rank 0 holds 1/8 of every parameter (dims divide by 8 in C4)
+    assert out["stream_elems"] * 8 >= 3_075_098_624 and out["stream_elems"] < 3_075_098_624 // 8 * 1.01
+
+
 def test_bench_zero3_training_iteration(gpu):
     """--zero 3: hooked forward/backward + update-mode step of the C2 MLP (configs[2] harness)."""
     out = _run([sys.executable, "bench.py", "--config", "C2", "--zero", "3", "--dtype", "fp32",
