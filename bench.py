@@ -167,6 +167,18 @@ def comm_selfcheck(comm, world, rank, dev):
     return out
 
 
+def _teardown(opt):
+    """Drain the device and destroy the optimizer's own RCCL communicator while the HIP runtime
+    and the process group are still up (not from a finaliser at interpreter exit)."""
+    import torch
+
+    torch.cuda.synchronize()
+    for name in ("_comm", "comm"):
+        comm = getattr(opt, name, None)
+        if comm is not None and hasattr(comm, "close"):
+            comm.close()
+
+
 def _checked_comm(kw, world, rank, dev):
     """Run comm_selfcheck on kw["comm"] (AND-ed over ranks) before anything is measured.  If the
     library's own communicator gets any closed-form result wrong on any rank, every rank switches
@@ -375,6 +387,7 @@ def bench_zero3(args, world, rank, dev, use_nccl):
                       "prefetch_hits": opt.runtime.n_prefetch_hits},
         }
         print(json.dumps(out), flush=True)
+    _teardown(opt)
     dist.destroy_process_group()
 
 
@@ -432,6 +445,7 @@ def bench_train_smollm3(args, world, rank, dev, use_nccl):
             "reference_published": "fsdp/train_fsdp.py:85-86: 1849 tok/s (ZeRO-3) / 3000 tok/s "
                                    "(ZeRO-2), 2x A100-80GB, different harness",
         }), flush=True)
+    _teardown(opt)
     dist.destroy_process_group()
 
 
@@ -639,6 +653,7 @@ def main():
                           "window_elems": eng.W, "stream_elems": eng.L,
                           "host_enqueue_ms_per_step": host_ms,
                           "copy_kernels": copy_kernels}), flush=True)
+        _teardown(opt)
         dist.destroy_process_group()
         return
     if rank == 0:
@@ -692,6 +707,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline(shapes, args.cpu_sample)
             out["cpu_reference_adam"] = cpu_reference_adam(shapes, args.cpu_sample)
         print(json.dumps(out), flush=True)
+    _teardown(opt)
     dist.destroy_process_group()
 
 
