@@ -1,8 +1,8 @@
 // CDNA4 (gfx950) kernels of the ZeRO step: segment copy (pack / unpack) and the fused Adam.
 //
 // Both kernels are HBM-bound streaming kernels (no MFMA, no LDS): 64-wide waves, 256-thread
-// workgroups, 16-byte-per-lane coalesced accesses, a grid of ~8 workgroups per CU that strides over
-// fixed-size chunks of a segment table.  A workgroup finds the segment of its chunk with a forward
+// workgroups, 16-byte-per-lane coalesced accesses, a grid of 128 workgroups per CU (16x the 8
+// resident) that strides over fixed-size chunks of a segment table.  A workgroup finds the segment of its chunk with a forward
 // scan from the previous one (chunks are visited in increasing order), so the lookup is a couple of
 // scalar loads, not a per-chunk binary search.
 //
