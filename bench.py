@@ -167,6 +167,32 @@ def comm_selfcheck(comm, world, rank, dev):
     return out
 
 
+_PHASE = ["start"]
+
+
+def _phase(name: str) -> None:
+    _PHASE[0] = name
+    log(f"[bench] phase: {name}")
+
+
+def _start_watchdog(seconds: float) -> None:
+    """A daemon timer: if the run is still going after ``seconds``, say which phase it was in and
+    end the process (os._exit, no exec) so a collective that never completes fails loudly instead of
+    holding the job until an outer limit."""
+    import threading
+
+    if seconds <= 0:
+        return
+
+    def fire():
+        log(f"[bench] WATCHDOG: still in phase '{_PHASE[0]}' after {seconds:.0f} s; exiting")
+        os._exit(3)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+
+
 def _teardown(opt):
     """Drain the device and destroy the optimizer's own RCCL communicator while the HIP runtime
     and the process group are still up (not from a finaliser at interpreter exit)."""
@@ -494,7 +520,11 @@ def main():
                          "N ranks sharing one GPU")
     ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "r01_c4_n1_adam_pmc.json"),
                     help="PMC HBM-bytes summary (profiles/*.json) for the roofline 'traffic' field")
+    ap.add_argument("--watchdog-s", type=float, default=1200.0,
+                    help="end the process (exit 3) with a diagnostic if the run has not finished "
+                         "after this many seconds (a collective that never completes)")
     args = ap.parse_args()
+    _start_watchdog(args.watchdog_s)
 
     import numpy as np
     import torch
@@ -568,6 +598,7 @@ def main():
             else real_get(what, dm)
     selfcheck = None
     if world > 1 and args.comm in ("rccl", "c10d"):
+        _phase("communicator self-check")
         selfcheck = _checked_comm(kw, world, rank, dev)
         comm_used = selfcheck.pop("comm_used", comm_used)
     opt = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), layout=args.layout,
@@ -578,6 +609,7 @@ def main():
             p.grad = g
         opt.step()
 
+    _phase("warmup")
     for _ in range(args.warmup):
         step()
     eng = opt.engine
@@ -587,6 +619,7 @@ def main():
     torch.cuda.synchronize()  # warmup drained first: no collective of ours beside c10d's barrier
     dist.barrier()
     torch.cuda.synchronize()
+    _phase("timed steps")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -643,6 +676,7 @@ def main():
     if world > 1:
         collectives = collective_summary(comm_events, args.steps, world, red_dev)
         if args.comm in ("rccl", "c10d") and not args.no_comm_sweep:
+            _phase("bucket-size sweep")
             collectives["sweep"] = comm_sweep(opt._comm, eng.arena, world, red_dev)
 
     if rank == 0 and args.simulate_ws > 1:
