@@ -34,9 +34,10 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(shapes, sample_elems: int, min_seconds: float = 10.0):
+def cpu_baseline(shapes, sample_elems: int, min_seconds: float = 10.0, split: bool = True):
     """The C oracle (oracle/adam_oracle.c, a restatement of torch.optim.Adam + ZeRO /ws) doing the
-    same N=1 ZeRO-2 step (bf16 grads → fp32 master/m/v → bf16 params) on a bounded sample."""
+    same N=1 ZeRO-2 step (bf16 grads → fp32 master (split: bf16 param + int16 residual) and m/v →
+    bf16 params) on a bounded sample."""
     import numpy as np
 
     from oracle import c_oracle
@@ -55,17 +56,23 @@ def cpu_baseline(shapes, sample_elems: int, min_seconds: float = 10.0):
     m = np.zeros(n, np.float32)
     v = np.zeros(n, np.float32)
     p = np.zeros(n, np.uint16)
+    if split:
+        p, lo = c_oracle.split_master(master)
     steps, t0 = 0, time.perf_counter()
     while True:
         steps += 1
-        c_oracle.adam_bf16(master, p, g, m, v, c_oracle.hparams(step=steps))
+        if split:
+            c_oracle.adam_bf16_split(p, lo, g, m, v, c_oracle.hparams(step=steps))
+        else:
+            c_oracle.adam_bf16(master, p, g, m, v, c_oracle.hparams(step=steps))
         el = time.perf_counter() - t0
         if el >= min_seconds or steps >= 200:
             break
     return dict(value=n * steps / el, unit="params/s", cores=c_oracle.num_threads(), kind="port",
                 sample=f"first {n:,} params (leading {ntens} tensors of the set), "
-                       f"{steps} steps of the ws=1 ZeRO-2 step (bf16 grads, fp32 master/m/v, "
-                       f"bf16 params out) by oracle/adam_oracle.c, {el:.1f} s")
+                       f"{steps} steps of the ws=1 ZeRO-2 step (bf16 grads, fp32 m/v, "
+                       f"{'split' if split else 'fp32'} master, bf16 params out) by "
+                       f"oracle/adam_oracle.c, {el:.1f} s")
 
 
 def _busbw(bus_bytes, ms):
@@ -508,6 +515,9 @@ def main():
     ap.add_argument("--no-comm-sweep", action="store_true",
                     help="skip the RS/AG bus-bandwidth sweep (N>1, after the timed region)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--master", default="split", choices=["split", "fp32"],
+                    help="bf16 params: the fp32 master as the bf16 param + an int16 residual "
+                         "(split, 26 B/element per update) or a separate fp32 array (28 B)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=256 << 20)
     ap.add_argument("--simulate-ws", type=int, default=0,
@@ -518,8 +528,9 @@ def main():
                     help="rccl: the library's own RCCL communicator; c10d: the same RCCL through "
                          "torch.distributed (A/B); gloo-staged = TEST ONLY (tests/_gloo_comm.py): "
                          "N ranks sharing one GPU")
-    ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "r01_c4_n1_adam_pmc.json"),
-                    help="PMC HBM-bytes summary (profiles/*.json) for the roofline 'traffic' field")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC HBM-bytes summary for the roofline 'traffic' field (default: the "
+                         "profiles/*_pmc.json whose config matches this run)")
     ap.add_argument("--watchdog-s", type=float, default=1200.0,
                     help="end the process (exit 3) with a diagnostic if the run has not finished "
                          "after this many seconds (a collective that never completes)")
@@ -602,7 +613,8 @@ def main():
         selfcheck = _checked_comm(kw, world, rank, dev)
         comm_used = selfcheck.pop("comm_used", comm_used)
     opt = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), layout=args.layout,
-                               bucket_mb=args.bucket_mb, sync=False, buckets=args.buckets, **kw)
+                               bucket_mb=args.bucket_mb, sync=False, buckets=args.buckets,
+                               master=args.master, **kw)
 
     def step():
         for p, g in zip(params, grads):
@@ -650,11 +662,16 @@ def main():
     achieved = float(stats[0])
     traffic = None
     traffic_src = None
-    tj = Path(args.traffic_json) if args.traffic_json else None
-    if tj is not None and tj.exists():
+    want = {"workload": args.config, "zero": args.zero, "param_dtype": args.dtype,
+            "layout": args.layout, "n_gpus": world}
+    if args.dtype == "bf16":
+        want["master"] = args.master
+    cands = [Path(args.traffic_json)] if args.traffic_json else sorted(
+        (REPO / "profiles").glob("*_pmc.json"))
+    for tj in cands:
+        if not tj.exists():
+            continue
         d = json.loads(tj.read_text())
-        want = {"workload": args.config, "zero": args.zero, "param_dtype": args.dtype,
-                "layout": args.layout, "n_gpus": world}
         if d.get("config") == want:  # PMC passes of this same configuration (profiles/README.md)
             traffic = d.get("hbm_bytes_per_launch")
             traffic_src = str(tj.relative_to(REPO) if tj.is_absolute() else tj)
@@ -713,7 +730,11 @@ def main():
                              f"on the chunks, AG of the updated chunks (one gather per iteration)"),
                 "params": total, "tensors": len(shapes),
                 "param_dtype": args.dtype, "grad_dtype": args.dtype,
-                "state_dtype": "fp32 (master, exp_avg, exp_avg_sq)",
+                "state_dtype": ("fp32 exp_avg, exp_avg_sq; fp32 master held as the bf16 param + "
+                                "an int16 residual (include/zero_amd.h ZS_BF16_SPLIT)")
+                if args.dtype == "bf16" and args.master == "split"
+                else "fp32 (master, exp_avg, exp_avg_sq)",
+                "master": args.master if args.dtype == "bf16" else "param",
                 "zero": args.zero, "layout": args.layout, "bucket_mb": args.bucket_mb,
                 "bucket_mode": args.buckets,
                 "buckets": eng.K, "parallelism": f"dp{world}", "comm": comm_used,
@@ -738,7 +759,8 @@ def main():
         if copy_kernels is not None:
             out["copy_kernels"] = copy_kernels
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(shapes, args.cpu_sample)
+            out["cpu_baseline"] = cpu_baseline(shapes, args.cpu_sample,
+                                               split=args.dtype == "bf16" and args.master == "split")
             out["cpu_reference_adam"] = cpu_reference_adam(shapes, args.cpu_sample)
         print(json.dumps(out), flush=True)
     _teardown(opt)

@@ -157,6 +157,18 @@ __device__ __forceinline__ unsigned short f32_to_bf16(float f) {
   return r;
 }
 
+// Split master (ZS_BF16_SPLIT): the fp32 master's bits u live as hi = RNE-bf16(u) — the bf16 param
+// itself — and the int16 residual lo = u - (hi << 16), so u = (hi << 16) + sext(lo).  The one
+// residual int16 cannot hold, +0x8000 (an exact tie rounded down to an even hi), is stored as
+// 0x7FFF: that master moves 1 ulp toward zero and its bf16 param stays the same.
+__device__ __forceinline__ float join_master(uint32_t hi, uint32_t lo) {
+  return __uint_as_float((hi << 16) + uint32_t(int32_t(int16_t(uint16_t(lo)))));
+}
+__device__ __forceinline__ uint32_t master_residual(float p, uint32_t hi) {
+  const uint32_t d = __float_as_uint(p) - (hi << 16);
+  return d == 0x8000u ? 0x7FFFu : (d & 0xFFFFu);
+}
+
 // One element of torch.optim.Adam's single-tensor update (adam.py:394-547), in the rounding order
 // of torch's CPU kernels: lerp = fma(w, end-self, self) (ATen Lerp.h weight<0.5 branch),
 // exp_avg_sq.mul_(b2).addcmul_(g,g,1-b2) = fma((1-b2)*g, g, v*b2), denom = sqrt(v)/bc2_sqrt + eps,
@@ -192,7 +204,7 @@ __device__ __forceinline__ float load_g1(const void* g, int64_t i) {
 }
 
 // Scalar kernel: any alignment, any length (segment tails and unaligned segments; tiny).
-template <typename GT, bool AMS, bool CARRY>
+template <typename GT, bool AMS, bool CARRY, bool SPLIT>
 __global__ __launch_bounds__(kThreads) void adam_scalar_kernel(
     const AdamSeg* __restrict__ segs, const int64_t* __restrict__ chunk_prefix, int64_t nseg,
     int64_t total_chunks, HP hp) {
@@ -203,12 +215,21 @@ __global__ __launch_bounds__(kThreads) void adam_scalar_kernel(
     const int64_t i = (c - chunk_prefix[seg]) * kThreads + threadIdx.x;
     if (i >= s.n) continue;
     float gs = s.g ? load_g1<GT>(s.g, i) : 0.0f;
-    float p = glob(s.master)[i], m = glob(s.m)[i], v = glob(s.v)[i];
+    const gptr<unsigned short> lo = glob(reinterpret_cast<unsigned short*>(s.master_out));
+    float p = SPLIT ? join_master(glob(reinterpret_cast<const unsigned short*>(s.master))[i], lo[i])
+                    : glob(s.master)[i];
+    float m = glob(s.m)[i], v = glob(s.v)[i];
     float vm = AMS ? glob(s.vmax)[i] : 0.0f;
     float cr = CARRY ? glob(s.carry)[i] : 0.0f;
     adam_elem<AMS, CARRY>(gs, p, m, v, vm, cr, hp);
-    if (s.master_out) glob(s.master_out)[i] = p;
-    if (s.p_out) glob(s.p_out)[i] = f32_to_bf16(p);
+    if constexpr (SPLIT) {
+      const unsigned short h = f32_to_bf16(p);
+      glob(s.p_out)[i] = h;
+      lo[i] = (unsigned short)master_residual(p, h);
+    } else {
+      if (s.master_out) glob(s.master_out)[i] = p;
+      if (s.p_out) glob(s.p_out)[i] = f32_to_bf16(p);
+    }
     glob(s.m)[i] = m;
     glob(s.v)[i] = v;
     if constexpr (AMS) glob(s.vmax)[i] = vm;
@@ -241,7 +262,7 @@ __device__ __forceinline__ float4 load_g4(const void* g, int64_t i) {
 // splits tails off into the scalar table).  kAdamGroups float4 groups per thread, lane-contiguous
 // (16 B per lane per access), so each wave instruction touches one contiguous 1 KiB (f32) /
 // 512 B (bf16) run; every group's loads are issued before any math.
-template <typename GT, bool AMS, bool CARRY>
+template <typename GT, bool AMS, bool CARRY, bool SPLIT>
 __global__ __launch_bounds__(kThreads) void adam_segments_kernel(
     const AdamSeg* __restrict__ segs, const int64_t* __restrict__ chunk_prefix, int64_t nseg,
     int64_t total_chunks, HP hp) {
@@ -257,7 +278,14 @@ __global__ __launch_bounds__(kThreads) void adam_segments_kernel(
       const int64_t i = e0 + (int64_t(u) * kThreads + threadIdx.x) * 4;
       if (i < s.n) {
         g4[u] = s.g ? load_g4<GT>(s.g, i) : make_float4(0.f, 0.f, 0.f, 0.f);
-        p4[u] = ld4(s.master, i);
+        if constexpr (SPLIT) {
+          const uint2 h = nt_ld8(reinterpret_cast<const unsigned short*>(s.master) + i);
+          const uint2 l = nt_ld8(reinterpret_cast<const unsigned short*>(s.master_out) + i);
+          p4[u] = make_float4(join_master(h.x & 0xFFFFu, l.x), join_master(h.x >> 16, l.x >> 16),
+                              join_master(h.y & 0xFFFFu, l.y), join_master(h.y >> 16, l.y >> 16));
+        } else {
+          p4[u] = ld4(s.master, i);
+        }
         m4[u] = ld4(s.m, i);
         v4[u] = ld4(s.v, i);
         if constexpr (AMS) x4[u] = ld4(s.vmax, i);
@@ -282,12 +310,24 @@ __global__ __launch_bounds__(kThreads) void adam_segments_kernel(
           if constexpr (AMS) xp[j] = xv;
           if constexpr (CARRY) cp[j] = cv;
         }
-        if (s.master_out) st4(s.master_out, i, p4[u]);
-        if (s.p_out) {
-          uint2 r;
-          r.x = uint32_t(f32_to_bf16(pp[0])) | (uint32_t(f32_to_bf16(pp[1])) << 16);
-          r.y = uint32_t(f32_to_bf16(pp[2])) | (uint32_t(f32_to_bf16(pp[3])) << 16);
-          nt_st8(s.p_out + i, r);
+        if constexpr (SPLIT) {
+          uint32_t h[4], l[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            h[j] = f32_to_bf16(pp[j]);
+            l[j] = master_residual(pp[j], h[j]);
+          }
+          nt_st8(s.p_out + i, make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16)));
+          nt_st8(reinterpret_cast<unsigned short*>(s.master_out) + i,
+                 make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16)));
+        } else {
+          if (s.master_out) st4(s.master_out, i, p4[u]);
+          if (s.p_out) {
+            uint2 r;
+            r.x = uint32_t(f32_to_bf16(pp[0])) | (uint32_t(f32_to_bf16(pp[1])) << 16);
+            r.y = uint32_t(f32_to_bf16(pp[2])) | (uint32_t(f32_to_bf16(pp[3])) << 16);
+            nt_st8(s.p_out + i, r);
+          }
         }
         st4(s.m, i, m4[u]);
         st4(s.v, i, v4[u]);
@@ -675,7 +715,11 @@ int zs_adamset_create(const zs_adam_seg* in, int64_t n, int g_dtype, int p_dtype
   *out = nullptr;
   ZS_REQUIRE(n >= 0 && (n == 0 || in), "zs_adamset_create: bad table");
   ZS_REQUIRE(g_dtype == ZS_F32 || g_dtype == ZS_BF16, "zs_adamset_create: bad g_dtype %d", g_dtype);
-  ZS_REQUIRE(p_dtype == ZS_BF16, "zs_adamset_create: p_out must be bf16 (got %d)", p_dtype);
+  ZS_REQUIRE(p_dtype == ZS_BF16 || p_dtype == ZS_BF16_SPLIT,
+             "zs_adamset_create: p_dtype must be ZS_BF16 or ZS_BF16_SPLIT (got %d)", p_dtype);
+  const bool split = p_dtype == ZS_BF16_SPLIT;
+  ZS_REQUIRE(!split || g_dtype == ZS_BF16, "zs_adamset_create: ZS_BF16_SPLIT needs bf16 grads");
+  const int64_t msz = split ? 2 : 4;  // bytes per element of master / master_out
   const int64_t gsz = g_dtype == ZS_F32 ? 4 : 2;
   std::vector<AdamSeg> vec, sca;
   std::vector<int64_t> vpre(1, 0), spre(1, 0);
@@ -686,6 +730,9 @@ int zs_adamset_create(const zs_adam_seg* in, int64_t n, int g_dtype, int p_dtype
     ZS_REQUIRE(s.n >= 0, "zs_adamset_create: seg %lld n < 0", (long long)i);
     if (s.n == 0) continue;
     ZS_REQUIRE(s.master && s.m && s.v, "zs_adamset_create: seg %lld missing master/m/v",
+               (long long)i);
+    ZS_REQUIRE(!split || (s.master_out && s.p_out),
+               "zs_adamset_create: seg %lld: a split master needs master_out (residual) and p_out",
                (long long)i);
     const int c = s.carry ? 1 : 0;
     ZS_REQUIRE(carry_state < 0 || carry_state == c,
@@ -704,8 +751,8 @@ int zs_adamset_create(const zs_adam_seg* in, int64_t n, int g_dtype, int p_dtype
     d.v = reinterpret_cast<float*>(s.v);
     d.vmax = reinterpret_cast<float*>(s.vmax);
     d.carry = reinterpret_cast<float*>(s.carry);
-    const bool ok = aligned(s.g, uint64_t(gsz) * 4) && aligned(s.master, 16) &&
-                    aligned(s.master_out, 16) && aligned(s.p_out, 8) && aligned(s.m, 16) &&
+    const bool ok = aligned(s.g, uint64_t(gsz) * 4) && aligned(s.master, uint64_t(msz) * 4) &&
+                    aligned(s.master_out, uint64_t(msz) * 4) && aligned(s.p_out, 8) && aligned(s.m, 16) &&
                     aligned(s.v, 16) && aligned(s.vmax, 16) && aligned(s.carry, 16);
     const int64_t nv = ok ? (s.n & ~int64_t(3)) : 0;
     if (nv) {
@@ -720,8 +767,8 @@ int zs_adamset_create(const zs_adam_seg* in, int64_t n, int g_dtype, int p_dtype
         return p ? reinterpret_cast<P>(reinterpret_cast<uintptr_t>(p) + uintptr_t(nv * es)) : p;
       };
       t.g = s.g ? reinterpret_cast<const void*>(s.g + uint64_t(nv * gsz)) : nullptr;
-      t.master = adv(d.master, 4);
-      t.master_out = adv(d.master_out, 4);
+      t.master = adv(d.master, msz);
+      t.master_out = adv(d.master_out, msz);
       t.p_out = adv(d.p_out, 2);
       t.m = adv(d.m, 4);
       t.v = adv(d.v, 4);
@@ -732,8 +779,8 @@ int zs_adamset_create(const zs_adam_seg* in, int64_t n, int g_dtype, int p_dtype
       spre.push_back(spre.back() + (t.n + kThreads - 1) / kThreads);
     }
     elems += s.n;
-    int64_t b = (s.g ? gsz : 0) + 4 /*master*/ + 8 /*m*/ + 8 /*v*/;
-    if (s.master_out) b += 4;
+    int64_t b = (s.g ? gsz : 0) + msz /*master*/ + 8 /*m*/ + 8 /*v*/;
+    if (s.master_out) b += split ? 4 /*residual read + write*/ : 4;
     if (s.p_out) b += 2;
     if (s.vmax) b += 8;
     if (s.carry) b += 8;
@@ -786,25 +833,25 @@ int zs_adamset_run(const zs_adamset* as, const zs_adam_hparams* h, uintptr_t str
   hp.inv_div = float(1.0 / double(h->grad_div));
   hp.maximize = h->maximize;
   const bool ams = h->amsgrad != 0, carry = as->has_carry != 0;
+  const bool split = as->p_dtype == ZS_BF16_SPLIT;
   ZS_REQUIRE(!ams || as->has_vmax || (as->nvec + as->nsca) == 0,
              "zs_adamset_run: amsgrad needs vmax segments");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-#define ZS_LAUNCH(KERNEL, GT, A, C, TAB, PRE, NS, NCH)                                        \
-  hipLaunchKernelGGL((KERNEL<GT, A, C>), dim3(int(std::min<int64_t>(NCH, grid_cap()))),      \
+#define ZS_LAUNCH(KERNEL, GT, A, C, S, TAB, PRE, NS, NCH)                                     \
+  hipLaunchKernelGGL((KERNEL<GT, A, C, S>), dim3(int(std::min<int64_t>(NCH, grid_cap()))),   \
                      dim3(kThreads), 0, st, TAB, PRE, NS, NCH, hp)
+#define ZS_DISPATCH_AC(KERNEL, GT, S, TAB, PRE, NS, NCH)                                      \
+  do {                                                                                        \
+    if (ams && carry) ZS_LAUNCH(KERNEL, GT, true, true, S, TAB, PRE, NS, NCH);                \
+    else if (ams) ZS_LAUNCH(KERNEL, GT, true, false, S, TAB, PRE, NS, NCH);                   \
+    else if (carry) ZS_LAUNCH(KERNEL, GT, false, true, S, TAB, PRE, NS, NCH);                 \
+    else ZS_LAUNCH(KERNEL, GT, false, false, S, TAB, PRE, NS, NCH);                           \
+  } while (0)
 #define ZS_DISPATCH(KERNEL, TAB, PRE, NS, NCH)                                                \
   do {                                                                                        \
-    if (as->g_dtype == ZS_F32) {                                                              \
-      if (ams && carry) ZS_LAUNCH(KERNEL, float, true, true, TAB, PRE, NS, NCH);              \
-      else if (ams) ZS_LAUNCH(KERNEL, float, true, false, TAB, PRE, NS, NCH);                 \
-      else if (carry) ZS_LAUNCH(KERNEL, float, false, true, TAB, PRE, NS, NCH);               \
-      else ZS_LAUNCH(KERNEL, float, false, false, TAB, PRE, NS, NCH);                         \
-    } else {                                                                                  \
-      if (ams && carry) ZS_LAUNCH(KERNEL, unsigned short, true, true, TAB, PRE, NS, NCH);     \
-      else if (ams) ZS_LAUNCH(KERNEL, unsigned short, true, false, TAB, PRE, NS, NCH);        \
-      else if (carry) ZS_LAUNCH(KERNEL, unsigned short, false, true, TAB, PRE, NS, NCH);      \
-      else ZS_LAUNCH(KERNEL, unsigned short, false, false, TAB, PRE, NS, NCH);                \
-    }                                                                                         \
+    if (as->g_dtype == ZS_F32) ZS_DISPATCH_AC(KERNEL, float, false, TAB, PRE, NS, NCH);      \
+    else if (split) ZS_DISPATCH_AC(KERNEL, unsigned short, true, TAB, PRE, NS, NCH);         \
+    else ZS_DISPATCH_AC(KERNEL, unsigned short, false, TAB, PRE, NS, NCH);                   \
   } while (0)
   if (as->vec_chunks) {
     ZS_DISPATCH(adam_segments_kernel, as->d_vec, as->d_vec_prefix, as->nvec, as->vec_chunks);
@@ -815,6 +862,7 @@ int zs_adamset_run(const zs_adamset* as, const zs_adam_hparams* h, uintptr_t str
     ZS_HIP(hipGetLastError());
   }
 #undef ZS_DISPATCH
+#undef ZS_DISPATCH_AC
 #undef ZS_LAUNCH
   return ZS_OK;
 }

@@ -15,10 +15,10 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_PATH = Path(os.environ.get("ZERO_AMD_LIB", Path(__file__).resolve().parent / "libzero_amd.so"))
 
 ZS_OK, ZS_ERR_INVALID, ZS_ERR_HIP, ZS_ERR_RCCL, ZS_ERR_NOMEM = 0, 1, 2, 3, 4
-ZS_F32, ZS_BF16, ZS_U8 = 0, 1, 2
+ZS_F32, ZS_BF16, ZS_U8, ZS_BF16_SPLIT = 0, 1, 2, 3
 ZS_LAYOUT_R, ZS_LAYOUT_Z, ZS_LAYOUT_F = 0, 1, 2
 ZS_BUCKETS_RAGGED, ZS_BUCKETS_PADDED = 0, 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 ZS_UNIQUE_ID_BYTES = 128
 
 # Every symbol include/zero_amd.h declares (tests check the library exports all of them).

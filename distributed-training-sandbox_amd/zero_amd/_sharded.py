@@ -40,7 +40,7 @@ class ShardedOptimizerBase:
 
     def __init__(self, optimizer: Optimizer, *, layout: str = "reference",
                  bucket_mb: float = 256.0, comm=None, sync: bool = True, buckets: str = "ragged",
-                 overlap: bool = False, overlap_bucket_mb: float = 64.0):
+                 overlap: bool = False, overlap_bucket_mb: float = 64.0, master: str = "split"):
         if not isinstance(optimizer, torch.optim.Adam):
             raise TypeError("zero_amd ShardedOptimizer wraps torch.optim.Adam / AdamW "
                             f"(got {type(optimizer).__name__})")
@@ -72,6 +72,7 @@ class ShardedOptimizerBase:
         self._bucket_bytes = int(bucket_mb * (1 << 20))
         self._comm = comm
         self._sync = sync
+        self._master = master  # bf16 params: "split" (bf16 param + int16 residual) or "fp32"
         self.engine: ShardEngine | None = None
         self._step_tensors = {}
         self._overlap = bool(overlap)
@@ -97,7 +98,8 @@ class ShardedOptimizerBase:
             self._comm = comm
         self.engine = ShardEngine(self.params, self._group_of, self.world_size, self.rank,
                                   layout=self._layout, carry=self._carry, comm=comm,
-                                  bucket_bytes=self._bucket_bytes, buckets=self._buckets)
+                                  bucket_bytes=self._bucket_bytes, buckets=self._buckets,
+                                  master=self._master)
         if self.engine.plan.layout != 0:
             return
         self._expose_state()

@@ -92,7 +92,7 @@ def probed_zeros(n: int, dtype, device, tries: int = 5):
 class ShardEngine:
     def __init__(self, params, group_of, ws: int, rank: int, *, layout="reference", carry=False,
                  comm=None, bucket_bytes: int = 256 << 20, align: int = ALIGN_ELEMS,
-                 buckets: str = "ragged", placement_tries: int = 5):
+                 buckets: str = "ragged", placement_tries: int = 5, master: str = "split"):
         if not params:
             raise ValueError("ShardEngine: no parameters")
         dev = params[0].device
@@ -111,7 +111,13 @@ class ShardEngine:
         self.ws, self.rank = ws, rank
         self.device, self.dtype = dev, dtype
         self.es = params[0].element_size()
-        self.mixed = dtype == torch.bfloat16  # bf16 params → fp32 master in the shard
+        self.mixed = dtype == torch.bfloat16  # bf16 params → an fp32 master in the shard
+        if master not in ("split", "fp32"):
+            raise ValueError(f"master must be 'split' or 'fp32' (got {master!r})")
+        # split: the master is the bf16 param + an int16 residual (include/zero_amd.h
+        # ZS_BF16_SPLIT, 26 instead of 28 B/element per update); fp32: a separate fp32 array
+        self.split = self.mixed and master == "split"
+        self.p_dtype = _lib.ZS_BF16_SPLIT if self.split else _lib.ZS_BF16
         self.has_carry = bool(carry)
         self.comm = comm
         if ws > 1 and comm is None:
@@ -126,15 +132,20 @@ class ShardEngine:
         self.L = self.plan.stream_len(rank)
         self.pieces = self.plan.pieces(rank)
 
-        # exp_avg, exp_avg_sq (+ fp32 master, + ZeRO-1 carry): one allocation, placed by probe
-        nbuf = 2 + int(self.mixed) + int(bool(carry))
-        self.state, self.placement = probed_zeros(nbuf * self.L, torch.float32, dev, placement_tries)
-        views = iter(self.state.split(self.L) if self.L else [self.state] * nbuf)
+        # exp_avg, exp_avg_sq (+ ZeRO-1 carry, + fp32 master or its int16 residual): one
+        # allocation, placed by probe
+        L = self.L
+        nf = 2 + int(bool(carry)) + int(self.mixed and not self.split)
+        nlo = (L + 1) // 2 if self.split else 0  # int16 residuals, in fp32 words
+        self.state, self.placement = probed_zeros(nf * L + nlo, torch.float32, dev, placement_tries)
+        views = iter([self.state[k * L:(k + 1) * L] for k in range(nf)])
         self.m, self.v = next(views), next(views)
         self.vmax = None
-        self.master = next(views) if self.mixed else None
         self.carry = next(views) if carry else None
-        if self.mixed:
+        self.master = next(views) if self.mixed and not self.split else None
+        # residual 0 everywhere: the master starts as the bf16 param exactly
+        self.lo = self.state[nf * L:].view(torch.int16)[:L] if self.split else None
+        if self.master is not None:
             for i, po, so, n in zip(*self._piece_cols()):
                 self.master[so:so + n].copy_(params[i].detach().reshape(-1)[po:po + n])
         self.arena = None  # allocated on the first bucketed step (not at all in overlap mode)
@@ -176,6 +187,8 @@ class ShardEngine:
         views = {"exp_avg": self.m[so:so + n].view(shape), "exp_avg_sq": self.v[so:so + n].view(shape)}
         if self.master is not None:
             views["master_param"] = self.master[so:so + n].view(shape)
+        if self.lo is not None:  # the fp32 master = the bf16 param's bits << 16 + this residual
+            views["master_residual"] = self.lo[so:so + n].view(shape)
         return views
 
     def ensure_vmax(self):
@@ -223,6 +236,16 @@ class ShardEngine:
         rows[:, 8] = n.astype(np.uint64)
         return rows
 
+    def _mixed_rows(self, idx, g, hi, p_out, so, n):
+        """Rows of a bf16-param update: master read from the bf16 param ``hi`` + its residual
+        (split) or from the fp32 master array; the updated bf16 param written to ``p_out``."""
+        so64 = so.astype(np.uint64)
+        if self.split:
+            lo = np.uint64(self.lo.data_ptr()) + so64 * np.uint64(2)
+            return self._adam_rows(idx, g, hi, lo, p_out, so, n)
+        mst = np.uint64(self.master.data_ptr()) + so64 * np.uint64(4)
+        return self._adam_rows(idx, g, mst, mst, p_out, so, n)
+
     def _run_adam(self, tag, rows, param_idx, hparams_of, stream):
         """Partition rows by (group, step) — torch's bias correction is per param — and launch."""
         if len(rows) == 0:
@@ -233,7 +256,7 @@ class ShardEngine:
             sub = np.ascontiguousarray(rows[sel])
             gidx, step = int(key[0]), int(key[1])
             aset = self._cached(("adam", tag, gidx, len(sel), int(sel[0])), sub.tobytes(),
-                                lambda: AdamSet(sub, self.zdtype))
+                                lambda: AdamSet(sub, self.zdtype, self.p_dtype))
             hpd = hparams_of(gidx)
             if hpd["amsgrad"] and self.vmax is None:
                 raise RuntimeError("amsgrad state buffer missing")
@@ -287,8 +310,8 @@ class ShardEngine:
         es = np.uint64(self.es)
         g = gptr[idx] + po.astype(np.uint64) * es
         if self.mixed:
-            mst = np.uint64(self.master.data_ptr()) + so.astype(np.uint64) * np.uint64(4)
-            rows = self._adam_rows(idx, g, mst, mst, pptr + po.astype(np.uint64) * es, so, n)
+            pp = pptr + po.astype(np.uint64) * es
+            rows = self._mixed_rows(idx, g, pp, pp, so, n)
         else:
             p = pptr + po.astype(np.uint64) * np.uint64(4)
             rows = self._adam_rows(idx, g, p, p, 0, so, n)
@@ -371,9 +394,8 @@ class ShardEngine:
                 ln = s.length[own]
                 po = s.param_off[own].astype(np.uint64)
                 live = has[idx]
-                if self.mixed:
-                    mst = np.uint64(self.master.data_ptr()) + so.astype(np.uint64) * np.uint64(4)
-                    rows = self._adam_rows(idx, slot, mst, mst, slot, so, ln)
+                if self.mixed:  # master from module storage (+ residual), param out to the slot
+                    rows = self._mixed_rows(idx, slot, pptr[idx] + po * es, slot, so, ln)
                 else:
                     p = pptr[idx] + po * np.uint64(4)
                     rows = self._adam_rows(idx, slot, p, slot, 0, so, ln)
@@ -448,8 +470,7 @@ class ShardEngine:
                 # straight into module storage (no broadcast, no unpack)
                 out = slot if self.ws > 1 else p
                 if self.mixed:
-                    mst = np.uint64(self.master.data_ptr()) + so.astype(np.uint64) * np.uint64(4)
-                    rows = self._adam_rows(idx, slot, mst, mst, out, so, ln)
+                    rows = self._mixed_rows(idx, slot, p, out, so, ln)
                 else:
                     rows = self._adam_rows(idx, slot, p, out, 0, so, ln)
                 self._run_adam(("overlap", k), rows, idx, hparams_of, stream)

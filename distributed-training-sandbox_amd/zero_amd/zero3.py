@@ -40,7 +40,7 @@ from .engine import ALIGN_ELEMS, probed_zeros
 from .kernels import AdamSet, adam_hparams
 from .plan import Plan
 from ._sharded import adam_group_hparams
-from ._lib import ZS_BF16, ZS_F32
+from ._lib import ZS_BF16, ZS_BF16_SPLIT, ZS_F32
 from .training_utils.utils import get
 
 
@@ -324,18 +324,15 @@ class ShardedOptimizer:
         plan = Plan(numels, self.world_size, self.rank, "chunk", dim0=dim0, align_elems=ALIGN_ELEMS)
         L = plan.stream_len(self.rank)
         pc = plan.pieces(self.rank)
-        nbuf = 3 if dtype == torch.bfloat16 else 2  # exp_avg, exp_avg_sq (+ fp32 master)
-        state, placement = probed_zeros(nbuf * L, torch.float32, dev)
-        views = list(state.split(L)) if L else [state] * nbuf
+        # exp_avg, exp_avg_sq (+ for bf16 params the split master's int16 residual: the fp32
+        # master is the bf16 shard + residual, include/zero_amd.h ZS_BF16_SPLIT; starts at 0)
+        nlo = (L + 1) // 2 if dtype == torch.bfloat16 else 0
+        state, placement = probed_zeros(2 * L + nlo, torch.float32, dev)
         eng = dict(plan=plan, pieces=pc, L=L, dtype=dtype, state=state, placement=placement,
-                   m=views[0], v=views[1],
-                   vmax=None, gshard=torch.zeros(L, dtype=dtype, device=dev), master=None,
+                   m=state[:L], v=state[L:2 * L],
+                   vmax=None, gshard=torch.zeros(L, dtype=dtype, device=dev),
+                   lo=state[2 * L:].view(torch.int16)[:L] if nlo else None,
                    steps=np.zeros(len(self.params), np.int64), cache={}, retired=[])
-        if dtype == torch.bfloat16:
-            eng["master"] = views[2]
-            for i, so, ln in zip(pc.param, pc.stream_off, pc.length):
-                if ln:
-                    eng["master"][so:so + ln].copy_(self.param_managers[self.params[i]].shard.reshape(-1).float())
         self._engine = eng
         for i, so, ln in zip(pc.param, pc.stream_off, pc.length):
             p = self.params[i]
@@ -409,9 +406,9 @@ class ShardedOptimizer:
         so = pc.stream_off[owned].astype(np.uint64)
         rows[:, 0] = np.uint64(eng["gshard"].data_ptr()) + so * np.uint64(es)
         shard_ptr = np.array([self.param_managers[self.params[i]].shard.data_ptr() for i in idx], np.uint64)
-        if eng["master"] is not None:
-            mp = np.uint64(eng["master"].data_ptr()) + so * np.uint64(4)
-            rows[:, 1], rows[:, 2], rows[:, 3] = mp, mp, shard_ptr
+        if eng["lo"] is not None:  # master = bf16 shard (in and out) + residual
+            rows[:, 1], rows[:, 3] = shard_ptr, shard_ptr
+            rows[:, 2] = np.uint64(eng["lo"].data_ptr()) + so * np.uint64(2)
         else:
             rows[:, 1], rows[:, 2] = shard_ptr, shard_ptr
         rows[:, 4] = np.uint64(eng["m"].data_ptr()) + so * np.uint64(4)
@@ -428,7 +425,8 @@ class ShardedOptimizer:
             if hit is None or hit[0] != sub.tobytes():
                 if hit is not None:  # keep until the device is idle (hipFree would sync it)
                     eng["retired"].append(hit[1])
-                hit = (sub.tobytes(), AdamSet(sub, ZS_BF16 if eng["dtype"] == torch.bfloat16 else ZS_F32))
+                hit = (sub.tobytes(), AdamSet(sub, ZS_BF16, ZS_BF16_SPLIT) if eng["lo"] is not None
+                       else AdamSet(sub, ZS_F32))
                 eng["cache"][ck] = hit
             h = adam_group_hparams(self._groups[int(key[0])], self.optimizer)
             hp = adam_hparams(h["lr"], h["beta1"], h["beta2"], h["eps"], h["weight_decay"], int(key[1]),

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ZS_ABI_VERSION 2
+#define ZS_ABI_VERSION 3
 
 enum zs_status {
   ZS_OK = 0,
@@ -34,7 +34,13 @@ enum zs_status {
   ZS_ERR_NOMEM = 4
 };
 
-enum zs_dtype { ZS_F32 = 0, ZS_BF16 = 1, ZS_U8 = 2 /* raw bytes (fp8 payloads); collectives only */ };
+enum zs_dtype {
+  ZS_F32 = 0,
+  ZS_BF16 = 1,
+  ZS_U8 = 2,        /* raw bytes (fp8 payloads); collectives only */
+  ZS_BF16_SPLIT = 3 /* zs_adamset_create p_dtype only: the fp32 master stored as the bf16 param
+                       (its round-to-nearest-even high half) + a 16-bit residual, see zs_adam_seg */
+};
 
 /* Shard layouts (SURVEY.md §7 "Two shard layouts"). */
 enum zs_layout {
@@ -150,6 +156,14 @@ typedef struct {
   uint64_t carry;      /* fp32 ZeRO-1 carried average A_{t-1}, rewritten with A_t; or 0 */
   int64_t n;           /* elements */
 } zs_adam_seg;
+/* p_dtype ZS_BF16_SPLIT (bf16 params; g must be bf16): the fp32 master is not stored as such.
+ * Its bits u are the bf16 param hi = RNE(u) and the int16 residual lo = u - (hi << 16):
+ *   master     = bf16 param read (hi), 8-byte aligned for the vector path
+ *   master_out = int16 residual lo, read and rewritten in place
+ *   p_out      = bf16 param written (hi of the updated master; may equal master)
+ * u = (hi << 16) + sign_extend(lo) exactly, except an exact tie that rounds down to an even hi
+ * (residual +0x8000, 1 in 2^17 of uniformly random masters): that master is stored 1 ulp toward
+ * zero (lo = 0x7FFF), the bf16 param unchanged.  26 instead of 28 B/element per update. */
 
 typedef struct {
   /* scalars exactly as torch computes them (double on host, rounded to f32 once) */
@@ -173,9 +187,9 @@ int zs_adam_hparams_init(double lr, double beta1, double beta2, double eps, doub
                          double carry_mul, zs_adam_hparams* hp);
 
 typedef struct zs_adamset zs_adamset;
-/* g_dtype: dtype of every seg's g; p_dtype: dtype of every non-null p_out (ZS_BF16). All
- * fp32 pointers of a seg must be 16-byte aligned and bf16 pointers 8-byte aligned for the
- * vector path; other segments take a scalar path. */
+/* g_dtype: dtype of every seg's g; p_dtype: ZS_BF16 (fp32 master, optional bf16 p_out) or
+ * ZS_BF16_SPLIT (split master, above). All fp32 pointers of a seg must be 16-byte aligned and
+ * bf16 / int16 pointers 8-byte aligned for the vector path; other segments take a scalar path. */
 int zs_adamset_create(const zs_adam_seg* segs, int64_t n, int g_dtype, int p_dtype,
                       zs_adamset** out);
 int zs_adamset_run(const zs_adamset* as, const zs_adam_hparams* hp, uintptr_t stream);

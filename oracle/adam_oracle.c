@@ -103,6 +103,49 @@ void oracle_adam_bf16(float* master, uint16_t* p_bf16, const uint16_t* g, float*
   }
 }
 
+/* Split master (include/zero_amd.h ZS_BF16_SPLIT): the fp32 master's bits u are held as the bf16
+ * param hi = RNE(u) and an int16 residual lo = u - (hi << 16); u = (hi << 16) + sext(lo).  The
+ * residual +0x8000 (an exact tie rounded down to an even hi) does not fit int16 and is stored as
+ * 0x7FFF: that master moves 1 ulp toward zero, hi is unchanged. */
+static inline float join_master(uint16_t hi, uint16_t lo) {
+  const uint32_t u = ((uint32_t)hi << 16) + (uint32_t)(int32_t)(int16_t)lo;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+static inline uint16_t master_residual(float p, uint16_t hi) {
+  uint32_t u;
+  memcpy(&u, &p, 4);
+  const uint32_t d = u - ((uint32_t)hi << 16);
+  return d == 0x8000u ? (uint16_t)0x7fffu : (uint16_t)(d & 0xffffu);
+}
+
+/* bf16 grads and params with a split master: hi (the bf16 param) and lo updated in place. */
+void oracle_adam_bf16_split(uint16_t* hi, uint16_t* lo, const uint16_t* g, float* m, float* v,
+                            float* vmax, float* carry, int64_t n, const oracle_hparams* hp) {
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; ++i) {
+    float master = join_master(hi[i], lo[i]);
+    const float pp = adam_elem(g ? bf16_to_f32(g[i]) : 0.0f, &master, &m[i], &v[i],
+                               vmax ? &vmax[i] : 0, carry ? &carry[i] : 0, hp);
+    hi[i] = f32_to_bf16(pp);
+    lo[i] = master_residual(pp, hi[i]);
+  }
+}
+
+/* The split-master encoding alone (tests: round trips and the tie rule). */
+void oracle_split_master(const float* master, uint16_t* hi, uint16_t* lo, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) {
+    hi[i] = f32_to_bf16(master[i]);
+    lo[i] = master_residual(master[i], hi[i]);
+  }
+}
+
+void oracle_join_master(const uint16_t* hi, const uint16_t* lo, float* master, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) master[i] = join_master(hi[i], lo[i]);
+}
+
 int oracle_num_threads(void) {
 #ifdef _OPENMP
   extern int omp_get_max_threads(void);

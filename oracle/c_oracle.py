@@ -41,6 +41,10 @@ def lib():
         _lib.oracle_adam_f32.argtypes = [P, P, P, P, P, P, ctypes.c_int64, ctypes.POINTER(OracleHParams)]
         _lib.oracle_adam_bf16.argtypes = [P, P, P, P, P, P, P, ctypes.c_int64,
                                           ctypes.POINTER(OracleHParams)]
+        _lib.oracle_adam_bf16_split.argtypes = [P, P, P, P, P, P, P, ctypes.c_int64,
+                                                ctypes.POINTER(OracleHParams)]
+        _lib.oracle_split_master.argtypes = [P, P, P, ctypes.c_int64]
+        _lib.oracle_join_master.argtypes = [P, P, P, ctypes.c_int64]
         _lib.oracle_num_threads.restype = ctypes.c_int
     return _lib
 
@@ -69,6 +73,30 @@ def adam_bf16(master, p_bits, g_bits, m, v, hp, vmax=None, carry=None):
     """In-place update: bf16 grads (uint16 bits), fp32 master/m/v, bf16 params out (uint16)."""
     lib().oracle_adam_bf16(_p(master), _p(p_bits), _p(g_bits), _p(m), _p(v), _p(vmax), _p(carry),
                            master.size, ctypes.byref(hp))
+
+
+def adam_bf16_split(hi, lo, g_bits, m, v, hp, vmax=None, carry=None):
+    """In-place update with a split master: bf16 params ``hi`` (uint16) + int16 residuals ``lo``
+    (uint16 bits), bf16 grads, fp32 m/v (include/zero_amd.h ZS_BF16_SPLIT)."""
+    for a in (hi, lo, g_bits):
+        assert a is None or (a.dtype == np.uint16 and a.flags.c_contiguous)
+    lib().oracle_adam_bf16_split(_p(hi), _p(lo), _p(g_bits), _p(m), _p(v), _p(vmax), _p(carry),
+                                 hi.size, ctypes.byref(hp))
+
+
+def split_master(master):
+    """fp32 master → (hi, lo) uint16 arrays of the split encoding."""
+    master = np.ascontiguousarray(master, np.float32)
+    hi, lo = np.zeros(master.size, np.uint16), np.zeros(master.size, np.uint16)
+    lib().oracle_split_master(_p(master), _p(hi), _p(lo), master.size)
+    return hi, lo
+
+
+def join_master(hi, lo):
+    hi, lo = np.ascontiguousarray(hi, np.uint16), np.ascontiguousarray(lo, np.uint16)
+    out = np.zeros(hi.size, np.float32)
+    lib().oracle_join_master(_p(hi), _p(lo), _p(out), hi.size)
+    return out
 
 
 def num_threads() -> int:

@@ -137,6 +137,72 @@ def test_adam_bf16_master_and_carry_vs_oracle(gpu, ws, carry):
         assert np.array_equal(cr.cpu().numpy().view(np.uint32), ccr.view(np.uint32))
 
 
+@pytest.mark.parametrize("ws,carry,ams", [(1, False, False), (4, False, True), (3, True, False)])
+def test_adam_split_master_vs_oracle(gpu, ws, carry, ams):
+    """ZS_BF16_SPLIT: the fp32 master held as the bf16 param + an int16 residual, updated in place,
+    bit-exact against the C oracle over 6 steps (vector path and a scalar tail: n % 4 == 3).
+    The start state holds every tie class of the encoding: exact ties under an even and an odd
+    bf16 param, both signs, a denormal tie, and values next to the bf16 overflow threshold."""
+    from zero_amd._lib import ZS_BF16, ZS_BF16_SPLIT
+    from zero_amd.kernels import AdamSet, adam_hparams
+
+    rng = _seed(10 * ws + carry)
+    n = 65_539
+    master0 = (rng.standard_normal(n) * 0.02).astype(np.float32)
+    special = np.array([0x3C808000, 0x3C818000, 0xBC808000, 0xBC818000, 0x00008000, 0x80008000,
+                        0x7F7F7FFF, 0x7F7F8000, 0x3F80FFFF, 0x00000000], np.uint32)
+    u = master0.view(np.uint32)
+    u[:len(special)] = special
+    u[-len(special):] = special  # and in the scalar tail
+    hi0, lo0 = c_oracle.split_master(master0)
+    # the encoding itself: exact except an even-hi tie, which moves 1 ulp toward zero
+    back = c_oracle.join_master(hi0, lo0).view(np.uint32)
+    tie_even = ((u & 0xFFFF) == 0x8000) & (((u >> 16) & 1) == 0)
+    assert np.array_equal(back[~tie_even], u[~tie_even]) and np.array_equal(back[tie_even], u[tie_even] - 1)
+    assert np.array_equal(hi0, zo.f32_to_bf16_bits(master0))
+    hi = torch.from_numpy(hi0.view(np.int16).copy()).to(gpu).view(torch.bfloat16)
+    lo = torch.from_numpy(lo0.view(np.int16).copy()).to(gpu)
+    m, v = torch.zeros(n, device=gpu), torch.zeros(n, device=gpu)
+    vm = torch.zeros(n, device=gpu) if ams else None
+    cr = torch.zeros(n, device=gpu) if carry else None
+    g = torch.zeros(n, dtype=torch.bfloat16, device=gpu)
+    aset = AdamSet(_adam_rows(g, hi, lo, hi, m, v, vmax=vm, carry=cr, n=n), ZS_BF16, ZS_BF16_SPLIT)
+    assert aset.bytes == n * (2 + 2 + 4 + 8 + 8 + 2 + (8 if ams else 0) + (8 if carry else 0))
+    chi, clo = hi0.copy(), lo0.copy()
+    cm_, cv_ = np.zeros(n, np.float32), np.zeros(n, np.float32)
+    cvm = np.zeros(n, np.float32) if ams else None
+    ccr = np.zeros(n, np.float32) if carry else None
+    for t in range(1, 7):
+        gt = torch.from_numpy((rng.standard_normal(n) * 1e-2).astype(np.float32)).to(torch.bfloat16)
+        g.copy_(gt)
+        kw = dict(grad_div=float(ws), carry_mul=float(ws - 1) if carry else 0.0)
+        aset.run(adam_hparams(1e-3, 0.9, 0.999, 1e-8, 0.0, t, amsgrad=ams, **kw),
+                 torch.cuda.current_stream())
+        c_oracle.adam_bf16_split(chi, clo, gt.view(torch.int16).numpy().view(np.uint16).copy(), cm_,
+                                 cv_, c_oracle.hparams(step=t, amsgrad=ams, **kw), vmax=cvm, carry=ccr)
+    torch.cuda.synchronize()
+    assert np.array_equal(hi.cpu().view(torch.int16).numpy().view(np.uint16), chi)
+    assert np.array_equal(lo.cpu().numpy().view(np.uint16), clo)
+    assert np.array_equal(m.cpu().numpy().view(np.uint32), cm_.view(np.uint32))
+    assert np.array_equal(v.cpu().numpy().view(np.uint32), cv_.view(np.uint32))
+    if carry:
+        assert np.array_equal(cr.cpu().numpy().view(np.uint32), ccr.view(np.uint32))
+
+
+def test_adam_split_master_rejects_bad_tables(gpu):
+    from zero_amd._lib import ZS_BF16_SPLIT, ZS_F32, ZeroAmdError
+    from zero_amd.kernels import AdamSet
+
+    n = 64
+    hi = torch.zeros(n, dtype=torch.bfloat16, device=gpu)
+    m, v = torch.zeros(n, device=gpu), torch.zeros(n, device=gpu)
+    with pytest.raises(ZeroAmdError, match="master_out"):  # no residual buffer
+        AdamSet(_adam_rows(hi, hi, None, hi, m, v, n=n), 1, ZS_BF16_SPLIT)
+    lo = torch.zeros(n, dtype=torch.int16, device=gpu)
+    with pytest.raises(ZeroAmdError, match="bf16 grads"):
+        AdamSet(_adam_rows(m, hi, lo, hi, m, v, n=n), ZS_F32, ZS_BF16_SPLIT)
+
+
 def test_adam_many_segments_unaligned_and_tails(gpu):
     """Segment table with tails, unaligned (scalar-path) segments, null grads and 1-elem segs."""
     from zero_amd._lib import ZS_F32

@@ -1,7 +1,7 @@
 """SmolLM3 training step through the ZeRO-2 drop-in: a shrunken SmolLM3
 (transformers, random init) trains with zero2.ShardedOptimizer(AdamW) in backward-overlapped mode;
 after every step every parameter's bf16 bits equal the C oracle's AdamW (decoupled weight decay,
-fp32 master) applied to the gradients the backward produced."""
+split fp32 master = bf16 param + int16 residual) applied to the gradients the backward produced."""
 import numpy as np
 import pytest
 import torch
@@ -26,9 +26,11 @@ def test_smollm3_zero2_adamw_overlap_bit_exact(gpu):
         opt = zero2.ShardedOptimizer(torch.optim.AdamW(params, lr=lr, weight_decay=wd), overlap=True,
                                      overlap_bucket_mb=0.05)
         assert opt.engine.gb.K > 1
-        master = [p.detach().float().cpu().numpy().reshape(-1).copy() for p in params]
-        m = [np.zeros_like(x) for x in master]
-        v = [np.zeros_like(x) for x in master]
+        hi = [p.detach().reshape(-1).view(torch.int16).cpu().numpy().view(np.uint16).copy()
+              for p in params]
+        lo = [np.zeros_like(x) for x in hi]  # the master starts as the bf16 param exactly
+        m = [np.zeros(x.size, np.float32) for x in hi]
+        v = [np.zeros(x.size, np.float32) for x in hi]
         g = torch.Generator(device=gpu).manual_seed(1)
         ids = torch.randint(0, cfg.vocab_size, (2, 64), device=gpu, generator=g)
         opt.zero_grad()
@@ -41,10 +43,12 @@ def test_smollm3_zero2_adamw_overlap_bit_exact(gpu):
             opt.zero_grad()
             hp = c_oracle.hparams(lr=lr, weight_decay=wd, step=t, decoupled=True)
             for i, p in enumerate(params):
-                want = np.zeros(master[i].size, np.uint16)
-                c_oracle.adam_bf16(master[i], want, grads[i], m[i], v[i], hp)
+                c_oracle.adam_bf16_split(hi[i], lo[i], grads[i], m[i], v[i], hp)
                 got = p.detach().reshape(-1).view(torch.int16).cpu().numpy().view(np.uint16)
-                assert np.array_equal(got, want), (t, i)
+                assert np.array_equal(got, hi[i]), (t, i)
+                res = opt.optimizer.state[p].get("master_residual")
+                if res is not None:  # owned params expose the residual: equal to the oracle's
+                    assert np.array_equal(res.reshape(-1).cpu().numpy().view(np.uint16), lo[i]), (t, i)
             assert torch.isfinite(loss)
     finally:
         dist.destroy_process_group()

@@ -143,3 +143,51 @@ def test_simulate_end_to_end_mlp(golden, name):
     out = zo.simulate(variant, ws, init, xs, ys, steps=steps)
     for i in range(12):
         assert rel(out["params"][-1][0][i], z[f"r0_t{steps - 1}_p{i}"]) <= 1e-4
+
+
+def test_split_master_encoding():
+    """The split master (include/zero_amd.h ZS_BF16_SPLIT) as the C oracle states it: hi is the RNE
+    bf16 of the master; (hi, lo) gives the master back bit for bit, except an exact tie that rounds
+    down to an even hi, which comes back 1 ulp toward zero (hi unchanged); NaN stays NaN."""
+    from oracle import c_oracle
+
+    rng = np.random.default_rng(7)
+    x = (rng.standard_normal(1 << 20) * 0.02).astype(np.float32)
+    u = x.view(np.uint32)
+    u[:4] = [0x3C808000, 0x3C818000, 0xBC808000, 0x00008000]  # even tie, odd tie, -even, denormal
+    u[4:8] = [0x7F7FFFFF, 0x7F7F8000, 0x7F800000, 0x7FC00001]  # overflow to inf, inf, NaN
+    hi, lo = c_oracle.split_master(x)
+    assert np.array_equal(hi[:7], zo.f32_to_bf16_bits(x[:7]))
+    back = c_oracle.join_master(hi, lo).view(np.uint32)
+    tie_even = ((u & 0xFFFF) == 0x8000) & (((u >> 16) & 1) == 0)
+    ok = ~tie_even
+    ok[7] = False
+    assert np.array_equal(back[ok], u[ok])
+    assert np.array_equal(back[tie_even], u[tie_even] - 1)
+    assert np.array_equal(c_oracle.split_master(back[tie_even].view(np.float32))[0], hi[tie_even])
+    assert np.isnan(back[7:8].view(np.float32)).all()
+    assert 0 < tie_even.sum() < 64  # ~2^-17 of uniformly random masters (+ the planted one)
+
+
+def test_split_master_adam_tracks_fp32_master():
+    """Adam on the split master follows the fp32-master oracle: identical bf16 params and state
+    over 20 steps except where a tie nudge (1 ulp of the master) propagated."""
+    from oracle import c_oracle
+
+    rng = np.random.default_rng(3)
+    n = 1 << 16
+    master = (rng.standard_normal(n) * 0.02).astype(np.float32)
+    hi, lo = c_oracle.split_master(master)
+    master = c_oracle.join_master(hi, lo)  # start from a representable master
+    m1, v1, m2, v2 = (np.zeros(n, np.float32) for _ in range(4))
+    p_ref = np.zeros(n, np.uint16)
+    for t in range(1, 21):
+        g = zo.f32_to_bf16_bits((rng.standard_normal(n) * 1e-2).astype(np.float32))
+        hp = c_oracle.hparams(step=t, grad_div=2.0)
+        c_oracle.adam_bf16(master, p_ref, g, m1, v1, hp)
+        c_oracle.adam_bf16_split(hi, lo, g, m2, v2, hp)
+    joined = c_oracle.join_master(hi, lo)
+    diff = joined.view(np.uint32) != master.view(np.uint32)
+    assert diff.mean() < 1e-3
+    assert np.max(np.abs(joined - master)) <= 4 * np.max(np.spacing(np.abs(master)))
+    assert np.mean(hi != p_ref) < 1e-3
