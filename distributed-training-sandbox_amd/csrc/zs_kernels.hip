@@ -24,8 +24,10 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int64_t kCopyChunkBytes = int64_t(kThreads) * 16 * 4;  // 16 KiB per workgroup step
-constexpr int kAdamGroups = 2;                                       // float4 groups per thread
-constexpr int64_t kAdamChunk = int64_t(kThreads) * 4 * kAdamGroups;  // 2048 elements
+// float4 groups per thread: 2 (2048-element chunks); 4 (4096) for the split master, whose 26 B/elem
+// stream has one fp32 array fewer in flight per group (+1 % measured, profiles/r01_adam_split_master.log)
+constexpr int adam_groups(bool split) { return split ? 4 : 2; }
+constexpr int64_t adam_chunk(bool split) { return int64_t(kThreads) * 4 * adam_groups(split); }
 
 int grid_cap() {
   static int cap = 0;
@@ -259,7 +261,7 @@ __device__ __forceinline__ float4 load_g4(const void* g, int64_t i) {
 }
 
 // Vector kernel: every segment 16-B aligned (8-B for bf16 arrays) with n % 4 == 0 (the host
-// splits tails off into the scalar table).  kAdamGroups float4 groups per thread, lane-contiguous
+// splits tails off into the scalar table).  adam_groups() float4 groups per thread, lane-contiguous
 // (16 B per lane per access), so each wave instruction touches one contiguous 1 KiB (f32) /
 // 512 B (bf16) run; every group's loads are issued before any math.
 template <typename GT, bool AMS, bool CARRY, bool SPLIT>
@@ -270,11 +272,12 @@ __global__ __launch_bounds__(kThreads) void adam_segments_kernel(
   for (int64_t c = blockIdx.x; c < total_chunks; c += gridDim.x) {
     while (chunk_prefix[seg + 1] <= c) ++seg;
     const AdamSeg s = segs[seg];
-    const int64_t e0 = (c - chunk_prefix[seg]) * kAdamChunk;
-    float4 g4[kAdamGroups], p4[kAdamGroups], m4[kAdamGroups], v4[kAdamGroups];
-    float4 x4[kAdamGroups], c4[kAdamGroups];
+    constexpr int G = adam_groups(SPLIT);
+    const int64_t e0 = (c - chunk_prefix[seg]) * adam_chunk(SPLIT);
+    float4 g4[G], p4[G], m4[G], v4[G];
+    float4 x4[G], c4[G];
 #pragma unroll
-    for (int u = 0; u < kAdamGroups; ++u) {
+    for (int u = 0; u < G; ++u) {
       const int64_t i = e0 + (int64_t(u) * kThreads + threadIdx.x) * 4;
       if (i < s.n) {
         g4[u] = s.g ? load_g4<GT>(s.g, i) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -293,7 +296,7 @@ __global__ __launch_bounds__(kThreads) void adam_segments_kernel(
       }
     }
 #pragma unroll
-    for (int u = 0; u < kAdamGroups; ++u) {
+    for (int u = 0; u < G; ++u) {
       const int64_t i = e0 + (int64_t(u) * kThreads + threadIdx.x) * 4;
       if (i < s.n) {
         float* gp = reinterpret_cast<float*>(&g4[u]);
@@ -758,7 +761,7 @@ int zs_adamset_create(const zs_adam_seg* in, int64_t n, int g_dtype, int p_dtype
     if (nv) {
       d.n = nv;
       vec.push_back(d);
-      vpre.push_back(vpre.back() + (nv + kAdamChunk - 1) / kAdamChunk);
+      vpre.push_back(vpre.back() + (nv + adam_chunk(split) - 1) / adam_chunk(split));
     }
     if (nv < s.n) {  // tail (or the whole unaligned segment) through the scalar kernel
       AdamSeg t = d;
