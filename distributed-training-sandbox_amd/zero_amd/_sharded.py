@@ -97,7 +97,10 @@ class ShardedOptimizerBase:
             comm = RcclComm()
             self._comm = comm
         self.engine = ShardEngine(self.params, self._group_of, self.world_size, self.rank,
-                                  layout=self._layout, carry=self._carry, comm=comm,
+                                  # ws=1 owns every param, so zero_grad clears them all and
+                                  # there is no carry (zero1.py:107-108): no buffer, no 0·A term
+                                  layout=self._layout, carry=self._carry and self.world_size > 1,
+                                  comm=comm,
                                   bucket_bytes=self._bucket_bytes, buckets=self._buckets,
                                   master=self._master)
         if self.engine.plan.layout != 0:

@@ -68,6 +68,8 @@ def run_injected(z, variant: int, rank: int, ws: int, device, comm=None, window_
             assert rel(st["exp_avg"].cpu().numpy(), z[key]) <= tol
             assert rel(st["exp_avg_sq"].cpu().numpy(), z[f"r{rank}_state_{i}_exp_avg_sq"]) <= tol
     assert opt.local_param_indices == z[f"r{rank}_local"].tolist()
+    if opt.engine is not None:  # the ZeRO-1 carry exists exactly when ws > 1 (zero1.py:107-108)
+        assert (opt.engine.carry is not None) == (variant == 1 and ws > 1)
     return worst
 
 
