@@ -2,6 +2,8 @@
 #include <cstdarg>
 #include <cstdio>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "zs_common.h"
 
 namespace {
@@ -20,4 +22,17 @@ void set_error(const char* fmt, ...) {
 extern "C" {
 int zs_abi_version(void) { return ZS_ABI_VERSION; }
 const char* zs_last_error(void) { return g_last_error; }
+
+// roctx ranges around the step's phases, named like the reference's record_function ranges
+// (zero1.py:80-91): visible to `rocprofv3 --marker-trace` beside the kernels they enclose.
+int zs_range_push(const char* name) {
+  ZS_REQUIRE(name != nullptr, "zs_range_push: name is NULL");
+  roctxRangePushA(name);
+  return ZS_OK;
+}
+
+int zs_range_pop(void) {
+  roctxRangePop();
+  return ZS_OK;
+}
 }

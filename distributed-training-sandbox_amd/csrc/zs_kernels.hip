@@ -524,6 +524,14 @@ struct zs_adamset {
   int g_dtype = ZS_F32, p_dtype = ZS_BF16, has_carry = 0, has_vmax = 0;
 };
 
+// zs_adam_step's one-range tables: [vector segment, tail segment], prefixes {0, vch, 0, sch}.
+struct AdamTables {
+  AdamSeg seg[2];
+  int64_t prefix[4];
+};
+
+__global__ void write_tables_kernel(AdamTables* __restrict__ d, AdamTables t) { *d = t; }
+
 // Table uploads run on a private non-blocking stream per device, so creating a set never
 // synchronises with the legacy null stream (which may hold kernels waiting on collectives).
 static hipStream_t upload_stream() {
@@ -554,6 +562,62 @@ static int upload(const std::vector<T>& h, T** d) {
     *d = nullptr;
     return zs::fail(ZS_ERR_HIP, "table upload failed: %s", hipGetErrorString(e));
   }
+  return ZS_OK;
+}
+
+static HP make_hp(const zs_adam_hparams* h) {
+  HP hp;
+  hp.omb1 = h->one_minus_beta1;
+  hp.beta2 = h->beta2;
+  hp.omb2 = h->one_minus_beta2;
+  hp.neg_step = h->neg_step_size;
+  hp.bc2_sqrt = h->bc2_sqrt;
+  hp.eps = h->eps;
+  hp.wd = h->weight_decay;
+  hp.decay_mul = h->decay_mul;
+  hp.grad_div = h->grad_div;
+  hp.carry_mul = h->carry_mul;
+  int exp2 = 0;
+  hp.div_pow2 = std::frexp(double(h->grad_div), &exp2) == 0.5 ? 1 : 0;
+  hp.inv_div = float(1.0 / double(h->grad_div));
+  hp.maximize = h->maximize;
+  return hp;
+}
+
+// Vector table (aligned, n % 4 == 0) then scalar table (tails, unaligned), each a segment array
+// with its chunk prefix; the template instance is picked by grad dtype, split master, amsgrad
+// and carry.
+static int launch_adam_tables(const AdamSeg* vec, const int64_t* vpre, int64_t nvec, int64_t vch,
+                              const AdamSeg* sca, const int64_t* spre, int64_t nsca, int64_t sch,
+                              int g_dtype, bool split, bool ams, bool carry, const HP& hp,
+                              hipStream_t st) {
+#define ZS_LAUNCH(KERNEL, GT, A, C, S, TAB, PRE, NS, NCH)                                     \
+  hipLaunchKernelGGL((KERNEL<GT, A, C, S>), dim3(int(std::min<int64_t>(NCH, grid_cap()))),   \
+                     dim3(kThreads), 0, st, TAB, PRE, NS, NCH, hp)
+#define ZS_DISPATCH_AC(KERNEL, GT, S, TAB, PRE, NS, NCH)                                      \
+  do {                                                                                        \
+    if (ams && carry) ZS_LAUNCH(KERNEL, GT, true, true, S, TAB, PRE, NS, NCH);                \
+    else if (ams) ZS_LAUNCH(KERNEL, GT, true, false, S, TAB, PRE, NS, NCH);                   \
+    else if (carry) ZS_LAUNCH(KERNEL, GT, false, true, S, TAB, PRE, NS, NCH);                 \
+    else ZS_LAUNCH(KERNEL, GT, false, false, S, TAB, PRE, NS, NCH);                           \
+  } while (0)
+#define ZS_DISPATCH(KERNEL, TAB, PRE, NS, NCH)                                                \
+  do {                                                                                        \
+    if (g_dtype == ZS_F32) ZS_DISPATCH_AC(KERNEL, float, false, TAB, PRE, NS, NCH);          \
+    else if (split) ZS_DISPATCH_AC(KERNEL, unsigned short, true, TAB, PRE, NS, NCH);         \
+    else ZS_DISPATCH_AC(KERNEL, unsigned short, false, TAB, PRE, NS, NCH);                   \
+  } while (0)
+  if (vch) {
+    ZS_DISPATCH(adam_segments_kernel, vec, vpre, nvec, vch);
+    ZS_HIP(hipGetLastError());
+  }
+  if (sch) {
+    ZS_DISPATCH(adam_scalar_kernel, sca, spre, nsca, sch);
+    ZS_HIP(hipGetLastError());
+  }
+#undef ZS_DISPATCH
+#undef ZS_DISPATCH_AC
+#undef ZS_LAUNCH
   return ZS_OK;
 }
 
@@ -820,53 +884,78 @@ int zs_adamset_create(const zs_adam_seg* in, int64_t n, int g_dtype, int p_dtype
 
 int zs_adamset_run(const zs_adamset* as, const zs_adam_hparams* h, uintptr_t stream) {
   ZS_REQUIRE(as && h, "zs_adamset_run: NULL argument");
-  HP hp;
-  hp.omb1 = h->one_minus_beta1;
-  hp.beta2 = h->beta2;
-  hp.omb2 = h->one_minus_beta2;
-  hp.neg_step = h->neg_step_size;
-  hp.bc2_sqrt = h->bc2_sqrt;
-  hp.eps = h->eps;
-  hp.wd = h->weight_decay;
-  hp.decay_mul = h->decay_mul;
-  hp.grad_div = h->grad_div;
-  hp.carry_mul = h->carry_mul;
-  int exp2 = 0;
-  hp.div_pow2 = std::frexp(double(h->grad_div), &exp2) == 0.5 ? 1 : 0;
-  hp.inv_div = float(1.0 / double(h->grad_div));
-  hp.maximize = h->maximize;
-  const bool ams = h->amsgrad != 0, carry = as->has_carry != 0;
-  const bool split = as->p_dtype == ZS_BF16_SPLIT;
+  const bool ams = h->amsgrad != 0;
   ZS_REQUIRE(!ams || as->has_vmax || (as->nvec + as->nsca) == 0,
              "zs_adamset_run: amsgrad needs vmax segments");
+  return launch_adam_tables(as->d_vec, as->d_vec_prefix, as->nvec, as->vec_chunks, as->d_sca,
+                            as->d_sca_prefix, as->nsca, as->sca_chunks, as->g_dtype,
+                            as->p_dtype == ZS_BF16_SPLIT, ams, as->has_carry != 0, make_hp(h),
+                            reinterpret_cast<hipStream_t>(stream));
+}
+
+// zs_adam_step: one contiguous range through the same kernels.  Its two one-entry tables
+// (vector part + tail) are written on the caller's stream by a one-thread kernel into a
+// stream-ordered allocation, so the call neither synchronises nor keeps state between calls.
+int zs_adam_step(float* p, uint16_t* p_bf16, const void* g, int g_dtype, float* m, float* v,
+                 int64_t n, double lr, double beta1, double beta2, double eps, double weight_decay,
+                 int decoupled, int64_t step, double grad_div, float* carry, double carry_mul,
+                 uintptr_t stream) {
+  ZS_REQUIRE(n >= 0, "zs_adam_step: n < 0");
+  ZS_REQUIRE(g_dtype == ZS_F32 || g_dtype == ZS_BF16, "zs_adam_step: bad g_dtype %d", g_dtype);
+  ZS_REQUIRE(n == 0 || (p && m && v), "zs_adam_step: p, m and v must be non-NULL");
+  zs_adam_hparams h;
+  int rc = zs_adam_hparams_init(lr, beta1, beta2, eps, weight_decay, decoupled, 0, 0, step,
+                                grad_div, carry_mul, &h);
+  if (rc != ZS_OK) return rc;
+  if (n == 0) return ZS_OK;
+  const int64_t gsz = g_dtype == ZS_F32 ? 4 : 2;
+  const uint64_t up = reinterpret_cast<uint64_t>(p), ug = reinterpret_cast<uint64_t>(g);
+  const uint64_t ub = reinterpret_cast<uint64_t>(p_bf16), um = reinterpret_cast<uint64_t>(m);
+  const uint64_t uv = reinterpret_cast<uint64_t>(v), uc = reinterpret_cast<uint64_t>(carry);
+  const bool ok = aligned(ug, uint64_t(gsz) * 4) && aligned(up, 16) && aligned(ub, 8) &&
+                  aligned(um, 16) && aligned(uv, 16) && aligned(uc, 16);
+  const int64_t nv = ok ? (n & ~int64_t(3)) : 0;
+  AdamTables t;
+  AdamSeg& a = t.seg[0];
+  a.g = g;
+  a.master = p;
+  a.master_out = p;
+  a.p_out = reinterpret_cast<unsigned short*>(p_bf16);
+  a.m = m;
+  a.v = v;
+  a.vmax = nullptr;
+  a.carry = carry;
+  a.n = nv;
+  AdamSeg& b = t.seg[1];
+  b = a;
+  b.g = g ? reinterpret_cast<const void*>(ug + uint64_t(nv * gsz)) : nullptr;
+  b.master = p + nv;
+  b.master_out = p + nv;
+  b.p_out = p_bf16 ? reinterpret_cast<unsigned short*>(p_bf16 + nv) : nullptr;
+  b.m = m + nv;
+  b.v = v + nv;
+  b.carry = carry ? carry + nv : nullptr;
+  b.n = n - nv;
+  const int64_t vch = (nv + adam_chunk(false) - 1) / adam_chunk(false);
+  const int64_t sch = (b.n + kThreads - 1) / kThreads;
+  t.prefix[0] = 0;
+  t.prefix[1] = vch;
+  t.prefix[2] = 0;
+  t.prefix[3] = sch;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-#define ZS_LAUNCH(KERNEL, GT, A, C, S, TAB, PRE, NS, NCH)                                     \
-  hipLaunchKernelGGL((KERNEL<GT, A, C, S>), dim3(int(std::min<int64_t>(NCH, grid_cap()))),   \
-                     dim3(kThreads), 0, st, TAB, PRE, NS, NCH, hp)
-#define ZS_DISPATCH_AC(KERNEL, GT, S, TAB, PRE, NS, NCH)                                      \
-  do {                                                                                        \
-    if (ams && carry) ZS_LAUNCH(KERNEL, GT, true, true, S, TAB, PRE, NS, NCH);                \
-    else if (ams) ZS_LAUNCH(KERNEL, GT, true, false, S, TAB, PRE, NS, NCH);                   \
-    else if (carry) ZS_LAUNCH(KERNEL, GT, false, true, S, TAB, PRE, NS, NCH);                 \
-    else ZS_LAUNCH(KERNEL, GT, false, false, S, TAB, PRE, NS, NCH);                           \
-  } while (0)
-#define ZS_DISPATCH(KERNEL, TAB, PRE, NS, NCH)                                                \
-  do {                                                                                        \
-    if (as->g_dtype == ZS_F32) ZS_DISPATCH_AC(KERNEL, float, false, TAB, PRE, NS, NCH);      \
-    else if (split) ZS_DISPATCH_AC(KERNEL, unsigned short, true, TAB, PRE, NS, NCH);         \
-    else ZS_DISPATCH_AC(KERNEL, unsigned short, false, TAB, PRE, NS, NCH);                   \
-  } while (0)
-  if (as->vec_chunks) {
-    ZS_DISPATCH(adam_segments_kernel, as->d_vec, as->d_vec_prefix, as->nvec, as->vec_chunks);
-    ZS_HIP(hipGetLastError());
+  AdamTables* d = nullptr;
+  ZS_HIP(hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(AdamTables), st));
+  hipLaunchKernelGGL(write_tables_kernel, dim3(1), dim3(1), 0, st, d, t);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) {
+    rc = launch_adam_tables(d->seg, d->prefix, 1, vch, d->seg + 1, d->prefix + 2, 1, sch, g_dtype,
+                            false, false, carry != nullptr, make_hp(&h), st);
   }
-  if (as->sca_chunks) {
-    ZS_DISPATCH(adam_scalar_kernel, as->d_sca, as->d_sca_prefix, as->nsca, as->sca_chunks);
-    ZS_HIP(hipGetLastError());
-  }
-#undef ZS_DISPATCH
-#undef ZS_DISPATCH_AC
-#undef ZS_LAUNCH
+  const hipError_t ef = hipFreeAsync(d, st);  // after the launches, in stream order
+  if (e != hipSuccess)
+    return zs::fail(ZS_ERR_HIP, "zs_adam_step: table kernel: %s", hipGetErrorString(e));
+  if (rc != ZS_OK) return rc;
+  ZS_HIP(ef);
   return ZS_OK;
 }
 

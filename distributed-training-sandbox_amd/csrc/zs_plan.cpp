@@ -1,6 +1,7 @@
 // Layout planner: parameter ownership, per-rank optimizer-shard streams and bucket segments.
 //
-// Host-only (no HIP calls), so it runs in the CPU test suite.  Ownership follows the reference's
+// Host-only (no HIP calls of its own: zs_pack / zs_unpack launch through the copy-set API), so
+// the planner runs in the CPU test suite.  Ownership follows the reference's
 // ShardedOptimizer.__init__ exactly (zero1.py:55-62, zero2.py:51-58, zero3.py:93-100):
 //     ppr = n // ws, rem = n % ws
 //     start_r = r*ppr + min(r, rem), end_r = start_r + ppr + (r < rem)
@@ -19,7 +20,9 @@
 // collective move 1.52x the data; the ragged tail moves only the bytes that exist.
 #include <algorithm>
 #include <cstring>
+#include <map>
 #include <new>
+#include <utility>
 #include <vector>
 
 #include "zs_common.h"
@@ -41,6 +44,12 @@ struct Bucket {
 
 inline int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
+// zs_pack / zs_unpack descriptor tables of one bucket, keyed by the pointers they were built for.
+struct CopyCache {
+  std::vector<uint64_t> sig;
+  zs_copyset* cs = nullptr;
+};
+
 }  // namespace
 
 struct zs_plan {
@@ -53,6 +62,12 @@ struct zs_plan {
   std::vector<int64_t> stream_len;         // per rank
   std::vector<Bucket> buckets;
   std::vector<std::vector<Seg>> segs;      // per bucket
+  std::map<std::pair<int64_t, int>, CopyCache> copy_cache;  // (bucket, 0 = pack / 1 = unpack)
+  std::vector<zs_copyset*> retired;  // tables replaced while a copy might still read them
+  ~zs_plan() {
+    for (auto& kv : copy_cache) zs_copyset_destroy(kv.second.cs);
+    for (zs_copyset* cs : retired) zs_copyset_destroy(cs);
+  }
 };
 
 static void owner_range(int64_t n, int ws, int r, int64_t* s, int64_t* e) {
@@ -65,6 +80,44 @@ static int owner_of(int64_t n, int ws, int64_t i) {
   const int64_t ppr = n / ws, rem = n % ws;
   if (i < (ppr + 1) * rem) return int(i / (ppr + 1));
   return int((i - rem) / ppr);
+}
+
+// zs_pack (unpack = 0: param grads -> bucket) / zs_unpack (unpack = 1: bucket -> params) of every
+// segment of `bucket`, through a cached copy set (host work only when the pointers change).
+static int bucket_copy(zs_plan* p, int64_t bucket, int unpack, const uint64_t* ptrs, uint64_t buf,
+                       int dtype, uintptr_t stream, const char* fn) {
+  ZS_REQUIRE(p && ptrs, "%s: NULL argument", fn);
+  ZS_REQUIRE(bucket >= 0 && bucket < p->K, "%s: bucket %lld out of range", fn, (long long)bucket);
+  ZS_REQUIRE(dtype == ZS_F32 || dtype == ZS_BF16, "%s: dtype must be ZS_F32 or ZS_BF16 (got %d)",
+             fn, dtype);
+  ZS_REQUIRE(buf != 0, "%s: bucket buffer is NULL", fn);
+  const uint64_t es = dtype == ZS_F32 ? 4 : 2;
+  const auto& v = p->segs[bucket];
+  const size_t n = v.size();
+  std::vector<uint64_t> sig(2 * n + 1);  // src[n] | dst[n] | element size
+  std::vector<int64_t> nb(n);
+  for (size_t j = 0; j < n; ++j) {
+    const Seg& s = v[j];
+    const uint64_t prm = ptrs[s.param];
+    const uint64_t q = prm ? prm + uint64_t(s.param_off) * es : 0;
+    const uint64_t b = buf + uint64_t(s.buf_off) * es;
+    ZS_REQUIRE(!unpack || q != 0 || s.len == 0, "%s: param_ptrs[%lld] is NULL", fn,
+               (long long)s.param);
+    sig[j] = unpack ? b : q;  // a NULL grad source zero-fills its slot
+    sig[n + j] = unpack ? q : b;
+    nb[j] = s.len * int64_t(es);
+  }
+  sig[2 * n] = es;
+  CopyCache& c = p->copy_cache[{bucket, unpack}];
+  if (!c.cs || c.sig != sig) {
+    zs_copyset* cs = nullptr;
+    const int rc = zs_copyset_create(sig.data(), sig.data() + n, nb.data(), int64_t(n), &cs);
+    if (rc != ZS_OK) return rc;
+    if (c.cs) p->retired.push_back(c.cs);
+    c.cs = cs;
+    c.sig = std::move(sig);
+  }
+  return zs_copyset_run(c.cs, stream);
 }
 
 // Buckets over the per-rank streams, then the segments (param slices) of every bucket.
@@ -309,6 +362,33 @@ int zs_plan_pieces(const zs_plan* p, int rank, int64_t* param, int64_t* param_of
     len[j] = v[j].len;
   }
   return ZS_OK;
+}
+
+int zs_plan_num_buckets(const zs_plan* p, int64_t* n) {
+  ZS_REQUIRE(p && n, "zs_plan_num_buckets: NULL argument");
+  *n = p->K;
+  return ZS_OK;
+}
+
+int zs_plan_bucket_bytes(const zs_plan* p, int64_t bucket, int dtype, int64_t* bytes) {
+  ZS_REQUIRE(p && bytes, "zs_plan_bucket_bytes: NULL argument");
+  ZS_REQUIRE(bucket >= 0 && bucket < p->K, "zs_plan_bucket_bytes: bucket %lld out of range",
+             (long long)bucket);
+  ZS_REQUIRE(dtype == ZS_F32 || dtype == ZS_BF16, "zs_plan_bucket_bytes: bad dtype %d", dtype);
+  *bytes = p->buckets[bucket].elems * (dtype == ZS_F32 ? 4 : 2);
+  return ZS_OK;
+}
+
+int zs_pack(zs_plan* p, int64_t bucket, const uint64_t* grad_ptrs, void* bucket_buf, int dtype,
+            uintptr_t stream) {
+  return bucket_copy(p, bucket, 0, grad_ptrs, reinterpret_cast<uint64_t>(bucket_buf), dtype,
+                     stream, "zs_pack");
+}
+
+int zs_unpack(zs_plan* p, int64_t bucket, const void* bucket_buf, const uint64_t* param_ptrs,
+              int dtype, uintptr_t stream) {
+  return bucket_copy(p, bucket, 1, param_ptrs, reinterpret_cast<uint64_t>(bucket_buf), dtype,
+                     stream, "zs_unpack");
 }
 
 int zs_plan_num_segments(const zs_plan* p, int64_t bucket, int64_t* n) {

@@ -32,7 +32,6 @@ from __future__ import annotations
 
 import numpy as np
 import torch
-from torch.profiler import record_function  # the reference's step() ranges (zero1.py:80-91)
 
 from . import _lib
 from .comm import comm_stream, zs_dtype
@@ -315,7 +314,7 @@ class ShardEngine:
         else:
             p = pptr + po.astype(np.uint64) * np.uint64(4)
             rows = self._adam_rows(idx, g, p, p, 0, so, n)
-        with record_function("optimizer_step"):  # zero1.py:88
+        with _lib.phase_range("optimizer_step"):  # zero1.py:88
             self._run_adam("local", rows, idx, hparams_of, stream)
 
     def _run_copy(self, kind, cs, stream):
@@ -369,7 +368,7 @@ class ShardEngine:
         r = self.rank
         cs = self.comm_stream
         self.ev_c0.record(cs)
-        with record_function("all_reduce_gradients"):  # zero1.py:80-84: pack + reduce-scatter
+        with _lib.phase_range("all_reduce_gradients"):  # zero1.py:80-84: pack + reduce-scatter
             for k in range(self.K):  # pack every bucket on the compute stream
                 s, b = self.segs[k], self.buckets[k]
                 src = np.where(has[s.param], gptr[s.param] + s.param_off.astype(np.uint64) * es, 0)
@@ -383,7 +382,7 @@ class ShardEngine:
                 cs.wait_event(self.ev_pack[k])
                 self._collective(k, "rs")
                 self.ev_rs[k].record(cs)
-        with record_function("optimizer_step"):  # zero1.py:88
+        with _lib.phase_range("optimizer_step"):  # zero1.py:88
             for k in range(self.K):  # fused Adam on this rank's window
                 stream.wait_event(self.ev_rs[k])
                 s, b = self.segs[k], self.buckets[k]
@@ -407,7 +406,7 @@ class ShardEngine:
                     self._cached(("pass", k), src.tobytes() + slot[dead].tobytes(),
                                  lambda: CopySet(src, slot[dead], nb)).run(stream)
                 self.ev_adam[k].record(stream)
-        with record_function("broadcast_parameters"):  # zero1.py:91-102: all-gather + unpack
+        with _lib.phase_range("broadcast_parameters"):  # zero1.py:91-102: all-gather + unpack
             for k in range(self.K):  # in-place all-gather (-v) of the updated windows
                 cs.wait_event(self.ev_adam[k])
                 self._collective(k, "ag")
@@ -453,57 +452,61 @@ class ShardEngine:
 
     def _step_overlap(self, has, hparams_of, stream):
         gb, r, es = self.gb, self.rank, np.uint64(self.es)
-        gb.flush()
+        with _lib.phase_range("all_reduce_gradients"):  # zero1.py:80-84: reduces left by backward
+            gb.flush()
         cs = gb.comm_stream
         base = np.uint64(gb.buf.data_ptr())
-        for k in range(gb.K):  # fused Adam on the owned buckets, reading the reduced grads
-            if gb.key[k] != r:
-                continue
-            stream.wait_event(gb.ev_done[k])
-            idx = np.array([i for i in gb.groups[k] if has[i]], np.int64)
-            if len(idx):
-                slot = base + gb.slot[idx].astype(np.uint64) * es
-                so = np.array([self._so_of[int(i)] for i in idx], np.int64)
-                ln = np.array([self.params[int(i)].numel() for i in idx], np.int64)
-                p = np.fromiter((_ptr(self.params[int(i)]) for i in idx), np.uint64, len(idx))
-                # ws > 1: the updated params go into the slot, which the broadcast sends; ws == 1:
-                # straight into module storage (no broadcast, no unpack)
-                out = slot if self.ws > 1 else p
-                if self.mixed:
-                    rows = self._mixed_rows(idx, slot, p, out, so, ln)
-                else:
-                    rows = self._adam_rows(idx, slot, p, out, 0, so, ln)
-                self._run_adam(("overlap", k), rows, idx, hparams_of, stream)
-            dead = [i for i in gb.groups[k] if not has[i]]
-            if dead and self.ws > 1:  # params without a grad keep their value: copy into the slot
-                src = [_ptr(self.params[i]) for i in dead]
-                dst = [int(base) + int(gb.slot[i]) * self.es for i in dead]
-                self._cached(("opass", k), np.array(src + dst, np.uint64).tobytes(),
+        with _lib.phase_range("optimizer_step"):  # zero1.py:88
+            for k in range(gb.K):  # fused Adam on the owned buckets, reading the reduced grads
+                if gb.key[k] != r:
+                    continue
+                stream.wait_event(gb.ev_done[k])
+                idx = np.array([i for i in gb.groups[k] if has[i]], np.int64)
+                if len(idx):
+                    slot = base + gb.slot[idx].astype(np.uint64) * es
+                    so = np.array([self._so_of[int(i)] for i in idx], np.int64)
+                    ln = np.array([self.params[int(i)].numel() for i in idx], np.int64)
+                    p = np.fromiter((_ptr(self.params[int(i)]) for i in idx), np.uint64, len(idx))
+                    # ws > 1: the updated params go into the slot, which the broadcast
+                    # sends; ws == 1: straight into module storage (no broadcast, no unpack)
+                    out = slot if self.ws > 1 else p
+                    if self.mixed:
+                        rows = self._mixed_rows(idx, slot, p, out, so, ln)
+                    else:
+                        rows = self._adam_rows(idx, slot, p, out, 0, so, ln)
+                    self._run_adam(("overlap", k), rows, idx, hparams_of, stream)
+                dead = [i for i in gb.groups[k] if not has[i]]
+                if dead and self.ws > 1:  # params without a grad keep their value: copy into the slot
+                    src = [_ptr(self.params[i]) for i in dead]
+                    dst = [int(base) + int(gb.slot[i]) * self.es for i in dead]
+                    self._cached(("opass", k), np.array(src + dst, np.uint64).tobytes(),
+                                 lambda: CopySet(src, dst, [self.params[i].numel() * self.es
+                                                            for i in dead])).run(stream)
+                self.ev_oadam[k].record(stream)
+        with _lib.phase_range("broadcast_parameters"):  # zero1.py:91-102: broadcast + unpack
+            if self.ws > 1:
+                self.ev_c0.record(cs)
+                for k in range(gb.K):  # every rank, same order: broadcast each bucket from its owner
+                    cs.wait_event(self.ev_oadam[k] if gb.key[k] == r else gb.ev_done[k])
+                    region = gb.region(k)
+                    if self.comm_events is not None:
+                        e0 = torch.cuda.Event(enable_timing=True)
+                        e1 = torch.cuda.Event(enable_timing=True)
+                        e0.record(cs)
+                    self.comm.broadcast(region, gb.key[k], cs)
+                    if self.comm_events is not None:
+                        e1.record(cs)
+                        self.comm_events.append(("ag", False, e0, e1, region.numel() * self.es))
+                    self.ev_obc[k].record(cs)
+                self.ev_c1.record(cs)
+            for k in range(gb.K if self.ws > 1 else 0):  # unpack updated params into module storage
+                stream.wait_event(self.ev_obc[k])
+                g = gb.groups[k]
+                src = [int(base) + int(gb.slot[i]) * self.es for i in g]
+                dst = [_ptr(self.params[i]) for i in g]
+                self._cached(("ounpack", k), np.array(dst, np.uint64).tobytes(),
                              lambda: CopySet(src, dst, [self.params[i].numel() * self.es
-                                                        for i in dead])).run(stream)
-            self.ev_oadam[k].record(stream)
-        if self.ws > 1:
-            self.ev_c0.record(cs)
-            for k in range(gb.K):  # every rank, same order: broadcast each bucket from its owner
-                cs.wait_event(self.ev_oadam[k] if gb.key[k] == r else gb.ev_done[k])
-                region = gb.region(k)
-                if self.comm_events is not None:
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record(cs)
-                self.comm.broadcast(region, gb.key[k], cs)
-                if self.comm_events is not None:
-                    e1.record(cs)
-                    self.comm_events.append(("ag", False, e0, e1, region.numel() * self.es))
-                self.ev_obc[k].record(cs)
-            self.ev_c1.record(cs)
-        for k in range(gb.K if self.ws > 1 else 0):  # unpack updated params into module storage
-            stream.wait_event(self.ev_obc[k])
-            g = gb.groups[k]
-            src = [int(base) + int(gb.slot[i]) * self.es for i in g]
-            dst = [_ptr(self.params[i]) for i in g]
-            self._cached(("ounpack", k), np.array(dst, np.uint64).tobytes(),
-                         lambda: CopySet(src, dst, [self.params[i].numel() * self.es
-                                                    for i in g])).run(stream)
+                                                        for i in g])).run(stream)
         gb.reset()
 
     def comm_time_s(self) -> float:

@@ -2,6 +2,7 @@
 
 ``CopySet``  — one launch of the descriptor-driven gather/scatter copy (pack / unpack).
 ``AdamSet``  — one launch of the fused Adam/AdamW update over a list of segments.
+``adam_step`` — the same update over one contiguous range (zs_adam_step; no table to keep).
 
 Both upload their segment table once; ``run(stream)`` only enqueues a kernel on ``stream``.
 They raise ``ZeroAmdError`` on any failure; there is no CPU path.
@@ -89,3 +90,28 @@ class AdamSet:
             except Exception:  # interpreter teardown
                 pass
             self._h = None
+
+
+def adam_step(p, g, m, v, *, step, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0,
+              decoupled=False, grad_div=1.0, p_bf16=None, carry=None, carry_mul=0.0,
+              stream=None) -> None:
+    """One Adam/AdamW step over the contiguous fp32 tensors ``p`` / ``m`` / ``v`` (in place) with
+    gradient sum ``g`` (fp32 or bf16, or None = zero) divided by ``grad_div``; optional bf16 copy
+    of the result into ``p_bf16`` and ZeRO-1 carry.  Enqueued on ``stream`` (default: torch's
+    current stream on p's device)."""
+    import torch
+
+    n = p.numel()
+    for name, t in (("p", p), ("m", m), ("v", v), ("carry", carry)):
+        if t is not None:
+            assert t.dtype == torch.float32 and t.is_contiguous() and t.numel() == n, name
+    if g is not None:
+        assert g.dtype in (torch.float32, torch.bfloat16) and g.is_contiguous() and g.numel() == n
+    if p_bf16 is not None:
+        assert p_bf16.dtype == torch.bfloat16 and p_bf16.is_contiguous() and p_bf16.numel() == n
+    g_dtype = _lib.ZS_BF16 if g is not None and g.dtype == torch.bfloat16 else _lib.ZS_F32
+    ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    st = torch.cuda.current_stream(p.device) if stream is None else stream
+    _lib.call("zs_adam_step", ptr(p), ptr(p_bf16), ptr(g), g_dtype, ptr(m), ptr(v), n, float(lr),
+              float(beta1), float(beta2), float(eps), float(weight_decay), int(bool(decoupled)),
+              int(step), float(grad_div), ptr(carry), float(carry_mul), stream_handle(st))

@@ -124,3 +124,24 @@ class Plan:
         _lib.call("zs_plan_bucket", self._h, int(k), ctypes.byref(ao), ctypes.byref(el),
                   ctypes.byref(ev), *(_i64p(a) for a in arrs))
         return Bucket(ao.value, el.value, bool(ev.value), *arrs)
+
+    # --- bucket copies straight from the plan (zs_pack / zs_unpack) -------------------------
+    def bucket_bytes(self, k: int, dtype: int) -> int:
+        b = ctypes.c_int64()
+        _lib.call("zs_plan_bucket_bytes", self._h, int(k), int(dtype), ctypes.byref(b))
+        return b.value
+
+    def pack(self, k: int, grad_ptrs, bucket_ptr: int, dtype: int, stream: int) -> None:
+        """Copy every segment of bucket ``k`` from the per-parameter grads (device pointers
+        indexed by parameter; 0 = zeros) into the bucket buffer at ``bucket_ptr``."""
+        ptrs = np.ascontiguousarray(np.asarray(grad_ptrs, dtype=np.uint64))
+        assert ptrs.shape == (self.n,)
+        _lib.call("zs_pack", self._h, int(k), ptrs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                  int(bucket_ptr), int(dtype), int(stream))
+
+    def unpack(self, k: int, bucket_ptr: int, param_ptrs, dtype: int, stream: int) -> None:
+        """Scatter every segment of bucket ``k`` back into the parameters."""
+        ptrs = np.ascontiguousarray(np.asarray(param_ptrs, dtype=np.uint64))
+        assert ptrs.shape == (self.n,)
+        _lib.call("zs_unpack", self._h, int(k), int(bucket_ptr),
+                  ptrs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), int(dtype), int(stream))

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ZS_ABI_VERSION 3
+#define ZS_ABI_VERSION 4
 
 enum zs_status {
   ZS_OK = 0,
@@ -57,6 +57,13 @@ enum zs_bucket_mode {
 
 int zs_abi_version(void);
 const char* zs_last_error(void);
+
+/* roctx range around a phase of step(), named like the reference's torch.profiler ranges
+ * "all_reduce_gradients" / "optimizer_step" / "broadcast_parameters" (zero1.py:80-91), so
+ * `rocprofv3 --marker-trace` shows which kernels and collectives each phase enqueued.  Host only;
+ * no-ops unless a profiler is attached. */
+int zs_range_push(const char* name);
+int zs_range_pop(void);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Layout planner (host only; callable without a GPU).                                         */
@@ -108,6 +115,25 @@ int zs_plan_bucket(const zs_plan* plan, int64_t bucket, int64_t* arena_off, int6
 int zs_plan_num_segments(const zs_plan* plan, int64_t bucket, int64_t* n);
 int zs_plan_segments(const zs_plan* plan, int64_t bucket, int64_t* param, int64_t* rank,
                      int64_t* param_off, int64_t* buf_off, int64_t* len);
+
+/* Number of buckets K (= info[5]) and the byte size of bucket k's buffer for dtype ZS_F32 /
+ * ZS_BF16 (SURVEY.md §8(b) zs_plan_num_buckets / zs_plan_bucket_bytes). */
+int zs_plan_num_buckets(const zs_plan* plan, int64_t* n);
+int zs_plan_bucket_bytes(const zs_plan* plan, int64_t bucket, int dtype, int64_t* bytes);
+
+/* Pack / unpack one bucket straight from the plan (SURVEY.md §8(b) zs_pack / zs_unpack).
+ * grad_ptrs / param_ptrs: n_params device pointers indexed by parameter (flattened, dtype ZS_F32
+ * or ZS_BF16); bucket_buf: the bucket's buffer (zs_plan_bucket_bytes long).  zs_pack copies every
+ * segment of every rank's window (zero2.py:99-104 without the ws-fold torch.cat) — a NULL grad
+ * is written as zeros; zs_unpack scatters every segment back into the params (the per-tensor
+ * broadcast of zero2.py:122-133 after the all-gather).  Window padding is never written: zero
+ * the buffer once.  The descriptor tables are built on the first call and reused while the
+ * pointers are unchanged; tables replaced by new pointers are kept until zs_plan_destroy, which
+ * must not be called while a pack / unpack of the plan may still run. */
+int zs_pack(zs_plan* plan, int64_t bucket, const uint64_t* grad_ptrs, void* bucket_buf, int dtype,
+            uintptr_t stream);
+int zs_unpack(zs_plan* plan, int64_t bucket, const void* bucket_buf, const uint64_t* param_ptrs,
+              int dtype, uintptr_t stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Segment copy (pack / unpack).  Replaces the flatten + torch.cat([g]*ws) copies of            */
@@ -196,6 +222,21 @@ int zs_adamset_run(const zs_adamset* as, const zs_adam_hparams* hp, uintptr_t st
 int zs_adamset_destroy(zs_adamset* as);
 /* total elements covered by the set and algorithmic HBM bytes one run moves */
 int zs_adamset_stats(const zs_adamset* as, int64_t* elems, int64_t* bytes);
+
+/* Single-range form (SURVEY.md §8(b) `zs_adam_step`): one torch.optim.Adam/AdamW step over n
+ * contiguous elements — the update of one flat shard (zero1.py:88 on a flattened group) with no
+ * table to build.  p: fp32 master/param, updated in place; p_bf16: optional bf16 copy of the
+ * result (NULL = none); g: reduced gradient sum (g_dtype ZS_F32 or ZS_BF16; NULL = zero); m, v:
+ * fp32 exp_avg / exp_avg_sq, in place; carry: ZeRO-1's A_{t-1}, rewritten with A_t (NULL = none).
+ * The scalars are doubles because torch derives them from Python floats (adam.py:508-515); the
+ * gradient is DIVIDED by grad_div (the world size), as zero1.py:84 `p.grad /= ws` does — for a
+ * non-power-of-two ws that is not the same as multiplying by 1/ws.  Same kernels and bits as
+ * zs_adamset_run; amsgrad / maximize / the split master need an adamset.  Asynchronous on
+ * `stream`; its two-entry table is a stream-ordered allocation freed in stream order. */
+int zs_adam_step(float* p, uint16_t* p_bf16, const void* g, int g_dtype, float* m, float* v,
+                 int64_t n, double lr, double beta1, double beta2, double eps, double weight_decay,
+                 int decoupled, int64_t step, double grad_div, float* carry, double carry_mul,
+                 uintptr_t stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* RCCL over xGMI.  Replaces the per-tensor dist.all_reduce (zero1.py:83, zero3.py:146),        */

@@ -35,7 +35,7 @@ def test_library_is_gfx950_code_object():
 def test_abi_version_and_error_text():
     from zero_amd import _lib
 
-    assert _lib.lib.zs_abi_version() == _lib.ABI_VERSION == 3
+    assert _lib.lib.zs_abi_version() == _lib.ABI_VERSION == 4
     h = ctypes.c_void_p()
     rc = _lib.lib.zs_plan_create(0, None, None, 0, 0, 0, 64, 0, 0, ctypes.byref(h))
     assert rc == _lib.ZS_ERR_INVALID
@@ -94,3 +94,54 @@ def test_new_entry_points_validate_arguments():
     arr = (ctypes.c_int64 * 2)()
     assert lib.zs_plan_bucket(plan._h, plan.num_buckets, ctypes.byref(ao), ctypes.byref(el),
                               ctypes.byref(ev), arr, arr, arr) == _lib.ZS_ERR_INVALID
+
+
+def test_phase_ranges_nest_and_validate():
+    """roctx phase ranges (zero1.py:80-91 names) push/pop on the host without a GPU; a NULL name
+    is rejected with a message instead of reaching roctx."""
+    from zero_amd import _lib
+
+    with _lib.phase_range("all_reduce_gradients"):
+        with _lib.phase_range("optimizer_step"):
+            pass
+    assert _lib.lib.zs_range_push(None) == _lib.ZS_ERR_INVALID
+    assert b"name is NULL" in _lib.lib.zs_last_error()
+    with pytest.raises(RuntimeError):
+        with _lib.phase_range("broadcast_parameters"):
+            raise RuntimeError("propagates; the range is still popped")
+
+
+def test_contract_entry_points_validate_without_gpu():
+    """SURVEY.md §8(b)'s single-call forms (zs_plan_num_buckets / zs_plan_bucket_bytes / zs_pack /
+    zs_unpack / zs_adam_step) answer or reject before touching the device."""
+    from zero_amd import _lib
+    from zero_amd.plan import Plan
+
+    lib = _lib.lib
+    plan = Plan([100, 300, 5], 2, 0, window_elems=64)
+    n = ctypes.c_int64()
+    assert lib.zs_plan_num_buckets(plan._h, ctypes.byref(n)) == _lib.ZS_OK
+    assert n.value == plan.num_buckets > 0
+    for k in range(plan.num_buckets):
+        assert plan.bucket_bytes(k, _lib.ZS_F32) == 4 * plan.bucket(k).elems
+        assert plan.bucket_bytes(k, _lib.ZS_BF16) == 2 * plan.bucket(k).elems
+    b = ctypes.c_int64()
+    assert lib.zs_plan_bucket_bytes(plan._h, plan.num_buckets, _lib.ZS_F32, ctypes.byref(b)) == _lib.ZS_ERR_INVALID
+    assert lib.zs_plan_bucket_bytes(plan._h, 0, _lib.ZS_U8, ctypes.byref(b)) == _lib.ZS_ERR_INVALID
+    ptrs = (ctypes.c_uint64 * 3)(0, 0, 0)
+    assert lib.zs_pack(None, 0, ptrs, 4096, _lib.ZS_F32, 0) == _lib.ZS_ERR_INVALID
+    assert lib.zs_pack(plan._h, plan.num_buckets, ptrs, 4096, _lib.ZS_F32, 0) == _lib.ZS_ERR_INVALID
+    assert b"out of range" in lib.zs_last_error()
+    assert lib.zs_pack(plan._h, 0, ptrs, 4096, _lib.ZS_U8, 0) == _lib.ZS_ERR_INVALID
+    assert lib.zs_pack(plan._h, 0, ptrs, None, _lib.ZS_F32, 0) == _lib.ZS_ERR_INVALID
+    assert lib.zs_unpack(plan._h, 0, 4096, ptrs, _lib.ZS_F32, 0) == _lib.ZS_ERR_INVALID
+    assert b"param_ptrs" in lib.zs_last_error()  # unpack has nowhere to put a NULL param
+    f = ctypes.c_double
+    args = lambda n_, gd, step: (None, None, None, gd, None, None, n_, f(1e-3), f(0.9), f(0.999),  # noqa: E731
+                                 f(1e-8), f(0.0), 0, step, f(1.0), None, f(0.0), 0)
+    assert lib.zs_adam_step(*args(-1, _lib.ZS_F32, 1)) == _lib.ZS_ERR_INVALID
+    assert lib.zs_adam_step(*args(8, _lib.ZS_U8, 1)) == _lib.ZS_ERR_INVALID
+    assert lib.zs_adam_step(*args(8, _lib.ZS_F32, 1)) == _lib.ZS_ERR_INVALID
+    assert b"non-NULL" in lib.zs_last_error()
+    assert lib.zs_adam_step(*args(0, _lib.ZS_F32, 0)) == _lib.ZS_ERR_INVALID  # step must be >= 1
+    assert lib.zs_adam_step(*args(0, _lib.ZS_BF16, 1)) == _lib.ZS_OK  # empty: nothing to launch

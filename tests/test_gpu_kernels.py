@@ -261,3 +261,88 @@ def test_pack_unpack_round_trip_c2(gpu):
     torch.cuda.synchronize()
     for p, o in zip(ps, outs):
         assert torch.equal(p, o)
+
+
+@pytest.mark.parametrize("case", ["f32_l2_ws3", "bf16_out_carry_ws4", "adamw_f32", "unaligned_bf16"])
+def test_adam_step_single_range_vs_oracle(gpu, case):
+    """zs_adam_step (SURVEY.md §8(b)'s single-range form) is bit-exact against the C oracle over
+    3 steps: vector body + scalar tail (n = 100,003), grad / ws for ws = 3 and 4, ZeRO-1 carry,
+    L2 / AdamW decay, and a range offset by one element (scalar path throughout)."""
+    from zero_amd.kernels import adam_step
+
+    rng = _seed(["f32_l2_ws3", "bf16_out_carry_ws4", "adamw_f32", "unaligned_bf16"].index(case) + 40)
+    n = 100_003
+    bf16 = case in ("bf16_out_carry_ws4", "unaligned_bf16")
+    ws = {"f32_l2_ws3": 3, "bf16_out_carry_ws4": 4}.get(case, 1)
+    carry = case == "bf16_out_carry_ws4"
+    kw = dict(weight_decay=1e-2 if case in ("f32_l2_ws3", "adamw_f32") else 0.0,
+              decoupled=case == "adamw_f32")
+    off = 1 if case == "unaligned_bf16" else 0
+    p0 = (rng.standard_normal(n) * 0.02).astype(np.float32)
+    P = torch.zeros(n + off, device=gpu)[off:]
+    P.copy_(torch.from_numpy(p0))
+    M, V = torch.zeros(n + off, device=gpu)[off:], torch.zeros(n + off, device=gpu)[off:]
+    C = torch.zeros(n, device=gpu) if carry else None
+    PB = torch.zeros(n + off, dtype=torch.bfloat16, device=gpu)[off:] if bf16 else None
+    G = torch.zeros(n + off, dtype=torch.bfloat16 if bf16 else torch.float32, device=gpu)[off:]
+    rp, rm, rv = p0.copy(), np.zeros(n, np.float32), np.zeros(n, np.float32)
+    rb, rc = np.zeros(n, np.uint16), (np.zeros(n, np.float32) if carry else None)
+    for t in range(1, 4):
+        gt = torch.from_numpy((rng.standard_normal(n) * 1e-2).astype(np.float32))
+        gt = gt.to(torch.bfloat16) if bf16 else gt
+        G.copy_(gt)
+        adam_step(P, G, M, V, step=t, grad_div=float(ws), p_bf16=PB, carry=C,
+                  carry_mul=float(ws - 1) if carry else 0.0, **kw)
+        hp = c_oracle.hparams(step=t, grad_div=float(ws), carry_mul=float(ws - 1) if carry else 0.0,
+                              **kw)
+        if bf16:
+            c_oracle.adam_bf16(rp, rb, gt.view(torch.int16).numpy().view(np.uint16).copy(), rm, rv,
+                               hp, carry=rc)
+        else:
+            c_oracle.adam_f32(rp, gt.numpy().copy(), rm, rv, hp)
+    torch.cuda.synchronize()
+    assert np.array_equal(P.cpu().numpy().view(np.uint32), rp.view(np.uint32))
+    assert np.array_equal(M.cpu().numpy().view(np.uint32), rm.view(np.uint32))
+    assert np.array_equal(V.cpu().numpy().view(np.uint32), rv.view(np.uint32))
+    if bf16:
+        assert np.array_equal(PB.cpu().view(torch.int16).numpy().view(np.uint16), rb)
+    if carry:
+        assert np.array_equal(C.cpu().numpy().view(np.uint32), rc.view(np.uint32))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_pack_unpack_through_plan_bit_exact(gpu, dtype):
+    """zs_pack / zs_unpack against the plan's own segment table, bit-exact, at
+    ws=3 with even and ragged buckets: a missing grad packs as zeros, re-pointed grads rebuild the
+    cached tables, and unpacking every bucket returns every grad element to its parameter."""
+    from zero_amd import _lib
+    from zero_amd.plan import Plan
+
+    zdt = _lib.ZS_F32 if dtype == torch.float32 else _lib.ZS_BF16
+    es = 4 if dtype == torch.float32 else 2
+    shapes = [(257, 129), (3000,), (64, 64), (5,), (1000, 33), (1,), (4096, 7)]
+    numels = [int(np.prod(s)) for s in shapes]
+    plan = Plan(numels, 3, 1, "reference", window_elems=6000)
+    assert 0 < plan.num_even < plan.num_buckets
+    st = torch.cuda.current_stream().cuda_stream
+    rounds = [[torch.randn(n, device=gpu).to(dtype) for n in numels] for _ in range(2)]
+    rounds[1][3] = None  # a param without a grad: its slots pack as zeros
+    for grads in rounds:
+        ptrs = [0 if g is None else g.data_ptr() for g in grads]
+        host = [None if g is None else g.view(torch.int16 if es == 2 else torch.int32).cpu().numpy()
+                for g in grads]
+        outs = [torch.zeros(n, dtype=dtype, device=gpu) for n in numels]
+        for k in range(plan.num_buckets):
+            b, s = plan.bucket(k), plan.segments(k)
+            assert plan.bucket_bytes(k, zdt) == b.elems * es
+            buf = torch.full((b.elems,), 7, dtype=dtype, device=gpu)
+            plan.pack(k, ptrs, buf.data_ptr(), zdt, st)
+            want = buf.view(torch.int16 if es == 2 else torch.int32).cpu().numpy().copy()
+            for i, po, bo, ln in zip(s.param, s.param_off, s.buf_off, s.length):
+                want[bo:bo + ln] = 0 if host[i] is None else host[i][po:po + ln]
+            got = buf.view(torch.int16 if es == 2 else torch.int32).cpu().numpy()
+            assert np.array_equal(got, want), k
+            plan.unpack(k, buf.data_ptr(), [o.data_ptr() for o in outs], zdt, st)
+        torch.cuda.synchronize()
+        for g, o in zip(grads, outs):
+            assert torch.equal(o, torch.zeros_like(o) if g is None else g)
