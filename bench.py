@@ -27,6 +27,13 @@ sys.path.insert(0, str(REPO))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured copy)
 XGMI_LINK_GBS = 153.0  # one xGMI link, per direction (task brief: 7 links x ~153 GB/s per GPU)
 XGMI_LINKS = 7
+
+
+def peer_link_peak_gbs(world: int) -> float:
+    """Per-rank xGMI bound for a collective over `world` ranks of one fully connected 8-GPU node:
+    each rank has one direct link to every peer, so min(world-1, 7) links can carry its traffic
+    (one link at N=2, all seven at N=8)."""
+    return XGMI_LINK_GBS * max(1, min(world - 1, XGMI_LINKS))
 METRIC = "ZeRO step time & params/sec at 1/2/4/8 GPU; Adam HBM GB/s vs peak"
 
 
@@ -95,7 +102,9 @@ def collective_summary(events, steps, world, red_dev):
     t = torch.tensor([acc.get(k, (0.0, 0.0, 0))[0] for k in keys], dtype=torch.float64, device=red_dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     out = {"source": "HIP events around each collective on the comm stream, max over ranks",
-           "link_peak_gbs": XGMI_LINK_GBS, "aggregate_peak_gbs": XGMI_LINK_GBS * XGMI_LINKS}
+           "link_peak_gbs": XGMI_LINK_GBS, "aggregate_peak_gbs": XGMI_LINK_GBS * XGMI_LINKS,
+           "peer_links": max(1, min(world - 1, XGMI_LINKS)),
+           "peer_links_peak_gbs": peer_link_peak_gbs(world)}
     tot_ms = tot_bus = 0.0
     for k, ms in zip(keys, t.tolist()):
         if k not in acc:
@@ -108,6 +117,7 @@ def collective_summary(events, steps, world, red_dev):
     out["ms_per_step"] = tot_ms / steps
     out["busbw_gbs"] = _busbw(tot_bus, tot_ms)
     out["frac_of_aggregate"] = out["busbw_gbs"] / (XGMI_LINK_GBS * XGMI_LINKS)
+    out["frac_of_peer_links"] = out["busbw_gbs"] / peer_link_peak_gbs(world)
     return out
 
 
@@ -278,7 +288,9 @@ def comm_sweep(comm, arena, world, red_dev, sizes_mb=(4, 16, 64, 256), iters=5):
         bus = n * es * (world - 1) / world
         rs_ms, ag_ms = t.tolist()
         rows.append({"bucket_mb": mb, "rs_ms": rs_ms, "rs_busbw_gbs": _busbw(bus, rs_ms),
-                     "ag_ms": ag_ms, "ag_busbw_gbs": _busbw(bus, ag_ms)})
+                     "ag_ms": ag_ms, "ag_busbw_gbs": _busbw(bus, ag_ms),
+                     "rs_frac_of_peer_links": _busbw(bus, rs_ms) / peer_link_peak_gbs(world),
+                     "ag_frac_of_peer_links": _busbw(bus, ag_ms) / peer_link_peak_gbs(world)})
     torch.cuda.synchronize()
     arena.zero_()  # the sweep scribbled over the arena; padding must stay zero
     return rows
@@ -681,14 +693,15 @@ def main():
     # the 7-link xGMI aggregate, no overlap credit; the slowest rank's sum vs the measured step
     hbm_b = (adam_bytes + sum(b for *_, b in (copy_events or []))) / args.steps
     bus_b = sum(ev[-1] for ev in (comm_events or [])) / args.steps
-    ideal = torch.tensor([hbm_b / (HBM_PEAK_GBS * 1e9) * 1e3 + bus_b / (XGMI_LINK_GBS * XGMI_LINKS * 1e9) * 1e3,
+    ideal = torch.tensor([hbm_b / (HBM_PEAK_GBS * 1e9) * 1e3 + bus_b / (peer_link_peak_gbs(world) * 1e9) * 1e3,
                           hbm_b, bus_b], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(ideal, op=dist.ReduceOp.MAX)
     step_roofline = {"ideal_ms": float(ideal[0]), "frac": float(ideal[0]) / ms,
                      "hbm_gb_per_step": float(ideal[1]) / 1e9, "bus_gb_per_step": float(ideal[2]) / 1e9,
                      "model": "per rank: (Adam + pack + unpack algorithmic bytes) / 8 TB/s + bus bytes "
-                              "/ (7 x 153 GB/s), no overlap credit; max over ranks"}
+                              "/ (min(N-1, 7) x 153 GB/s: the direct links to its peers), no overlap "
+                              "credit; max over ranks"}
     collectives = None
     if world > 1:
         collectives = collective_summary(comm_events, args.steps, world, red_dev)

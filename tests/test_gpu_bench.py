@@ -43,6 +43,9 @@ def test_bench_harness_two_ranks_gloo_staged(gpu):
                 "--comm", "gloo-staged", "--bucket-mb", "64"], timeout=600)
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["value"] > 0
     assert out["config"]["buckets"] > 1 and out["roofline"]["launches_per_step"] >= 1
+    coll = out["collectives"]
+    assert coll["peer_links"] == 1 and coll["peer_links_peak_gbs"] == 153.0  # N=2: one direct link
+    assert coll["frac_of_peer_links"] == pytest.approx(coll["busbw_gbs"] / 153.0)
 
 
 def test_bench_simulated_ws8_bucket_path(gpu):

@@ -136,3 +136,12 @@ def _kat_worker(rank, port, inputs, want_ar, want_ag):
     assert t.tolist() == want_ar.tolist()
     assert ag.view(2, 3).tolist() == want_ag.tolist()
     dist.destroy_process_group()
+
+
+def test_bench_xgmi_peak_counts_direct_peer_links():
+    """bench.py's xGMI denominators: one direct link per peer in the 8-GPU mesh (N=2 → 1 link,
+    N=8 → all 7), never more than 7."""
+    import bench
+
+    assert [bench.peer_link_peak_gbs(n) for n in (1, 2, 4, 8, 16)] == \
+        [153.0, 153.0, 3 * 153.0, 7 * 153.0, 7 * 153.0]
