@@ -47,9 +47,13 @@ def test_hparams_match_torch_scalars():
     import numpy as np
     from zero_amd.kernels import adam_hparams
 
-    for step in (1, 2, 10, 1000):
-        lr, b1, b2, eps = 1e-3, 0.9, 0.999, 1e-8
+    for step, (b1, b2) in [(s, (0.9, 0.999)) for s in (1, 2, 10, 1000, 10**5, 10**7)] + \
+            [(s, (0.8, 0.95)) for s in (1, 3, 77, 5000)]:
+        lr, eps = 1e-3, 1e-8
         hp = adam_hparams(lr, b1, b2, eps, 0.0, step, grad_div=4.0, carry_mul=3.0)
+        # torch keeps `step` in a float32 tensor (adam.py:160-185) and reads it back as a Python
+        # float; exact for every step below 2**24, which the int64 step here matches
+        assert float(np.float32(step)) == step
         assert hp.neg_step_size == np.float32(-(lr / (1 - b1 ** step)))
         assert hp.bc2_sqrt == np.float32((1 - b2 ** step) ** 0.5)
         assert hp.one_minus_beta1 == np.float32(1 - b1)
