@@ -149,3 +149,24 @@ def test_contract_entry_points_validate_without_gpu():
     assert b"non-NULL" in lib.zs_last_error()
     assert lib.zs_adam_step(*args(0, _lib.ZS_F32, 0)) == _lib.ZS_ERR_INVALID  # step must be >= 1
     assert lib.zs_adam_step(*args(0, _lib.ZS_BF16, 1)) == _lib.ZS_OK  # empty: nothing to launch
+
+
+def test_plain_c_client(tmp_path):
+    """A C99 program built with gcc against include/zero_amd.h links libzero_amd.so and drives the
+    host-side entry points (ownership, buckets, segments, error codes) — the C ABI needs no Python
+    or torch in the caller."""
+    import shutil
+    import subprocess
+
+    from zero_amd import _lib
+
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    exe = tmp_path / "abi_host"
+    libdir = _lib.LIB_PATH.parent
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", str(REPO / "include"),
+                    str(REPO / "tests" / "c" / "abi_host.c"), "-L", str(libdir), "-lzero_amd",
+                    f"-Wl,-rpath,{libdir}", "-Wl,-rpath,/opt/rocm/lib", "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.startswith("c-abi ok")
