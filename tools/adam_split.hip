@@ -147,6 +147,58 @@ __global__ __launch_bounds__(256) void adam_split(const unsigned short* __restri
   }
 }
 
+// 8 consecutive elements per lane and group: the three 2-byte streams move 16 B per lane (1 KiB
+// per wave instruction, like the fp32 streams' float4), the fp32 streams two float4 per lane.
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u4 ld16(const unsigned short* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const u4*>(p));
+}
+__device__ __forceinline__ void st16(unsigned short* p, u4 x) {
+  __builtin_nontemporal_store(x, reinterpret_cast<u4*>(p));
+}
+template <int G>
+__global__ __launch_bounds__(256) void adam_split8(const unsigned short* __restrict__ g,
+                                                   unsigned short* __restrict__ hi,
+                                                   unsigned short* __restrict__ lo,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   long n, HP hp) {
+  const long chunk = 256L * 8 * G;
+  const long nchunks = n / chunk;
+  for (long c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    u4 gg[G], hh[G], ll[G];
+    f4 m0[G], m1[G], v0[G], v1[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const long i = c * chunk + (long(u) * 256 + threadIdx.x) * 8;
+      gg[u] = ld16(g + i);
+      hh[u] = ld16(hi + i);
+      ll[u] = ld16(lo + i);
+      m0[u] = ld4(m + i);
+      m1[u] = ld4(m + i + 4);
+      v0[u] = ld4(v + i);
+      v1[u] = ld4(v + i + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const long i = c * chunk + (long(u) * 256 + threadIdx.x) * 8;
+      f4 g0 = unbf(u2{gg[u].x, gg[u].y}), g1 = unbf(u2{gg[u].z, gg[u].w});
+      f4 p0 = join(u2{hh[u].x, hh[u].y}, u2{ll[u].x, ll[u].y});
+      f4 p1 = join(u2{hh[u].z, hh[u].w}, u2{ll[u].z, ll[u].w});
+      elem4(g0, p0, m0[u], v0[u], hp);
+      elem4(g1, p1, m1[u], v1[u], hp);
+      u2 h0, l0, h1, l1;
+      split(p0, h0, l0);
+      split(p1, h1, l1);
+      st16(hi + i, u4{h0.x, h0.y, h1.x, h1.y});
+      st16(lo + i, u4{l0.x, l0.y, l1.x, l1.y});
+      st4(m + i, m0[u]);
+      st4(m + i + 4, m1[u]);
+      st4(v + i, v0[u]);
+      st4(v + i + 4, v1[u]);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void copy_nt(const float* __restrict__ a, float* __restrict__ b,
                                                long n) {
   for (long i = (long(blockIdx.x) * 256 + threadIdx.x) * 4; i < n; i += long(gridDim.x) * 256 * 4)
@@ -207,6 +259,15 @@ int main(int argc, char** argv) {
       ms = time_ms([&] { adam_split<4><<<grid, 256>>>(g, po, lo, m, v, n, hp); }, 5);
       printf("alloc %d round %d adam split G=4    26 B %8.3f ms %7.1f GB/s %.4g elem/s\n", a, r, ms,
              26.0 * n / ms / 1e6, n / ms * 1e3);
+      ms = time_ms([&] { adam_split8<1><<<grid, 256>>>(g, po, lo, m, v, n, hp); }, 5);
+      printf("alloc %d round %d adam split8 G=1   26 B %8.3f ms %7.1f GB/s %.4g elem/s\n", a, r, ms,
+             26.0 * n / ms / 1e6, n / ms * 1e3);
+      ms = time_ms([&] { adam_split8<2><<<grid, 256>>>(g, po, lo, m, v, n, hp); }, 5);
+      printf("alloc %d round %d adam split8 G=2   26 B %8.3f ms %7.1f GB/s %.4g elem/s\n", a, r, ms,
+             26.0 * n / ms / 1e6, n / ms * 1e3);
+      ms = time_ms([&] { copy_nt<<<grid, 256>>>(m, v, n); }, 5);
+      printf("alloc %d round %d copy_nt           8 B %8.3f ms %7.1f GB/s\n", a, r, ms,
+             8.0 * n / ms / 1e6);
     }
     // keep s allocated so the next iteration gets new memory
   }
