@@ -352,21 +352,226 @@ class _NoComm:
         pass
 
 
+def _zero3_comm_summary(opt, steps, world, red_dev):
+    """Per-step time and bus bandwidth of the ZeRO-3 collectives (gathers and gradient
+    reduce-scatters, HIP events on the side stream), slowest rank."""
+    import torch
+    import torch.distributed as dist
+
+    ge = opt.runtime.gather_events or []
+    re = opt._reducer.timing or [] if opt._reducer is not None else []
+    vals = [sum(a.elapsed_time(b) for a, b, _ in ge), sum(a.elapsed_time(b) for a, b, _ in re)]
+    t = torch.tensor(vals, dtype=torch.float64, device=red_dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    out = {"source": "HIP events around each gather group / reduce-scatter bucket on the side "
+                     "stream, max over ranks", "peer_links_peak_gbs": peer_link_peak_gbs(world)}
+    for key, ev, ms in (("all_gather", ge, float(t[0])), ("reduce_scatter", re, float(t[1]))):
+        bus = sum(b for *_, b in ev)
+        out[key] = {"calls_per_step": len(ev) / steps, "ms_per_step": ms / steps,
+                    "bus_gb_per_step": bus / steps / 1e9, "busbw_gbs": _busbw(bus, ms),
+                    "frac_of_peer_links": _busbw(bus, ms) / peer_link_peak_gbs(world)}
+    return out
+
+
+def _zero3_report(args, opt, world, rank, red_dev, el, total, workload, extra):
+    """Time / Adam-roofline bookkeeping shared by the two ZeRO-3 benches; rank 0 prints."""
+    import torch
+    import torch.distributed as dist
+
+    ev, opt.timing_events = opt.timing_events, None
+    adam_ms = sum(a.elapsed_time(b) for a, b, _ in ev)
+    adam_bytes = sum(nb for _, _, nb in ev)
+    achieved = adam_bytes / (adam_ms / 1e3) / 1e9 if adam_ms > 0 else 0.0
+    t = torch.tensor([el, -achieved], dtype=torch.float64, device=red_dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)  # slowest rank's time and Adam bandwidth
+    el, achieved = float(t[0]), -float(t[1])
+    ms = el / args.steps * 1e3
+    comm = _zero3_comm_summary(opt, args.steps, world, red_dev) if world > 1 else None
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": total / (ms / 1e3), "unit": "params/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": ("bf16 params/grads, fp32 Adam (split master)" if args.dtype == "bf16"
+                      else "fp32"),
+            "data": "synthetic",
+            "config": dict(workload=workload, params=int(total), param_dtype=args.dtype, zero=3,
+                           update="real ZeRO-3 (update=True)", bucket_mb=args.bucket_mb,
+                           gather_dtype=args.gather or args.dtype, parallelism=f"dp{world}"),
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "adam_segments_kernel",
+                         "avg_launch_ms": adam_ms / max(len(ev), 1),
+                         "alg_bytes_per_launch": adam_bytes / max(len(ev), 1),
+                         "launches_per_step": len(ev) / args.steps},
+            "zero3": {"gathers_per_step": opt.runtime.n_gathers / (args.steps + args.warmup),
+                      "prefetch_hits": opt.runtime.n_prefetch_hits,
+                      "reduce_buckets_per_step": opt._reducer.K,
+                      "reduced_in_backward": opt._reducer.launched_in_backward},
+        }
+        if comm is not None:
+            out["collectives"] = comm
+        out.update(extra)
+        print(json.dumps(out), flush=True)
+
+
+def _zero3_timed(args, opt, step, dev, world):
+    import torch
+    import torch.distributed as dist
+
+    for _ in range(args.warmup):
+        step()
+    opt.timing_events = []
+    if world > 1:
+        opt.runtime.gather_events = []
+        opt._reducer.timing = []
+    torch.cuda.synchronize()  # warmup drained first: no collective of ours beside c10d's barrier
+    dist.barrier()
+    torch.cuda.synchronize()
+    _phase("timed steps")
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    return time.perf_counter() - t0
+
+
+def _zero3_comm(args, world, rank, dev):
+    """The communicator for the ZeRO-3 benches (self-checked at N>1 like the ZeRO-1/2 one)."""
+    kw = {}
+    if world > 1 and args.comm == "gloo-staged":
+        sys.path.insert(0, str(REPO / "tests"))
+        from _gloo_comm import GlooStagedComm
+
+        return GlooStagedComm(), None
+    if world > 1:
+        from zero_amd.comm import C10dComm, RcclComm
+
+        kw["comm"] = C10dComm() if args.comm == "c10d" else RcclComm()
+        _phase("communicator self-check")
+        chk = _checked_comm(kw, world, rank, dev)
+        return kw["comm"], chk
+    return None, None
+
+
+def _fail_check(what: str, rank: int, detail) -> None:
+    log(f"[bench] EXCHANGE CHECK FAILED on rank {rank}: {what}: {detail}")
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(4)
+
+
+def _bf16_sum_tolerance(world: int) -> float:
+    """Bound on |RCCL bf16 sum - exact sum| relative to sum_r |g_r|: each of the (world-1) hops
+    of a ring adds in fp32 and rounds the partial sum to bf16 (<= 2^-9 of its magnitude, which
+    is <= sum_r |g_r|), plus the final rounding; doubled for margin."""
+    return world * 2.0 ** -8
+
+
+def _regen_grads(shapes, world, dev, keep):
+    """The bench's synthetic gradients of every rank (seed = rank, N(0,1)*1e-3, one generator
+    pass over the set, as generated in main / bench_zero3_paramset), reduced on the fly to the
+    exact fp32 sum and sum of |g| of the tensors in ``keep`` (index -> flat element slice)."""
+    import torch
+
+    gen = torch.Generator(device=dev)
+    exact = {i: None for i in keep}
+    absum = {i: None for i in keep}
+    for r in range(world):
+        gen.manual_seed(1000 * 0 + r)
+        for i, s in enumerate(shapes):
+            t = (torch.empty(s, dtype=torch.float32, device=dev).normal_(generator=gen) * 1e-3)
+            if i not in keep:
+                continue
+            v = t.to(torch.bfloat16).float().reshape(-1)[keep[i]]
+            exact[i] = v.clone() if exact[i] is None else exact[i] + v
+            absum[i] = v.abs() if absum[i] is None else absum[i] + v.abs()
+    return exact, absum
+
+
+def zero3_gather_check(opt, model, shapes, full_copies, dev, world, rank, red_dev):
+    """Before timing at N>1 (BASELINE configs[4]): (1) one side-stream all-gather of a decoder
+    layer through the real communicator must reproduce every full tensor bit for bit; (2) one
+    hooked forward/backward: the gradient chunks the backward reduce-scatters left in p.grad must
+    equal the exact fp32 sum of every rank's known synthetic gradient within the bf16 ring bound.
+    AND-ed over ranks; a failure ends the run (exit 4) naming the rank and tensor."""
+    import torch
+    import torch.distributed as dist
+
+    rt = opt.runtime
+    layer = model.layers[1]
+    idx = model.groups[1]
+    ms = [opt.param_managers[getattr(layer, f"p{k}")] for k in range(layer.n)]
+    rt.launch(("exchange-check",), ms)
+    out, ev = rt.pending.pop(("exchange-check",))
+    torch.cuda.current_stream(dev).wait_event(ev)
+    torch.cuda.synchronize()
+    bits = lambda t: t.reshape(-1).view(torch.int16 if t.element_size() == 2 else torch.int32)  # noqa: E731
+    bad = [i for (m, full), i in zip(out, idx) if not torch.equal(bits(full[:m.numel]),
+                                                                   bits(full_copies[i]))]
+    for m, _ in out:
+        m.release()
+    gather_ok = not bad
+    # (2) reduce-scatter of one backward
+    ar = opt._arena
+    keep = {}
+    for i in idx:
+        r0, r1, row = ar.rows[i]
+        keep[i] = slice(r0 * row, r1 * row)
+    exact, absum = _regen_grads(shapes, world, dev, keep)
+    x = torch.zeros(1, device=dev, requires_grad=True)
+    opt.zero_grad()
+    model(x).sum().backward()
+    torch.cuda.synchronize()
+    tol = _bf16_sum_tolerance(world)
+    worst = 0.0
+    rs_bad = []
+    params = list(model.parameters())
+    for i in idx:
+        g = params[i].grad
+        if g is None:
+            rs_bad.append((i, "no grad chunk"))
+            continue
+        err = (g.float().reshape(-1) - exact[i]).abs()
+        bound = tol * absum[i] + 1e-30
+        ratio = float((err / bound).max()) if err.numel() else 0.0
+        worst = max(worst, ratio)
+        if ratio > 1.0:
+            rs_bad.append((i, ratio))
+    opt.step()  # completes the iteration (a warm-up step)
+    torch.cuda.synchronize()
+    ok = torch.tensor([1.0 if (gather_ok and not rs_bad) else 0.0], device=red_dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    res = {"gather_bit_exact": gather_ok, "gather_tensors": len(idx),
+           "reduce_scatter_max_err_over_bound": worst,
+           "reduce_scatter_bound": f"|sum - exact fp32 sum| <= {world} * 2^-8 * sum_r |g_r| "
+                                   "(bf16 ring: one rounding per hop)",
+           "all_ranks_ok": bool(ok.item() == 1.0)}
+    if not gather_ok:
+        _fail_check("ZeRO-3 all-gather of layer 1", rank, f"tensors {bad} differ from the full params")
+    if rs_bad:
+        _fail_check("ZeRO-3 backward reduce-scatter of layer 1", rank, rs_bad)
+    if not res["all_ranks_ok"]:
+        _fail_check("ZeRO-3 exchange", rank, "another rank failed")
+    return res
+
+
 def bench_zero3(args, world, rank, dev, use_nccl):
     """ZeRO-3 (BASELINE.json configs[2]): one step = one training iteration of the reference
     harness loop (zero3.py:171-258: zero_grad → forward → MSE → backward → step) on the
     6×Linear(D,D)+ReLU MLP, with every parameter dim-0 sharded, the hooks' all-gathers grouped per
-    module and prefetched on a side stream, and update-mode step() = grouped reduce-scatter of the
-    full grads + fused Adam on the local chunks.  value = params / iteration time."""
-    import numpy as np
+    module and prefetched on a side stream, the gradients reduce-scattered from backward hooks
+    into the grad chunk arena, and update-mode step() = fused Adam on the local chunks.
+    value = params / iteration time."""
     import torch
     import torch.distributed as dist
 
     from zero_amd import zero3
     from zero_amd.shapes import CONFIGS
 
-    if args.config not in ("C2", "C3"):
-        raise SystemExit("--zero 3 runs the MLP configs C2 / C3")
     D = CONFIGS[args.config][1]()[0][0]
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     torch.manual_seed(0)
@@ -379,8 +584,10 @@ def bench_zero3(args, world, rank, dev, use_nccl):
     batch = args.batch or 16
     x = torch.randn(batch, D, device=dev, generator=g).to(dt)
     y = torch.randn(batch, D, device=dev, generator=g).to(dt)
+    comm, chk = _zero3_comm(args, world, rank, dev)
+    kw = {} if comm is None else {"comm": comm}
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
-                                 sync=False, gather_dtype=args.gather)
+                                 sync=False, gather_dtype=args.gather, bucket_mb=args.bucket_mb, **kw)
     zero3.register_zero3_hooks(model, opt.param_managers)
 
     def step():
@@ -389,49 +596,103 @@ def bench_zero3(args, world, rank, dev, use_nccl):
         loss.backward()
         opt.step()
 
-    for _ in range(args.warmup):
-        step()
-    opt.timing_events = []
-    torch.cuda.synchronize()  # warmup drained first: no collective of ours beside c10d's barrier
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    el = time.perf_counter() - t0
-    ev, opt.timing_events = opt.timing_events, None
+    _phase("warmup")
+    el = _zero3_timed(args, opt, step, dev, world)
     red_dev = dev if use_nccl else "cpu"
-    adam_ms = sum(a.elapsed_time(b) for a, b, _ in ev)
-    adam_bytes = sum(nb for _, _, nb in ev)
-    achieved = adam_bytes / (adam_ms / 1e3) / 1e9 if adam_ms > 0 else 0.0
-    t = torch.tensor([el, -achieved], dtype=torch.float64, device=red_dev)
+    extra = {"rccl_selfcheck": chk} if chk is not None else {}
+    _zero3_report(args, opt, world, rank, red_dev, el, total,
+                  f"{args.config} ZeRO-3 training iteration of the reference MLP 6xLinear({D},{D})+ReLU "
+                  f"(hooked all-gathers, backward reduce-scatters, update-mode step), batch {batch}",
+                  extra)
+    _teardown(opt)
+    dist.destroy_process_group()
+
+
+def bench_zero3_paramset(args, world, rank, dev, use_nccl):
+    """ZeRO-3 on a synthetic parameter set (BASELINE.json configs[4]: C5 8.03e9 params; C4 also):
+    one step = one hooked iteration of zero_amd.paramset.ParamSetModel — per decoder layer an
+    all-gather in the forward pre-hook and again in the backward pre-hook, the synthetic full
+    gradients (resident in HBM, N(0,1)·1e-3 per rank) reduce-scattered from the backward hooks into
+    the grad chunk arena, then zero3.ShardedOptimizer(update=True).step() = fused Adam on the
+    chunks.  value = params / iteration time (strong scaling)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from zero_amd import zero3
+    from zero_amd.paramset import ParamSetModel, decoder_layer_groups
+    from zero_amd.shapes import CONFIGS
+
+    name, shape_fn = CONFIGS[args.config]
+    shapes = shape_fn()
+    if args.set_layers is not None:  # test-size copy of the set: fewer decoder layers
+        from zero_amd import shapes as shp
+
+        shapes = shp.decoder_shapes(args.config, args.set_layers)
+        name += f" ({args.set_layers} layers)"
+    total = int(sum(int(np.prod(s)) for s in shapes))
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(0)
+    params = [torch.nn.Parameter(torch.empty(s, dtype=torch.float32, device=dev).normal_(
+        0.0, 0.02, generator=gen).to(dt)) for s in shapes]
+    gen.manual_seed(1000 * 0 + rank)
+    grads = [(torch.empty(s, dtype=torch.float32, device=dev).normal_(generator=gen) * 1e-3).to(dt)
+             for s in shapes]
+    model = ParamSetModel(params, decoder_layer_groups(len(shapes)))
+    model.set_grad_source(grads)
+    full_copies = ({i: params[i].detach().clone() for i in model.groups[1]} if world > 1 else None)
+    comm, chk = _zero3_comm(args, world, rank, dev)
+    if args.simulate_ws > 1:  # DIAGNOSTIC: rank 0 of a simulate_ws-rank job, collectives skipped
+        assert world == 1, "--simulate-ws is a single-GPU diagnostic"
+        comm = _NoComm(args.simulate_ws)
+        sim_ws, real_get = args.simulate_ws, zero3.get
+        zero3.get = lambda what, dm=None: {"ws": sim_ws, "rank": 0}.get(what) \
+            if what in ("ws", "rank") else real_get(what, dm)
+    kw = {} if comm is None else {"comm": comm}
+    opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
+                                 sync=False, gather_dtype=args.gather, bucket_mb=args.bucket_mb, **kw)
+    zero3.register_zero3_hooks(model, opt.param_managers)
+    gather_check = None
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)  # slowest rank's time and Adam bandwidth
-    el, achieved = float(t[0]), -float(t[1])
-    ms = el / args.steps * 1e3
-    if rank == 0:
-        out = {
-            "metric": METRIC, "value": total / (ms / 1e3), "unit": "params/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
-            "data": "synthetic",
-            "config": {"workload": f"{args.config} ZeRO-3 training iteration of the reference MLP "
-                                   f"6xLinear({D},{D})+ReLU (hooked all-gathers, update-mode step)",
-                       "params": int(total), "batch": batch, "param_dtype": args.dtype,
-                       "zero": 3, "gather_dtype": args.gather or args.dtype,
-                       "parallelism": f"dp{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "adam_segments_kernel",
-                         "avg_launch_ms": adam_ms / max(len(ev), 1),
-                         "alg_bytes_per_launch": adam_bytes / max(len(ev), 1),
-                         "launches_per_step": len(ev) / args.steps},
-            "zero3": {"gathers_per_step": opt.runtime.n_gathers / (args.steps + args.warmup),
-                      "prefetch_hits": opt.runtime.n_prefetch_hits},
-        }
-        print(json.dumps(out), flush=True)
+        _phase("ZeRO-3 gather check")
+        gather_check = zero3_gather_check(opt, model, shapes, full_copies, dev, world, rank,
+                                          red_dev=dev if use_nccl else "cpu")
+        del full_copies
+    x = torch.zeros(1, device=dev, requires_grad=True)
+
+    def step():
+        opt.zero_grad()
+        model(x).sum().backward()
+        opt.step()
+
+    _phase("warmup")
+    el = _zero3_timed(args, opt, step, dev, world)
+    if args.simulate_ws > 1:
+        ev, opt.timing_events = opt.timing_events, None
+        adam_ms = sum(a.elapsed_time(b) for a, b, _ in ev)
+        adam_b = sum(nb for *_, nb in ev)
+        if rank == 0:
+            print(json.dumps({"diagnostic": f"simulate-ws {args.simulate_ws}: rank-0 compute of the "
+                              "hooked ZeRO-3 iteration, collectives skipped (NOT the metric)",
+                              "ms_per_step": el / args.steps * 1e3,
+                              "adam_ms_per_step": adam_ms / args.steps,
+                              "adam_achieved_gbs": adam_b / (adam_ms / 1e3) / 1e9 if adam_ms else 0.0,
+                              "chunk_elems": int(opt._arena.ln.sum()), "layers": len(model.layers),
+                              "reduce_buckets": opt._reducer.K}), flush=True)
+        _teardown(opt)
+        dist.destroy_process_group()
+        return
+    extra = {}
+    if chk is not None:
+        extra["rccl_selfcheck"] = chk
+    if gather_check is not None:
+        extra["exchange_check"] = gather_check
+    _zero3_report(args, opt, world, rank, dev if use_nccl else "cpu", el, total,
+                  f"{args.config} {name} synthetic parameter set, ZeRO-3 through the hooks: "
+                  f"{len(model.layers)} layer modules, per-layer all-gather in forward and backward, "
+                  f"backward reduce-scatter of synthetic full grads, fused Adam on the chunks",
+                  extra)
     _teardown(opt)
     dist.destroy_process_group()
 
@@ -516,6 +777,9 @@ def main():
     ap.add_argument("--seq", type=int, default=8192, help="--train sequence length "
                     "(fsdp/train_fsdp.py:44: 8192)")
     ap.add_argument("--train-layers", type=int, default=None, help="--train: fewer decoder layers")
+    ap.add_argument("--set-layers", type=int, default=None,
+                    help="--zero 3 on C4/C5: a copy of the parameter set with fewer decoder layers "
+                         "(tests)")
     ap.add_argument("--layout", default="reference", choices=["reference", "flat", "chunk"],
                     help="optimizer-shard layout: reference = whole params by index (zero1.py:55-62, "
                          "ZeRO-1/2); chunk = dim-0 chunks of every param (zero3.py:107-108, forced "
@@ -575,8 +839,8 @@ def main():
         return bench_train_smollm3(args, world, rank, dev, use_nccl)
     if args.zero == 3 and args.config in ("C2", "C3"):
         return bench_zero3(args, world, rank, dev, use_nccl)
-    if args.zero == 3:  # parameter-set ZeRO-3 (BASELINE.json configs[4]): Layout Z buckets
-        args.layout = "chunk"
+    if args.zero == 3:  # parameter-set ZeRO-3 (BASELINE.json configs[4]) through the hooks
+        return bench_zero3_paramset(args, world, rank, dev, use_nccl)
     name, shape_fn = CONFIGS[args.config]
     shapes = shape_fn()
     total = int(sum(int(np.prod(s)) for s in shapes))
@@ -592,7 +856,7 @@ def main():
     for s in shapes:
         grads.append((torch.empty(s, dtype=torch.float32, device=dev).normal_(generator=gen) * 1e-3).to(dt))
     torch.cuda.synchronize()
-    mod = zero1 if args.zero == 1 else zero2  # zero=3 here: zero2's engine over Layout Z
+    mod = zero1 if args.zero == 1 else zero2
     kw = {}
     comm_used = None
     if args.comm == "gloo-staged" and world > 1:
@@ -732,15 +996,12 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "fp32",
+            # the arithmetic: bf16 params and grads, Adam in fp32 (master, exp_avg, exp_avg_sq)
+            "dtype": ("bf16 params/grads, fp32 Adam" if args.dtype == "bf16" else "fp32"),
             "data": "synthetic",
             "config": {
                 "workload": (f"{args.config} {name} synthetic parameter set: ZeRO-{args.zero} "
-                             f"ShardedOptimizer(Adam lr=1e-3).step(), grads resident in HBM")
-                if args.zero != 3 else
-                            (f"{args.config} {name} synthetic parameter set: ZeRO-3 step on dim-0 "
-                             f"chunks (zero3.py:107-108): bucketed RS of the full grads, fused Adam "
-                             f"on the chunks, AG of the updated chunks (one gather per iteration)"),
+                             f"ShardedOptimizer(Adam lr=1e-3).step(), grads resident in HBM"),
                 "params": total, "tensors": len(shapes),
                 "param_dtype": args.dtype, "grad_dtype": args.dtype,
                 "state_dtype": ("fp32 exp_avg, exp_avg_sq; fp32 master held as the bf16 param + "

@@ -37,6 +37,15 @@ def llama31_8b_shapes():
     return _decoder(128256, 4096, 14336, 32, 8 * 128, tied=False)
 
 
+def decoder_shapes(config: str, layers: int):
+    """C4 / C5 with ``layers`` decoder layers (test-size copies of the sets)."""
+    if config == "C4":
+        return _decoder(128256, 2048, 11008, layers, 4 * 128, tied=True)
+    if config == "C5":
+        return _decoder(128256, 4096, 14336, layers, 8 * 128, tied=False)
+    raise ValueError(f"{config} is not a decoder parameter set")
+
+
 CONFIGS = {
     "C1": ("reference MLP 6xLinear(10000,10000)", lambda: mlp_shapes(10000)),
     "C2": ("MLP 6xLinear(4096,4096)", lambda: mlp_shapes(4096)),

@@ -1,49 +1,74 @@
-"""Memory accounting helpers (reference: zero/training_utils/memory.py:8-50).
+"""Per-rank memory report for the ZeRO harness (what zero/training_utils/memory.py:37-50 prints).
 
-``get_optimizer_memory`` walks ``optimizer.optimizer.state`` exactly like the reference; the
-drop-in ShardedOptimizer exposes its flat fp32 shard buffers there as per-parameter views, so the
-numbers are comparable.
+One pass over the model and the optimizer state builds a ``MemoryReport``; ``print_memory_stats``
+renders it in the reference's five-line format so the harness output reads the same.  Sizes are
+logical (numel × element size, in MiB) — the quantity the reference reports — and, separately,
+physical: the distinct storages behind those tensors.  The two differ for the drop-ins on purpose:
+``optimizer.optimizer.state[p]`` holds *views* of one flat fp32 shard buffer, and ZeRO-3 parameters
+are views of one flat chunk arena, so the physical column shows what is really resident.
 """
 from __future__ import annotations
 
+from dataclasses import dataclass
+
 import torch
 
-
-def get_size_in_mb(tensor):
-    if tensor is None:
-        return 0
-    return tensor.element_size() * tensor.nelement() / 1024**2
+_MIB = float(1 << 20)
 
 
-def get_optimizer_memory(optimizer):
-    total = 0
-    if hasattr(optimizer, "optimizer"):
-        optimizer = optimizer.optimizer
-    for state in optimizer.state.values():
-        for t in state.values():
-            if torch.is_tensor(t):
-                total += get_size_in_mb(t)
-    return total
+def _walk(tensors):
+    """(logical MiB, physical MiB) of an iterable of tensors / None; storages counted once."""
+    logical, seen, physical = 0, set(), 0
+    for t in tensors:
+        if not torch.is_tensor(t):
+            continue
+        logical += t.numel() * t.element_size()
+        st = t.untyped_storage()
+        key = (st.data_ptr(), t.device)
+        if key not in seen:
+            seen.add(key)
+            physical += st.nbytes()
+    return logical / _MIB, physical / _MIB
 
 
-def get_model_memory(model):
-    return sum(get_size_in_mb(p) for p in model.parameters())
+def _state_tensors(optimizer):
+    inner = getattr(optimizer, "optimizer", optimizer)  # a ShardedOptimizer wraps torch's
+    for per_param in inner.state.values():
+        yield from per_param.values()
 
 
-def get_gradient_memory(model):
-    return sum(get_size_in_mb(p.grad) for p in model.parameters() if p.grad is not None)
+@dataclass(frozen=True)
+class MemoryReport:
+    params_mb: float
+    grads_mb: float
+    optimizer_mb: float
+    params_physical_mb: float
+    grads_physical_mb: float
+    optimizer_physical_mb: float
+    allocated_mb: float
+    max_allocated_mb: float
+
+    def lines(self, prefix: str, rank: int):
+        return [f"\nGPU {rank} - {prefix}:",
+                f"  Model parameters: {self.params_mb:.2f} MB",
+                f"  Gradients: {self.grads_mb:.2f} MB",
+                f"  Optimizer states: {self.optimizer_mb:.2f} MB",
+                f"  Total allocated: {self.allocated_mb:.2f} MB",
+                f"  Max allocated: {self.max_allocated_mb:.2f} MB",
+                "-" * 40]
+
+
+def memory_report(model, optimizer, device) -> MemoryReport:
+    params = list(model.parameters())
+    p_l, p_p = _walk(params)
+    g_l, g_p = _walk(p.grad for p in params)
+    o_l, o_p = _walk(_state_tensors(optimizer))
+    on_gpu = torch.cuda.is_available() and torch.device(device).type == "cuda"
+    alloc = torch.cuda.memory_allocated(device) / _MIB if on_gpu else 0.0
+    peak = torch.cuda.max_memory_allocated(device) / _MIB if on_gpu else 0.0
+    return MemoryReport(p_l, g_l, o_l, p_p, g_p, o_p, alloc, peak)
 
 
 def print_memory_stats(prefix: str, model, optimizer, rank, device):
-    model_memory = get_model_memory(model)
-    grad_memory = get_gradient_memory(model)
-    optim_memory = get_optimizer_memory(optimizer)
-    total_allocated = torch.cuda.memory_allocated(device) / 1024**2
-    max_allocated = torch.cuda.max_memory_allocated(device) / 1024**2
-    print(f"\nGPU {rank} - {prefix}:")
-    print(f"  Model parameters: {model_memory:.2f} MB")
-    print(f"  Gradients: {grad_memory:.2f} MB")
-    print(f"  Optimizer states: {optim_memory:.2f} MB")
-    print(f"  Total allocated: {total_allocated:.2f} MB")
-    print(f"  Max allocated: {max_allocated:.2f} MB")
-    print("-" * 40)
+    """memory.py:37-50's report (same lines), computed by ``memory_report``."""
+    print("\n".join(memory_report(model, optimizer, device).lines(prefix, rank)))

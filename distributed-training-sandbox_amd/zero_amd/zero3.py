@@ -11,18 +11,28 @@ Reference behaviour:
     (zero3.py:131-147) — and then the ``for … else`` at zero3.py:150-153 sets EVERY ``param.grad``
     to None, so the inner Adam never sees a gradient and parameters never change.
 
-This module keeps that API.  Two modes:
+Here every rank's chunks of every parameter live in ONE flat *chunk arena* (slot i holds param
+i's padded chunk of S_i = ceil(d0/ws)·row elements, 64-element aligned, zero beyond the rank's
+real rows), and ``param.data`` is a view of its slot between gathers.  Two modes:
+
   * ``update=False`` (default): reference semantics, bit-for-bit in what is observable — the
     reduced shard grads are computed (one grouped RCCL all-reduce per step, exposed as
     ``last_reduced_grads``) and then discarded; parameters stay at their initial values.
-  * ``update=True``: the ZeRO-3 the reference intends — release() keeps full-size grads, step()
-    reduce-scatters them (one grouped RCCL reduce-scatter) so every rank gets the summed grad of
-    exactly its chunk, and the fused HIP Adam updates the chunk in place (== data-parallel Adam,
-    sliced).  Optimizer state is one flat fp32 buffer over the rank's chunks.
-In both modes ``materialize`` is a zero-copy RCCL all-gather from the shard straight into the full
-tensor (rows of torch.chunk are contiguous: full = [chunk_0 | … | chunk_{ws-1}]), grouped per
-module, launched on a side HIP stream, and the NEXT module's gather is prefetched there while the
-current module computes (the order is learned on the first iteration).
+  * ``update=True``: the ZeRO-3 the reference intends.  A post-accumulate-grad hook on every
+    parameter hands its full-size gradient, as soon as backward has produced it, to a bucketed
+    reduce-scatter (one RCCL group per bucket, buckets in backward order, launched strictly in
+    order so every rank issues the same sequence) that writes the summed chunk straight into a
+    flat *grad chunk arena*; the full gradient is released right after, so gradient memory is one
+    bucket in flight plus 1/ws of the model.  ``step()`` is one fused HIP Adam launch over the
+    chunk arena (grad /ws folded in) — data-parallel Adam, sliced.  Every rank updates its chunk
+    of every parameter, so the inner optimizer's groups are not filtered in this mode and
+    ``optimizer.state[p]`` holds chunk-shaped views of the flat fp32 state.
+
+``materialize`` is a zero-copy RCCL all-gather from the chunk slot (already padded to S) straight
+into the full tensor (rows of torch.chunk are contiguous: full = [chunk_0 | … | chunk_{ws-1}]),
+grouped per module, on a side HIP stream, and the NEXT module's gather is prefetched there while
+the current module computes (the order is learned on the first iteration).  Reduce-scatters run
+on the same side stream, so one communicator sees one totally ordered sequence of collectives.
 """
 from __future__ import annotations
 
@@ -34,24 +44,33 @@ import torch
 from torch.optim import Optimizer
 
 from . import _lib
-from .comm import RcclComm, comm_stream, zs_dtype
-from .kernels import stream_handle
-from .engine import ALIGN_ELEMS, probed_zeros
-from .kernels import AdamSet, adam_hparams
-from .plan import Plan
-from ._sharded import adam_group_hparams
 from ._lib import ZS_BF16, ZS_BF16_SPLIT, ZS_F32
+from ._sharded import adam_group_hparams
+from .comm import RcclComm, comm_stream, zs_dtype
+from .engine import ALIGN_ELEMS, probed_zeros
+from .kernels import AdamSet, adam_hparams, stream_handle
 from .training_utils.utils import get
 
 
 def _chunk_geom(d0: int, ws: int, rank: int):
-    cs = -(-d0 // ws) if d0 else 0  # torch.chunk rows per chunk
+    """torch.chunk(ws, dim=0) rows: chunk size cs = ceil(d0/ws), rank's rows [r0, r1)."""
+    cs = -(-d0 // ws) if d0 else 0
     r0, r1 = min(rank * cs, d0), min((rank + 1) * cs, d0)
     return cs, r0, r1
 
 
+def _round_up(x: int, a: int) -> int:
+    return -(-int(x) // a) * a
+
+
+def _group_ctx(comm):
+    grp = getattr(comm, "group", None)
+    return grp() if grp is not None else contextlib.nullcontext()
+
+
 class _GatherRuntime:
-    """Side-stream all-gathers of module parameter groups with one-ahead prefetch.
+    """Side-stream collectives of one ShardedOptimizer: module all-gathers with one-ahead prefetch
+    (and, in update mode, the gradient reduce-scatters, on the same stream).
 
     The first iteration records the order in which module groups are materialised (forward, then
     backward); afterwards each materialise also launches the gather of the next group in that
@@ -68,10 +87,7 @@ class _GatherRuntime:
         self.key_managers = {}
         self.n_gathers = 0
         self.n_prefetch_hits = 0
-
-    def _group(self):
-        grp = getattr(self.comm, "group", None)
-        return grp() if grp is not None else contextlib.nullcontext()
+        self.gather_events = None  # optional list of (start, end, bus_bytes) per gather group
 
     def launch(self, key, managers):
         """Enqueue the all-gather of ``managers`` on the side stream; returns immediately."""
@@ -79,17 +95,25 @@ class _GatherRuntime:
             return
         ev_ready = torch.cuda.Event()
         ev_ready.record(torch.cuda.current_stream(self.device))  # shards may just have been updated
+        timed = self.gather_events is not None and self.ws > 1
         with torch.cuda.stream(self.stream):
             self.stream.wait_event(ev_ready)
-            # kernels (pad copies, fp8 quantisation) before the RCCL group, dequantisation after:
-            # an RCCL group only launches its collectives at group end
+            if timed:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record(self.stream)
+            # kernels (fp8 quantisation) before the RCCL group, dequantisation after: an RCCL
+            # group only launches its collectives at group end; every buffer a collective of the
+            # group touches is referenced from `states` until the group has ended
             states = [m._gather_prepare(self.stream) for m in managers]
-            with self._group():
+            with _group_ctx(self.comm):
                 for m, st in zip(managers, states):
                     m._gather_issue(self.comm, self.stream, st)
             out = [(m, m._gather_finish(self.stream, st)) for m, st in zip(managers, states)]
             ev = torch.cuda.Event()
             ev.record(self.stream)
+            if timed:  # ring all-gather bus bytes: (ws-1)/ws of the gathered tensor, per rank
+                bus = sum(m.gather_bytes() for m in managers) * (self.ws - 1)
+                self.gather_events.append((e0, _timed_after(self.stream), bus))
         self.pending[key] = (out, ev)
         self.n_gathers += 1
 
@@ -125,11 +149,21 @@ class _GatherRuntime:
         self._prefetch(0)
 
 
+def _timed_after(stream):
+    e = torch.cuda.Event(enable_timing=True)
+    e.record(stream)
+    return e
+
+
 class Zero3ParamManager:
-    """zero3.py:25-52: tracks one parameter's dim-0 shard and gathers / releases the full tensor."""
+    """zero3.py:25-52: tracks one parameter's dim-0 shard and gathers / releases the full tensor.
+
+    Standalone use (the reference's constructor): ``param.data`` must already be this rank's
+    chunk; the gathers then run on a private side-stream runtime over a communicator created on
+    first use (a collective call, so every rank must materialise the same parameters)."""
 
     def __init__(self, param, shard_idx, world_size, shard_dim=0, *, runtime=None, shard=None,
-                 full_shape=None, keep_full_grad=False, gather_dtype=None):
+                 full_shape=None, keep_full_grad=False, gather_dtype=None, send_slot=None):
         if shard_dim != 0:
             raise NotImplementedError("zero_amd ZeRO-3 shards along dim 0 (as zero3.py:106)")
         self.param = param
@@ -146,10 +180,17 @@ class Zero3ParamManager:
         self.cs, self.r0, self.r1 = _chunk_geom(d0, world_size, shard_idx)
         self.S = self.cs * self.row  # padded chunk elements (equal on every rank)
         self.numel = int(np.prod(self.full_shape)) if self.full_shape else 1
+        # S elements starting at the shard, zero beyond its rows (the chunk arena's slot): the
+        # all-gather sends it as it is, so uneven chunks need no padding copy
+        self.send_slot = send_slot
         if gather_dtype not in (None, "fp8"):
             raise ValueError(f"gather_dtype must be None or 'fp8' (got {gather_dtype!r})")
         # fp8 only for matrices (row-wise scales); vectors (biases, norms) gather as they are
         self.fp8 = gather_dtype == "fp8" and len(self.full_shape) >= 2
+
+    def gather_bytes(self) -> int:
+        """Bytes this rank contributes to one all-gather of the parameter."""
+        return self.S + 4 * self.cs if self.fp8 else self.S * self.shard.element_size()
 
     # -- gather ----------------------------------------------------------------------------------
     # Three phases so a module's managers share one RCCL group: prepare (kernels on the side
@@ -165,13 +206,16 @@ class Zero3ParamManager:
                           q.data_ptr(), sc.data_ptr(), rows, self.row, stream_handle(stream))
             return (q, sc, torch.empty(ws * self.S, dtype=torch.uint8, device=dev),
                     torch.empty(ws * self.cs, dtype=torch.float32, device=dev))
-        send = self.shard.reshape(-1)
+        if self.send_slot is not None:
+            send = self.send_slot
+        else:
+            send = self.shard.reshape(-1)
+            if send.numel() != self.S:  # standalone short / empty chunk: pad to S elements
+                pad = torch.zeros(self.S, dtype=send.dtype, device=dev)
+                pad[:send.numel()].copy_(send)
+                send = pad
         if ws == 1:  # the shard is the whole parameter: nothing to gather
             return (send, send)
-        if send.numel() != self.S:  # short / empty last chunks: pad so every rank sends S elements
-            pad = torch.zeros(self.S, dtype=send.dtype, device=dev)
-            pad[:send.numel()].copy_(send)
-            send = pad
         return (send, torch.empty(ws * self.S, dtype=self.shard.dtype, device=dev))
 
     def _gather_issue(self, comm, stream, st):
@@ -197,11 +241,18 @@ class Zero3ParamManager:
         self.full_data = full[:self.numel].view(self.full_shape)
         self.param.data = self.full_data
 
+    def _runtime(self):
+        if self.runtime is None:
+            self.runtime = _GatherRuntime(self.world_size, self.shard_idx, RcclComm(),
+                                          self.shard.device)
+        return self.runtime
+
     def materialize(self):
         """zero3.py:36-41 for this one parameter."""
-        rt = self.runtime
-        rt.launch(("param", id(self)), [self])
-        out, ev = rt.pending.pop(("param", id(self)))
+        rt = self._runtime()
+        key = ("param", id(self))
+        rt.launch(key, [self])
+        out, ev = rt.pending.pop(key)
         cur = torch.cuda.current_stream(self.shard.device)
         cur.wait_event(ev)
         for m, full in out:
@@ -210,7 +261,7 @@ class Zero3ParamManager:
 
     def release(self):
         """zero3.py:43-52: back to the local shard; shrink a full-size grad to its local rows
-        (reference mode) or keep it for the reduce-scatter in step() (update mode)."""
+        (reference mode) or leave it to the reduce-scatter hook (update mode)."""
         self.param.data = self.shard
         g = self.param.grad
         if g is not None and g.shape != self.shard.shape and not self.keep_full_grad:
@@ -262,11 +313,203 @@ def register_zero3_hooks(model, param_managers):
     return handles
 
 
+class _ChunkArena:
+    """This rank's dim-0 chunks of every parameter in one flat buffer (Layout Z, zero3.py:107-108).
+
+    slot i: S_i = ceil(d0/ws)·row elements (the padded chunk every rank gathers), 64-element
+    aligned; the rank's real rows fill the first ln_i elements and the rest stays zero."""
+
+    def __init__(self, params, ws: int, rank: int, align: int = ALIGN_ELEMS):
+        self.ws, self.rank = ws, rank
+        self.full_shapes, self.rows, self.S, self.ln, self.slot, self.shard_shapes = [], [], [], [], [], []
+        self.numel = []
+        off = 0
+        for p in params:
+            fs = tuple(p.shape)
+            d0 = fs[0] if fs else 1
+            row = int(np.prod(fs[1:])) if len(fs) > 1 else 1
+            cs, r0, r1 = _chunk_geom(d0, ws, rank)
+            self.full_shapes.append(fs)
+            self.rows.append((r0, r1, row))
+            self.S.append(cs * row)
+            self.ln.append((r1 - r0) * row)
+            self.shard_shapes.append((r1 - r0,) + fs[1:])
+            self.numel.append(int(np.prod(fs)) if fs else 1)
+            self.slot.append(off)
+            off += _round_up(cs * row, align)
+        self.total = max(off, align)
+        self.S = np.asarray(self.S, np.int64)
+        self.ln = np.asarray(self.ln, np.int64)
+        self.slot = np.asarray(self.slot, np.int64)
+        p0 = params[0]
+        self.dtype, self.device = p0.dtype, p0.device
+        self.P = torch.zeros(self.total, dtype=self.dtype, device=self.device)
+        for i, p in enumerate(params):
+            r0, r1, row = self.rows[i]
+            n, s = int(self.ln[i]), int(self.slot[i])
+            if n:
+                self.P[s:s + n].copy_(p.detach().reshape(-1)[r0 * row:r0 * row + n])
+
+    def shard(self, i: int) -> torch.Tensor:
+        s, n = int(self.slot[i]), int(self.ln[i])
+        return self.P[s:s + n].view(self.shard_shapes[i])
+
+    def send_slot(self, i: int) -> torch.Tensor:
+        s = int(self.slot[i])
+        return self.P[s:s + int(self.S[i])]
+
+
+class _GradReducer:
+    """update mode: full-size gradients → summed chunks in the grad chunk arena, from backward.
+
+    Parameters are grouped in reverse index order (the order backward produces a sequential
+    model's grads) into buckets of at most ``bucket_bytes`` of full gradient.  A
+    post-accumulate-grad hook marks a parameter ready; a complete bucket whose predecessors have
+    all been launched is reduce-scattered at once — one RCCL group on the side stream, behind an
+    event on the stream that produced the grads — and its full gradients are released (their
+    memory returns to torch's allocator once the side stream has passed the collective).  The end
+    of backward (an autograd callback) launches whatever is left in the same fixed order, so every
+    rank issues the same collective sequence, and makes the compute stream wait for the last one."""
+
+    def __init__(self, opt, bucket_bytes: int):
+        self.opt = opt
+        arena = opt._arena
+        n = len(opt.params)
+        es = opt.params[0].element_size()
+        groups, cur, cur_b = [], [], 0
+        for i in reversed(range(n)):
+            b = arena.numel[i] * es
+            if cur and cur_b + b > bucket_bytes:
+                groups.append(cur)
+                cur, cur_b = [], 0
+            cur.append(i)
+            cur_b += b
+        if cur:
+            groups.append(cur)
+        self.groups = groups
+        self.K = len(groups)
+        self.bucket_of = np.zeros(n, np.int64)
+        for k, g in enumerate(groups):
+            self.bucket_of[g] = k
+        self._size = np.array([len(g) for g in groups], np.int64)
+        self.ev_done = [torch.cuda.Event() for _ in range(self.K)]
+        self.timing = None  # optional list of (start, end, bus_bytes) per launched bucket
+        self.reset()
+
+    def reset(self):
+        n = len(self.opt.params)
+        self.pending = self._size.copy()
+        self.marked = np.zeros(n, bool)
+        self.had_grad = np.zeros(n, bool)
+        self.local_grads = [None] * n  # ws == 1: the grad itself is the chunk's gradient
+        self.next = 0
+        self.callback_queued = False
+        self.launched_in_backward = 0
+
+    def register_hooks(self):
+        return [p.register_post_accumulate_grad_hook(lambda _p, i=i: self.on_grad_ready(i))
+                for i, p in enumerate(self.opt.params) if p.requires_grad]
+
+    def on_grad_ready(self, i: int):
+        if self.marked[i]:
+            raise RuntimeError(
+                "zero_amd ZeRO-3: gradient of parameter %d accumulated twice before step(); "
+                "update mode reduce-scatters each gradient once per step" % i)
+        self.marked[i] = True
+        self.pending[self.bucket_of[i]] -= 1
+        if not self.callback_queued:
+            self.callback_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._end_backward)
+        while self.next < self.K and self.pending[self.next] == 0:
+            self._launch(self.next)
+            self.launched_in_backward += 1
+            self.next += 1
+
+    def _end_backward(self):
+        self.flush()
+        self.install_shard_grads()
+
+    def flush(self):
+        """Launch every bucket not launched yet, in the fixed order."""
+        while self.next < self.K:
+            self._launch(self.next)
+            self.next += 1
+
+    def install_shard_grads(self):
+        """After backward every parameter shows its (summed, not yet averaged) gradient chunk, the
+        shard-size grad the reference's release() leaves (zero3.py:49-51)."""
+        opt = self.opt
+        if opt.world_size == 1:
+            return
+        cur = torch.cuda.current_stream(opt._arena.device)
+        if self.K:
+            cur.wait_event(self.ev_done[self.K - 1])
+        for i, p in enumerate(opt.params):
+            if self.had_grad[i] and p.data.shape == opt._arena.shard_shapes[i]:
+                s, n = int(opt._arena.slot[i]), int(opt._arena.ln[i])
+                p.grad = opt._G[s:s + n].view(opt._arena.shard_shapes[i])
+
+    def _launch(self, k: int):
+        opt = self.opt
+        ar, ws = opt._arena, opt.world_size
+        if ws == 1:  # nothing to exchange: Adam reads the local grad in place
+            for i in self.groups[k]:
+                g = opt.params[i].grad
+                if g is not None:
+                    if g.numel() != ar.numel[i] or not g.is_contiguous() or g.dtype != ar.dtype:
+                        raise ValueError("zero_amd ZeRO-3: grads must be contiguous, full-size and "
+                                         "of the parameter dtype")
+                    self.had_grad[i] = True
+                    self.local_grads[i] = g
+            return
+        dev = ar.device
+        cur = torch.cuda.current_stream(dev)
+        sends = []  # (param index, send buffer): alive until the RCCL group has been enqueued
+        for i in self.groups[k]:
+            p = opt.params[i]
+            g = p.grad
+            S, N = int(ar.S[i]), int(ar.numel[i])
+            if g is None:
+                send = torch.zeros(ws * S, dtype=ar.dtype, device=dev)  # every rank takes part
+            else:
+                if g.numel() != N or g.dtype != ar.dtype:
+                    raise ValueError("zero_amd ZeRO-3 update mode needs the full-size gradient "
+                                     "(param %d: got %s)" % (i, tuple(g.shape)))
+                self.had_grad[i] = True
+                flat = g.reshape(-1) if g.is_contiguous() else g.contiguous().reshape(-1)
+                if N == ws * S:
+                    send = flat  # zero-copy: rows of torch.chunk are contiguous
+                else:  # uneven chunks: every rank sends ws*S elements
+                    send = torch.zeros(ws * S, dtype=ar.dtype, device=dev)
+                    send[:N].copy_(flat)
+            sends.append((i, send))
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        cs = opt.runtime.stream
+        cs.wait_event(ready)
+        if self.timing is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record(cs)
+        with _group_ctx(opt.comm):
+            for i, send in sends:
+                s = int(ar.slot[i])
+                opt.comm.reduce_scatter(send, opt._G[s:s + int(ar.S[i])], cs)
+        # the group has been enqueued: a buffer freed from here on is only reused after it
+        for i, send in sends:
+            send.record_stream(cs)
+            opt.params[i].grad = None
+        self.ev_done[k].record(cs)
+        if self.timing is not None:
+            bus = sum(int(ar.S[i]) * ws for i, _ in sends) * ar.P.element_size() * (ws - 1) / ws
+            self.timing.append((e0, _timed_after(cs), bus))
+        del sends
+
+
 class ShardedOptimizer:
     """zero3.py:81-168 with ``update`` selecting reference (no-op) or real ZeRO-3 updates."""
 
     def __init__(self, optimizer: Optimizer, *, update: bool = False, comm=None, sync: bool = True,
-                 gather_dtype=None):
+                 gather_dtype=None, bucket_mb: float = 128.0):
         if not isinstance(optimizer, torch.optim.Adam):
             raise TypeError("zero_amd ShardedOptimizer wraps torch.optim.Adam / AdamW")
         self.optimizer = optimizer
@@ -289,58 +532,71 @@ class ShardedOptimizer:
         dev = self.params[0].device
         if dev.type != "cuda":
             raise RuntimeError("zero_amd: parameters must live on a GPU; there is no CPU path")
+        dtype = self.params[0].dtype
+        for p in self.params:
+            if p.device != dev or p.dtype != dtype:
+                raise TypeError("zero_amd: all parameters must share one device and dtype")
         if comm is None:
             comm = RcclComm()
         self.comm = comm
         self.runtime = _GatherRuntime(world_size, rank, comm, dev)
-        # zero3.py:104-110: every param becomes its dim-0 chunk; one manager per param
+        # zero3.py:104-110: every param becomes its dim-0 chunk — here a view of the chunk arena
+        # (the full tensor is released); one manager per param
+        self._arena = _ChunkArena(self.params, world_size, rank)
         self.param_managers = {}
-        self._full_shapes = []
-        for param in self.params:
-            full_shape = tuple(param.shape)
-            self._full_shapes.append(full_shape)
-            cs, r0, r1 = _chunk_geom(full_shape[0] if full_shape else 1, world_size, rank)
-            shard = param.data.reshape(full_shape or (1,))[r0:r1].contiguous() if full_shape else \
-                param.data.reshape(1).clone()
+        for i, param in enumerate(self.params):
+            shard = self._arena.shard(i)
             param.data = shard
             self.param_managers[param] = Zero3ParamManager(
                 param, rank, world_size, 0, runtime=self.runtime, shard=shard,
-                full_shape=full_shape, keep_full_grad=self.update, gather_dtype=gather_dtype)
-        for group in self.optimizer.param_groups:  # zero3.py:114-115
-            group["params"] = [p for p in group["params"] if p in self.local_params]
+                full_shape=self._arena.full_shapes[i], keep_full_grad=self.update,
+                gather_dtype=gather_dtype, send_slot=self._arena.send_slot(i))
+        if not self.update:
+            for group in self.optimizer.param_groups:  # zero3.py:114-115
+                group["params"] = [p for p in group["params"] if p in self.local_params]
         self.grad_hooks = {}
         self.communication_time = 0.0
         self.step_time = 0.0
         self.last_reduced_grads = None
-        self._engine = None
         self.timing_events = None  # optional list of (start, end, bytes) around each Adam launch
+        self._comm_spans = []      # (start event, end event) pairs not yet added to comm time
+        self._reducer = None
+        self._G = None
+        self._hook_handles = []
+        if self.update:
+            self._build_update_state()
+            self._reducer = _GradReducer(self, int(bucket_mb * (1 << 20)))
+            self._hook_handles = self._reducer.register_hooks()
 
     # ------------------------------------------------------------------------------------------
-    def _build_update_engine(self):
-        dev = self.params[0].device
-        dtype = self.params[0].dtype
-        numels = [int(np.prod(s)) if s else 1 for s in self._full_shapes]
-        dim0 = [s[0] if s else 1 for s in self._full_shapes]
-        plan = Plan(numels, self.world_size, self.rank, "chunk", dim0=dim0, align_elems=ALIGN_ELEMS)
-        L = plan.stream_len(self.rank)
-        pc = plan.pieces(self.rank)
+    def _build_update_state(self):
+        ar = self._arena
+        L = ar.total
+        split = ar.dtype == torch.bfloat16
         # exp_avg, exp_avg_sq (+ for bf16 params the split master's int16 residual: the fp32
-        # master is the bf16 shard + residual, include/zero_amd.h ZS_BF16_SPLIT; starts at 0)
-        nlo = (L + 1) // 2 if dtype == torch.bfloat16 else 0
-        state, placement = probed_zeros(2 * L + nlo, torch.float32, dev)
-        eng = dict(plan=plan, pieces=pc, L=L, dtype=dtype, state=state, placement=placement,
-                   m=state[:L], v=state[L:2 * L],
-                   vmax=None, gshard=torch.zeros(L, dtype=dtype, device=dev),
-                   lo=state[2 * L:].view(torch.int16)[:L] if nlo else None,
-                   steps=np.zeros(len(self.params), np.int64), cache={}, retired=[])
-        self._engine = eng
-        for i, so, ln in zip(pc.param, pc.stream_off, pc.length):
-            p = self.params[i]
-            shp = self.param_managers[p].shard.shape
+        # master is the bf16 chunk + residual, include/zero_amd.h ZS_BF16_SPLIT; starts at 0)
+        nlo = (L + 1) // 2 if split else 0
+        state, self.placement = probed_zeros(2 * L + nlo, torch.float32, ar.device)
+        self._state = state
+        self._m, self._v = state[:L], state[L:2 * L]
+        self._lo = state[2 * L:].view(torch.int16)[:L] if split else None
+        self._vmax = None
+        self._split = split
+        self._G = torch.zeros(L, dtype=ar.dtype, device=ar.device) if self.world_size > 1 else None
+        self._steps = np.zeros(len(self.params), np.int64)
+        self._adam_cache = {}
+        self._retired = []
+        for i, p in enumerate(self.params):
+            s, n = int(ar.slot[i]), int(ar.ln[i])
             st = self.optimizer.state[p]
-            st["exp_avg"] = eng["m"][so:so + ln].view(shp)
-            st["exp_avg_sq"] = eng["v"][so:so + ln].view(shp)
+            st["exp_avg"] = self._m[s:s + n].view(ar.shard_shapes[i])
+            st["exp_avg_sq"] = self._v[s:s + n].view(ar.shard_shapes[i])
 
+    def grad_arena(self):
+        """The flat gradient chunk arena (update mode, ws > 1): slot i holds param i's summed chunk."""
+        return self._G
+
+    # ------------------------------------------------------------------------------------------
     def _reduce_reference(self):
         """zero3.py:131-153: chunk full grads, all-reduce shard grads, /ws, then discard all."""
         cur = torch.cuda.current_stream()
@@ -358,93 +614,102 @@ class ShardedOptimizer:
                 pad[:n].copy_(g.reshape(-1))
                 shards.append((pad, n, g.shape))
             else:
-                shards.append((g, n, g.shape))
-        grp = getattr(self.comm, "group", None)
-        with (grp() if grp is not None else contextlib.nullcontext()):
+                shards.append((g.contiguous(), n, g.shape))
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        cs = self.runtime.stream
+        cs.wait_event(ready)
+        with _group_ctx(self.comm):
             for buf, _, _ in shards:
-                self.comm.all_reduce(buf, cur)
-        self.last_reduced_grads = [buf.reshape(-1)[:n].view(shp).div_(self.world_size)
-                                   for buf, n, shp in shards]
+                self.comm.all_reduce(buf, cs)
+        # after the group: the division runs behind the collectives on the side stream
+        with torch.cuda.stream(cs):
+            self.last_reduced_grads = [buf.reshape(-1)[:n].view(shp).div_(self.world_size)
+                                       for buf, n, shp in shards]
+        for buf, _, _ in shards:
+            buf.record_stream(cs)
+        done = _timed_after(cs)
+        cur.wait_event(done)
         for param in self.params:  # zero3.py:150-153 for-else: every grad is dropped
             param.grad = None
+        return done
+
+    def _adam_rows(self, idx):
+        """zs_adam_seg rows (g, master, master_out, p_out, m, v, vmax, carry, n) of the chunks of
+        the params in ``idx``."""
+        ar, red = self._arena, self._reducer
+        es = ar.P.element_size()
+        so = ar.slot[idx].astype(np.uint64)
+        rows = np.zeros((len(idx), 9), np.uint64)
+        if self.world_size > 1:
+            rows[:, 0] = np.uint64(self._G.data_ptr()) + so * np.uint64(es)
+        else:
+            rows[:, 0] = [red.local_grads[i].data_ptr() for i in idx]
+        pp = np.uint64(ar.P.data_ptr()) + so * np.uint64(es)
+        if self._split:  # master = bf16 chunk (in and out) + int16 residual
+            rows[:, 1], rows[:, 3] = pp, pp
+            rows[:, 2] = np.uint64(self._lo.data_ptr()) + so * np.uint64(2)
+        else:
+            rows[:, 1], rows[:, 2] = pp, pp
+        rows[:, 4] = np.uint64(self._m.data_ptr()) + so * np.uint64(4)
+        rows[:, 5] = np.uint64(self._v.data_ptr()) + so * np.uint64(4)
+        if self._vmax is not None:
+            rows[:, 6] = np.uint64(self._vmax.data_ptr()) + so * np.uint64(4)
+        rows[:, 8] = ar.ln[idx].astype(np.uint64)
+        return rows
 
     def _step_update(self):
-        if self._engine is None:
-            self._build_update_engine()
-        eng = self._engine
-        cur = torch.cuda.current_stream()
-        pc, ws = eng["pieces"], self.world_size
-        has = np.array([p.grad is not None for p in self.params])
-        # 1. reduce-scatter every full-size grad into this rank's chunk (one RCCL group)
-        grp = getattr(self.comm, "group", None)
-        with (grp() if grp is not None else contextlib.nullcontext()):
-            for i, so, ln in zip(pc.param, pc.stream_off, pc.length):
-                p = self.params[i]
-                man = self.param_managers[p]
-                if p.grad is None:
-                    continue
-                g = p.grad.reshape(-1)
-                if g.numel() != man.numel:
-                    raise RuntimeError("ZeRO-3 update mode needs full-size grads at step()")
-                if man.S * ws != man.numel:  # uneven chunks: pad to ws*S
-                    pad = torch.zeros(man.S * ws, dtype=g.dtype, device=g.device)
-                    pad[:man.numel].copy_(g)
-                    g = pad
-                recv = eng["gshard"][so:so + man.S] if ln == man.S else torch.empty(
-                    man.S, dtype=g.dtype, device=g.device)
-                self.comm.reduce_scatter(g, recv, cur)
-                if ln != man.S and ln:
-                    eng["gshard"][so:so + ln].copy_(recv[:ln])
-        # 2. fused Adam over every chunk this rank holds
-        owned = np.array([ln > 0 for ln in pc.length]) & has[pc.param]
-        idx = pc.param[owned]
-        eng["steps"][idx] += 1
-        if any(adam_group_hparams(g, self.optimizer)["amsgrad"] for g in self._groups) and eng["vmax"] is None:
-            eng["vmax"] = torch.zeros(eng["L"], dtype=torch.float32, device=eng["m"].device)
-        rows = np.zeros((len(idx), 9), np.uint64)
-        es = self.params[0].element_size()
-        so = pc.stream_off[owned].astype(np.uint64)
-        rows[:, 0] = np.uint64(eng["gshard"].data_ptr()) + so * np.uint64(es)
-        shard_ptr = np.array([self.param_managers[self.params[i]].shard.data_ptr() for i in idx], np.uint64)
-        if eng["lo"] is not None:  # master = bf16 shard (in and out) + residual
-            rows[:, 1], rows[:, 3] = shard_ptr, shard_ptr
-            rows[:, 2] = np.uint64(eng["lo"].data_ptr()) + so * np.uint64(2)
-        else:
-            rows[:, 1], rows[:, 2] = shard_ptr, shard_ptr
-        rows[:, 4] = np.uint64(eng["m"].data_ptr()) + so * np.uint64(4)
-        rows[:, 5] = np.uint64(eng["v"].data_ptr()) + so * np.uint64(4)
-        if eng["vmax"] is not None:
-            rows[:, 6] = np.uint64(eng["vmax"].data_ptr()) + so * np.uint64(4)
-        rows[:, 8] = pc.length[owned].astype(np.uint64)
-        keys = np.stack([np.asarray(self._group_of)[idx], eng["steps"][idx]], axis=1)
-        for key in np.unique(keys, axis=0) if len(idx) else []:
-            sel = np.nonzero((keys == key).all(axis=1))[0]
-            sub = np.ascontiguousarray(rows[sel])
-            ck = (int(key[0]), len(sel), int(sel[0]))
-            hit = eng["cache"].get(ck)
-            if hit is None or hit[0] != sub.tobytes():
-                if hit is not None:  # keep until the device is idle (hipFree would sync it)
-                    eng["retired"].append(hit[1])
-                hit = (sub.tobytes(), AdamSet(sub, ZS_BF16, ZS_BF16_SPLIT) if eng["lo"] is not None
-                       else AdamSet(sub, ZS_F32))
-                eng["cache"][ck] = hit
-            h = adam_group_hparams(self._groups[int(key[0])], self.optimizer)
-            hp = adam_hparams(h["lr"], h["beta1"], h["beta2"], h["eps"], h["weight_decay"], int(key[1]),
-                              decoupled=h["decoupled"], amsgrad=h["amsgrad"], maximize=h["maximize"],
-                              grad_div=float(ws))
-            if self.timing_events is not None:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(cur)
-                hit[1].run(hp, cur)
-                e1.record(cur)
-                self.timing_events.append((e0, e1, hit[1].bytes))
-            else:
-                hit[1].run(hp, cur)
+        red, ar = self._reducer, self._arena
+        cur = torch.cuda.current_stream(ar.device)
+        red.flush()  # grads assigned outside backward (or backward without hooks firing)
+        done = None
+        if self.world_size > 1 and red.K:
+            done = red.ev_done[red.K - 1]
+            cur.wait_event(done)
+        idx = np.nonzero(red.had_grad & (ar.ln > 0))[0]
+        self._steps[idx] += 1
+        hps = {gi: adam_group_hparams(self._groups[gi], self.optimizer) for gi in set(self._group_of)}
+        if any(h["amsgrad"] for h in hps.values()) and self._vmax is None:
+            self._vmax = torch.zeros(ar.total, dtype=torch.float32, device=ar.device)
+            for i, p in enumerate(self.params):
+                s, n = int(ar.slot[i]), int(ar.ln[i])
+                self.optimizer.state[p]["max_exp_avg_sq"] = self._vmax[s:s + n].view(ar.shard_shapes[i])
+        if len(idx):
+            rows = self._adam_rows(idx)
+            keys = np.stack([np.asarray(self._group_of)[idx], self._steps[idx]], axis=1)
+            for key in np.unique(keys, axis=0):
+                sel = np.nonzero((keys == key).all(axis=1))[0]
+                sub = np.ascontiguousarray(rows[sel])
+                ck = (int(key[0]), len(sel), int(sel[0]))
+                hit = self._adam_cache.get(ck)
+                if hit is None or hit[0] != sub.tobytes():
+                    if hit is not None:  # keep until the device is idle (hipFree would sync it)
+                        self._retired.append(hit[1])
+                    hit = (sub.tobytes(), AdamSet(sub, ZS_BF16, ZS_BF16_SPLIT) if self._split
+                           else AdamSet(sub, ZS_F32))
+                    self._adam_cache[ck] = hit
+                h = hps[int(key[0])]
+                hp = adam_hparams(h["lr"], h["beta1"], h["beta2"], h["eps"], h["weight_decay"],
+                                  int(key[1]), decoupled=h["decoupled"], amsgrad=h["amsgrad"],
+                                  maximize=h["maximize"], grad_div=float(self.world_size))
+                if self.timing_events is not None:
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e0.record(cur)
+                    hit[1].run(hp, cur)
+                    self.timing_events.append((e0, _timed_after(cur), hit[1].bytes))
+                else:
+                    hit[1].run(hp, cur)
+        step_t = {}
         for i in idx:
-            st = self.optimizer.state[self.params[i]]
-            st["step"] = torch.tensor(float(eng["steps"][i]))
-        for p in self.params:
+            s = int(self._steps[i])
+            t = step_t.get(s)
+            if t is None:
+                t = step_t[s] = torch.tensor(float(s))
+            self.optimizer.state[self.params[i]]["step"] = t
+        for p in self.params:  # zero3.py:150-153: no grad survives the step
             p.grad = None
+        red.reset()
+        return done
 
     def step(self, closure=None):
         loss = None
@@ -452,19 +717,31 @@ class ShardedOptimizer:
             with torch.enable_grad():
                 loss = closure()
         step_start = time.perf_counter()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record(torch.cuda.current_stream(self.params[0].device))
         with torch.no_grad():
-            if self.update:
-                self._step_update()
-            else:
-                self._reduce_reference()
-        if self._sync or (self._engine is not None and len(self._engine["retired"]) > 64):
+            done = self._step_update() if self.update else self._reduce_reference()
+        if done is not None and self.world_size > 1:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record(self.runtime.stream)  # after the last gradient collective
+            self._comm_spans.append((e0, e1))
+        retired = len(self._retired) if self.update else 0
+        if self._sync or retired > 64:
             torch.cuda.synchronize()
-            if self._engine is not None:
-                self._engine["retired"].clear()
-        self.communication_time += time.perf_counter() - step_start
+            if self.update:
+                self._retired.clear()
+            self._collect_comm_time()
         self.runtime.end_iteration()
         self.step_time += time.perf_counter() - step_start
         return loss
+
+    def _collect_comm_time(self):
+        """zero3.py:125,158: communication_time = from step() entry until the gradient reduction is
+        done.  Measured on the device: step-entry event on the compute stream → event after the
+        last gradient collective on the side stream (0 when backward already finished them)."""
+        for e0, e1 in self._comm_spans:
+            self.communication_time += max(0.0, e0.elapsed_time(e1) / 1e3)
+        self._comm_spans.clear()
 
     def zero_grad(self, set_to_none: bool = True):
         self.optimizer.zero_grad(set_to_none=set_to_none)

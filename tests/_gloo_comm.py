@@ -5,7 +5,14 @@ ranks of the same Communicator is not supported", rccl.h:174-176), and the GPU b
 exercise the engine's multi-rank orchestration (Layout R buckets, in-place reduce-scatter /
 all-gather slices, ZeRO-1 carry, per-rank Adam windows) with the real HIP pack / Adam / unpack
 kernels, ws processes share cuda:0 and exchange through this class.  Sums are done in fp32.
+
+``group()`` behaves like an RCCL group: collectives issued inside it are held back and run at
+group exit, after every kernel the caller enqueued on the stream before the exit — so a caller
+that reads a collective's output, or frees one of its buffers, inside the group is caught here as
+it would be on the device.
 """
+import contextlib
+
 import torch
 import torch.distributed as dist
 
@@ -16,8 +23,30 @@ class GlooStagedComm:
         self.ws = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.calls = []
+        self._deferred = None
+
+    @contextlib.contextmanager
+    def group(self):
+        if self._deferred is not None:  # nested: the outer group runs everything
+            yield
+            return
+        self._deferred = []
+        try:
+            yield
+        finally:
+            ops, self._deferred = self._deferred, None
+            for fn, args in ops:
+                fn(*args)
+
+    def _defer(self, fn, *args):
+        if self._deferred is None:
+            return False
+        self._deferred.append((fn, args))
+        return True
 
     def reduce_scatter(self, send, recv, stream):
+        if self._defer(self.reduce_scatter, send, recv, stream):
+            return
         stream.synchronize()
         h = send.detach().to("cpu", torch.float32)
         out = torch.empty(recv.numel(), dtype=torch.float32)
@@ -27,6 +56,8 @@ class GlooStagedComm:
         self.calls.append(("rs", send.numel()))
 
     def all_gather(self, send, recv, stream):
+        if self._defer(self.all_gather, send, recv, stream):
+            return
         stream.synchronize()
         h = send.detach().to("cpu")
         if h.dtype != torch.float32:  # a gather is a byte copy: move bf16 / uint8 as int8 bytes
@@ -42,6 +73,8 @@ class GlooStagedComm:
         return dist.get_global_rank(self.group, root) if self.group else root
 
     def reduce(self, t, root, stream):
+        if self._defer(self.reduce, t, root, stream):
+            return
         stream.synchronize()
         h = t.detach().to("cpu", torch.float32)
         dist.reduce(h, dst=self._root(root), group=self.group)
@@ -51,6 +84,8 @@ class GlooStagedComm:
         self.calls.append(("reduce", t.numel()))
 
     def broadcast(self, t, root, stream):
+        if self._defer(self.broadcast, t, root, stream):
+            return
         stream.synchronize()
         h = t.detach().to("cpu")
         if h.dtype != torch.float32:
@@ -62,6 +97,8 @@ class GlooStagedComm:
         self.calls.append(("bcast", t.numel()))
 
     def reduce_v(self, buf, win_off, win_len, stream):
+        if self._defer(self.reduce_v, buf, win_off, win_len, stream):
+            return
         stream.synchronize()
         h = buf.detach().to("cpu", torch.float32)
         for root, (off, n) in enumerate(zip(win_off, win_len)):
@@ -76,6 +113,8 @@ class GlooStagedComm:
         self.calls.append(("rsv", int(sum(win_len))))
 
     def broadcast_v(self, buf, win_off, win_len, stream):
+        if self._defer(self.broadcast_v, buf, win_off, win_len, stream):
+            return
         stream.synchronize()
         h = buf.detach().to("cpu")
         for root, (off, n) in enumerate(zip(win_off, win_len)):
@@ -89,9 +128,60 @@ class GlooStagedComm:
         self.calls.append(("agv", int(sum(win_len))))
 
     def all_reduce(self, t, stream):
+        if self._defer(self.all_reduce, t, stream):
+            return
         stream.synchronize()
         h = t.detach().to("cpu", torch.float32)
         dist.all_reduce(h, group=self.group)
         with torch.cuda.stream(stream):
             t.copy_(h.to(t.device).to(t.dtype))
         self.calls.append(("ar", t.numel()))
+
+
+class SimRankComm:
+    """TEST-ONLY stand-in for rank ``rank`` of a ``ws``-rank job on one GPU, where every other rank
+    contributes zeros to each sum and holds, for every gather, the same shard as this rank.  It lets
+    a full-scale run exercise rank 0's real layout and kernels (arena slots, uneven chunks, Adam on
+    the owned window) without peers.  ``log`` keeps, per reduce-scatter, a copy of this rank's
+    chunk of the send buffer (what the sum delivers) and the receive pointer."""
+
+    def __init__(self, ws, rank=0, keep_log=False):
+        self.ws, self.rank = ws, rank
+        self.log = [] if keep_log else None
+
+    def group(self):
+        return contextlib.nullcontext()
+
+    def reduce_scatter(self, send, recv, stream):
+        n = recv.numel()
+        with torch.cuda.stream(stream):
+            mine = send[self.rank * n:(self.rank + 1) * n]
+            if self.log is not None:
+                self.log.append((recv.data_ptr(), mine.clone()))
+            if mine.data_ptr() != recv.data_ptr():
+                recv.copy_(mine)
+
+    def all_gather(self, send, recv, stream):
+        with torch.cuda.stream(stream):
+            src = send.clone()
+            recv.view(self.ws, -1).copy_(src.view(1, -1).expand(self.ws, -1))
+
+    def reduce_out(self, send, recv, root, stream):
+        if root == self.rank and send.data_ptr() != recv.data_ptr():
+            with torch.cuda.stream(stream):
+                recv.copy_(send)
+
+    def all_reduce(self, t, stream):
+        pass
+
+    def reduce(self, t, root, stream):
+        pass
+
+    def broadcast(self, t, root, stream):
+        pass
+
+    def reduce_v(self, buf, win_off, win_len, stream):
+        pass
+
+    def broadcast_v(self, buf, win_off, win_len, stream):
+        pass

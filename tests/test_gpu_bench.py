@@ -55,13 +55,33 @@ def test_bench_simulated_ws8_bucket_path(gpu):
     assert "diagnostic" in out and out["buckets"] > 1 and out["ms_per_step"] > 0
 
 
-def test_bench_zero3_parameter_set_simulated_ws8(gpu):
-    """--zero 3 on C4: the Layout Z (dim-0 chunk) bucket path of rank 0 of 8 at full scale."""
+def test_bench_zero3_parameter_set_n1(gpu):
+    """--zero 3 on C4 (configs[4]'s step on the 3B set): 38 hooked layer modules, update mode."""
     out = _run([sys.executable, "bench.py", "--config", "C4", "--zero", "3", "--steps", "3",
+                "--warmup", "1", "--no-cpu-baseline"])
+    assert out["config"]["zero"] == 3 and out["value"] > 0 and out["n_gpus"] == 1
+    assert out["zero3"]["gathers_per_step"] > 0 and out["roofline"]["frac"] > 0
+
+
+def test_bench_zero3_parameter_set_simulated_ws8(gpu):
+    """Rank 0's compute of the hooked ZeRO-3 C5 iteration at ws=8 (collectives skipped)."""
+    out = _run([sys.executable, "bench.py", "--config", "C5", "--zero", "3", "--steps", "2",
                 "--warmup", "1", "--simulate-ws", "8", "--no-cpu-baseline"])
-    assert "diagnostic" in out and out["buckets"] > 1
-    # Layout Z is balanced: rank 0 holds 1/8 of every parameter (dims divide by 8 in C4)
-    assert out["stream_elems"] * 8 >= 3_075_098_624 and out["stream_elems"] < 3_075_098_624 // 8 * 1.01
+    assert "diagnostic" in out and out["layers"] == 34
+    # Layout Z is balanced: rank 0 holds 1/8 of every parameter (C5 dims divide by 8)
+    assert out["chunk_elems"] * 8 == 8_030_261_248
+
+
+def test_bench_zero3_parameter_set_two_ranks_gloo_staged(gpu):
+    """The N>1 ZeRO-3 parameter-set path incl. its exchange check (gather bit-exact, backward
+    reduce-scatter within the bf16 bound), 2 ranks on the one GPU through the gloo-staged comm."""
+    out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+                "--config", "C4", "--zero", "3", "--set-layers", "2", "--steps", "2", "--warmup", "1",
+                "--comm", "gloo-staged"], timeout=600)
+    assert out["n_gpus"] == 2 and out["exchange_check"]["all_ranks_ok"]
+    assert out["exchange_check"]["gather_bit_exact"]
+    assert out["collectives"]["all_gather"]["calls_per_step"] > 0
 
 
 def test_bench_zero3_training_iteration(gpu):

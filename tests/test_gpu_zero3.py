@@ -1,5 +1,10 @@
 """ZeRO-3 drop-in on the MI355X vs the reference (tests/golden/traj_z3_*) and, in update mode,
-vs data-parallel Adam (the ZeRO-2 fixtures, sliced to each rank's dim-0 chunk)."""
+vs data-parallel Adam (the ZeRO-2 fixtures, sliced to each rank's dim-0 chunk).
+
+Multi-rank cases run ws processes on the box's one GPU with the gloo-staged communicator
+(tests/_gloo_comm.py), whose group() holds collectives back to the group's end like RCCL does.
+Full-scale cases (C3's 6 × Linear(12800), C5's 8.03e9-parameter set) run rank 0 of ws=8 against
+SimRankComm and check sampled chunk elements bit-exactly against the C oracle."""
 
 import numpy as np
 import pytest
@@ -17,19 +22,25 @@ def _port():
     return free_port()
 
 
-def _model(z, dev):
+def _model(z, dev, dtype=torch.float32):
     layers = []
     for i in range(6):
         lin = torch.nn.Linear(16, 16)
         lin.weight.data = torch.from_numpy(z[f"init_{2 * i}"].copy())
         lin.bias.data = torch.from_numpy(z[f"init_{2 * i + 1}"].copy())
         layers += [lin, torch.nn.ReLU()] if i < 5 else [lin]
-    return torch.nn.Sequential(*layers).to(dev)
+    return torch.nn.Sequential(*layers).to(dev, dtype)
 
 
 def _chunk(a, ws, r):
     cs = -(-a.shape[0] // ws)
     return a[r * cs:(r + 1) * cs]
+
+
+def _xy(z, rank, dev):
+    x = torch.from_numpy(z["x"] if "x" in z.files else z[f"r{rank}_x"]).to(dev)
+    y = torch.from_numpy(z["y"] if "y" in z.files else z[f"r{rank}_y"]).to(dev)
+    return x, y
 
 
 def _set_grad(p, g):
@@ -52,8 +63,7 @@ def _ref_mode(rank, ws, name, dev, comm=None):
     kw = {} if comm is None else {"comm": comm}
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), **kw)
     zero3.register_zero3_hooks(model, opt.param_managers)
-    x = torch.from_numpy(z["x"] if "x" in z.files else z[f"r{rank}_x"]).to(dev)
-    y = torch.from_numpy(z["y"] if "y" in z.files else z[f"r{rank}_y"]).to(dev)
+    x, y = _xy(z, rank, dev)
     for t in range(int(z["steps"])):
         opt.zero_grad()
         loss = torch.nn.functional.mse_loss(model(x), y)
@@ -103,6 +113,7 @@ def _update_injected(rank, ws, name, dev, comm=None, dtype=torch.float32):
         for i, p in enumerate(params):
             _set_grad(p, torch.from_numpy(z[f"r{rank}_t{t}_lg{i}"].copy()).to(dev))
         opt.step()
+        assert all(p.grad is None for p in params)
         if f"r{rank}_t{t}_p0" in z.files:
             for i, p in enumerate(params):
                 want = _chunk(z[f"r{rank}_t{t}_p{i}"], ws, rank)
@@ -113,6 +124,45 @@ def _update_injected(rank, ws, name, dev, comm=None, dtype=torch.float32):
         torch.cuda.synchronize()
         assert rel(p.detach().cpu().numpy(), z[f"r{rank}_t9_p{i}"]) <= 1e-6
         m.release()
+    # every rank's optimizer state is its chunk of the reference's (DP-Adam) state
+    for i, p in enumerate(params):
+        key = f"r{rank}_state_{i}_exp_avg"
+        if key in z.files:  # the fixture holds the state of the reference owner's params
+            st = opt.optimizer.state[p]
+            assert st["exp_avg"].shape == p.shape
+            assert rel(st["exp_avg"].cpu().numpy(), _chunk(z[key], ws, rank)) <= 1e-6
+
+
+def _update_hooks(rank, ws, name, dev, comm=None):
+    """update=True through the real hooks: forward / backward all-gathers, gradients
+    reduce-scattered from the post-accumulate-grad hooks during backward, fused Adam on the
+    chunks.  Grads come from hipBLAS GEMMs, so the bound vs the CPU reference is 1e-4."""
+    from zero_amd import zero3
+
+    z = np.load(GOLDEN / name)
+    model = _model(z, dev)
+    kw = {} if comm is None else {"comm": comm}
+    opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
+                                 bucket_mb=2e-3, **kw)  # ~2 KB buckets: several launches in backward
+    zero3.register_zero3_hooks(model, opt.param_managers)
+    params = list(model.parameters())
+    x, y = _xy(z, rank, dev)
+    for t in range(int(z["steps"])):
+        opt.zero_grad()
+        loss = torch.nn.functional.mse_loss(model(x), y)
+        loss.backward()
+        if ws > 1:  # backward left every grad as its summed chunk, full grads already released
+            assert opt._reducer.next == opt._reducer.K and opt._reducer.launched_in_backward > 0
+            assert [tuple(p.grad.shape) for p in params] == [tuple(p.shape) for p in params]
+        opt.step()
+        assert all(p.grad is None for p in params)
+        if f"r{rank}_t{t}_p0" in z.files:
+            for i, p in enumerate(params):
+                want = _chunk(z[f"r{rank}_t{t}_p{i}"], ws, rank)
+                assert rel(p.detach().cpu().numpy(), want) <= 1e-4, (t, i)
+    assert opt.runtime.n_prefetch_hits > 0
+    if ws > 1:
+        assert opt.communication_time >= 0.0
 
 
 @pytest.fixture
@@ -134,6 +184,10 @@ def test_ws1_update_mode(gpu, pg1):
     _update_injected(0, 1, "traj_z2_ws1_d16_distinct.npz", gpu)
 
 
+def test_ws1_update_mode_hooks(gpu, pg1):
+    _update_hooks(0, 1, "traj_z2_ws1_d16_ref.npz", gpu)
+
+
 def _mr(rank, ws, port, fn, name):
     from _gloo_comm import GlooStagedComm
 
@@ -144,7 +198,7 @@ def _mr(rank, ws, port, fn, name):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws", [2, 4])
+@pytest.mark.parametrize("ws", [2, 4, 8])
 def test_multirank_reference_mode_hooks(gpu, ws):
     mp.spawn(_mr, args=(ws, _port(), "_ref_mode", f"traj_z3_ws{ws}_d16_distinct.npz"), nprocs=ws)
 
@@ -154,8 +208,179 @@ def test_multirank_reference_mode_injected(gpu, ws):
     mp.spawn(_mr, args=(ws, _port(), "_ref_injected", f"traj_z3_ws{ws}_d16_ref.npz"), nprocs=ws)
 
 
-@pytest.mark.parametrize("ws", [2, 3, 4])
+@pytest.mark.parametrize("ws", [2, 3, 4, 8])
 def test_multirank_update_mode(gpu, ws):
     """ws=3 exercises uneven torch.chunk (16 rows → 6,6,4), which deadlocks the reference."""
     mp.spawn(_mr, args=(ws, _port(), "_update_injected", f"traj_z2_ws{ws}_d16_distinct.npz"),
              nprocs=ws)
+
+
+@pytest.mark.parametrize("ws,mode", [(2, "distinct"), (3, "distinct"), (4, "distinct"), (8, "ref"),
+                                     (8, "distinct")])
+def test_multirank_update_mode_hooks(gpu, ws, mode):
+    mp.spawn(_mr, args=(ws, _port(), "_update_hooks", f"traj_z2_ws{ws}_d16_{mode}.npz"), nprocs=ws)
+
+
+def _mem_worker(rank, ws, port):
+    """update mode frees each full gradient once its reduce-scatter is enqueued: peak gradient
+    memory during backward is one bucket, not the model; the full parameters are released."""
+    from _gloo_comm import GlooStagedComm
+    from zero_amd import zero3
+
+    torch.cuda.set_device(0)
+    init_pg(rank, ws, port)
+    dev = torch.device("cuda:0")
+    D, L = 1024, 8
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(*[torch.nn.Linear(D, D, bias=False) for _ in range(L)]).to(dev)
+    full_bytes = L * D * D * 4
+    torch.cuda.synchronize()
+    before = torch.cuda.memory_allocated(dev)
+    opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
+                                 comm=GlooStagedComm(), bucket_mb=D * D * 4 / (1 << 20))
+    zero3.register_zero3_hooks(model, opt.param_managers)
+    torch.cuda.synchronize()
+    after = torch.cuda.memory_allocated(dev)
+    # the full params are gone; the chunk arena, grad chunks and fp32 m / v (each 1/ws) remain
+    assert after - before <= -full_bytes + 4 * full_bytes // ws + (1 << 20), (before, after)
+    for p in model.parameters():  # the shard is a view of the chunk arena, not of the old tensor
+        assert p.data.untyped_storage().data_ptr() == opt._arena.P.untyped_storage().data_ptr()
+    x = torch.randn(4, D, device=dev)
+    for _ in range(2):
+        opt.zero_grad()
+        loss = model(x).square().mean()
+        torch.cuda.synchronize()
+        base = torch.cuda.memory_allocated(dev)
+        torch.cuda.reset_peak_memory_stats(dev)
+        loss.backward()
+        torch.cuda.synchronize()
+        peak = torch.cuda.max_memory_allocated(dev) - base
+        # one layer's full weight gathered + one full grad in flight (+ slack), never all L grads
+        assert peak <= 4 * D * D * 4 + (1 << 20), (peak, full_bytes)
+        opt.step()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_update_mode_gradient_memory_is_sharded(gpu):
+    mp.spawn(_mem_worker, args=(4, _port()), nprocs=4)
+
+
+def test_update_mode_double_backward_raises(gpu, pg1):
+    from zero_amd import zero3
+
+    lin = torch.nn.Linear(8, 8).to(gpu)
+    opt = zero3.ShardedOptimizer(torch.optim.Adam(lin.parameters(), lr=1e-3), update=True)
+    zero3.register_zero3_hooks(lin, opt.param_managers)
+    x = torch.randn(2, 8, device=gpu)
+    lin(x).sum().backward()
+    with pytest.raises(RuntimeError, match="accumulated twice"):
+        lin(x).sum().backward()
+
+
+def test_c3_hooked_iteration_rank0_of_ws8(gpu, monkeypatch):
+    """BASELINE.json configs[2] at full size: 6 × Linear(12800, 12800) + ReLU (983M fp32 params),
+    rank 0 of ws=8: hooked forward / backward (gathers, backward reduce-scatters into the grad
+    chunk arena) then the update.  Rank 0's updated chunks equal the C oracle's Adam of (its chunk
+    of the gradient / 8) on 4096 sampled elements per tensor, bit for bit."""
+    import zero_amd.zero3 as z3
+    from _gloo_comm import SimRankComm
+    from oracle import c_oracle
+
+    ws, D = 8, 12800
+    init_pg(0, 1, _port())
+    real_get = z3.get
+    monkeypatch.setattr(z3, "get", lambda what, dm=None: {"ws": ws, "rank": 0}[what]
+                        if what in ("ws", "rank") else real_get(what, dm))
+    try:
+        torch.manual_seed(0)
+        layers = []
+        for i in range(6):
+            layers += [torch.nn.Linear(D, D, device=gpu)] + ([torch.nn.ReLU()] if i < 5 else [])
+        model = torch.nn.Sequential(*layers)
+        comm = SimRankComm(ws, 0, keep_log=True)
+        opt = z3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
+                                  comm=comm, sync=True)
+        z3.register_zero3_hooks(model, opt.param_managers)
+        params = list(model.parameters())
+        init = opt._arena.P.clone()
+        g = torch.Generator(device=gpu).manual_seed(42)
+        x = torch.randn(16, D, device=gpu, generator=g)
+        y = torch.randn(16, D, device=gpu, generator=g)
+        opt.zero_grad()
+        torch.nn.functional.mse_loss(model(x), y).backward()
+        assert opt._reducer.launched_in_backward == opt._reducer.K  # all during backward
+        opt.step()
+        torch.cuda.synchronize()
+        ar = opt._arena
+        sent = {ptr: t for ptr, t in comm.log}
+        hp = c_oracle.hparams(step=1, grad_div=float(ws))
+        rng = np.random.default_rng(0)
+        gbase = opt.grad_arena().data_ptr()
+        for i, p in enumerate(params):
+            s, n = int(ar.slot[i]), int(ar.ln[i])
+            gi = sent[gbase + s * 4][:n]
+            idx = torch.from_numpy(np.unique(rng.integers(0, n, 4096))).to(gpu)
+            master = init[s:s + n][idx].cpu().numpy().copy()
+            gs = gi[idx].cpu().numpy().copy()
+            c_oracle.adam_f32(master, gs, np.zeros(len(idx), np.float32), np.zeros(len(idx), np.float32), hp)
+            got = p.detach().reshape(-1)[idx].cpu().numpy()
+            assert np.array_equal(got.view(np.uint32), master.view(np.uint32)), i
+    finally:
+        dist.destroy_process_group()
+
+
+def test_c5_paramset_step_rank0_of_ws8(gpu, monkeypatch):
+    """BASELINE.json configs[4] at full size: the Llama-3.1-8B-shaped set (291 bf16 tensors, 8.03e9
+    params) as 34 hooked layer modules, rank 0 of ws=8: per-layer gathers in forward and backward,
+    synthetic full gradients reduce-scattered from the hooks, split-master Adam on the chunks.
+    Sampled chunk elements equal the C oracle's split-master Adam of (chunk gradient / 8)."""
+    import zero_amd.zero3 as z3
+    from _gloo_comm import SimRankComm
+    from oracle import c_oracle
+    from zero_amd.paramset import ParamSetModel, decoder_layer_groups
+    from zero_amd.shapes import llama31_8b_shapes
+
+    ws = 8
+    init_pg(0, 1, _port())
+    real_get = z3.get
+    monkeypatch.setattr(z3, "get", lambda what, dm=None: {"ws": ws, "rank": 0}[what]
+                        if what in ("ws", "rank") else real_get(what, dm))
+    try:
+        shapes = llama31_8b_shapes()
+        gen = torch.Generator(device=gpu).manual_seed(0)
+        params = [torch.nn.Parameter(torch.empty(s, device=gpu, dtype=torch.bfloat16).normal_(
+            0.0, 0.02, generator=gen)) for s in shapes]
+        grads = [torch.empty(s, device=gpu, dtype=torch.bfloat16).normal_(0.0, 1e-3, generator=gen)
+                 for s in shapes]
+        model = ParamSetModel(params, decoder_layer_groups(len(shapes)))
+        model.set_grad_source(grads)
+        comm = SimRankComm(ws, 0)
+        opt = z3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
+                                  comm=comm, sync=True)
+        z3.register_zero3_hooks(model, opt.param_managers)
+        init = opt._arena.P.clone()
+        x = torch.zeros(1, device=gpu, requires_grad=True)
+        model(x).sum().backward()
+        assert opt._reducer.launched_in_backward == opt._reducer.K
+        opt.step()
+        torch.cuda.synchronize()
+        # forward + backward per layer, plus the prefetch of the next iteration's first gather
+        assert opt.runtime.n_gathers == 2 * len(model.layers) + 1
+        ar = opt._arena
+        hp = c_oracle.hparams(step=1, grad_div=float(ws))
+        rng = np.random.default_rng(1)
+        for i, p in enumerate(params):
+            s, n = int(ar.slot[i]), int(ar.ln[i])
+            r0, r1, row = ar.rows[i]
+            idx = torch.from_numpy(np.unique(rng.integers(0, n, 2048))).to(gpu)
+            hi = init[s:s + n][idx].view(torch.int16).cpu().numpy().view(np.uint16).copy()
+            lo = np.zeros(len(idx), np.int16)
+            gb = grads[i].reshape(-1)[r0 * row:r0 * row + n][idx].view(torch.int16).cpu().numpy()
+            c_oracle.adam_bf16_split(hi, lo, gb.view(np.uint16).copy(), np.zeros(len(idx), np.float32),
+                                     np.zeros(len(idx), np.float32), hp)
+            got = p.detach().reshape(-1)[idx].view(torch.int16).cpu().numpy().view(np.uint16)
+            assert np.array_equal(got, hi), i
+            assert torch.equal(opt._lo[s:s + n][idx].cpu(), torch.from_numpy(lo)), i
+    finally:
+        dist.destroy_process_group()
