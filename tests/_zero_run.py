@@ -109,3 +109,36 @@ def run_backward(z, variant: int, rank: int, ws: int, device, comm=None, tol=1e-
             assert int(st["step"].item()) == int(z[f"r{rank}_state_{i}_step"])
             assert rel(st["exp_avg"].cpu().numpy(), z[key]) <= tol
     return opt
+
+
+def _shifted(i, fn, args):
+    fn(i + 1, *args)
+
+
+def spawn_ranks(fn, ws: int, args=()):
+    """Run ``fn(rank, *args)`` for every rank of a ws-rank job: rank 0 in THIS process, ranks
+    1..ws-1 spawned.  So a ws-rank GPU test puts exactly ws processes on the box's GPU (the
+    hardware schedules up to 8 processes on a device at once; a 9th — the pytest process beside
+    8 spawned ranks — over-subscribed it and stalled ws=8 runs).  A failure on any rank fails
+    the test; rank 0's failure terminates the others."""
+    import torch.multiprocessing as mp
+
+    if ws == 1:
+        fn(0, *args)
+        return
+    ctx = mp.start_processes(_shifted, args=(fn, args), nprocs=ws - 1, join=False,
+                             start_method="spawn")
+    try:
+        fn(0, *args)
+    except BaseException:
+        try:  # a spawned rank's own failure (which broke rank 0's collective) is the real error
+            ctx.join(timeout=15)
+        finally:
+            for p in ctx.processes:
+                if p.is_alive():
+                    p.terminate()
+            if dist.is_initialized():
+                dist.destroy_process_group()
+        raise
+    while not ctx.join():
+        pass

@@ -11,6 +11,12 @@ for p in (str(REPO), str(PKG), str(REPO / "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+# The multi-rank GPU tests put up to 8 ranks (+ this process) on the box's one GPU.  At HIP's
+# default of 4 hardware queues per process that is more queues than the device schedules at once;
+# an over-subscribed 8-rank run stalled with half the ranks inside a backward pass while the
+# others waited in a collective.  Two queues per process keep 9 processes within the limit (in a
+# queue shared by two streams, a wait is always behind the record it waits for, in host order).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "2")
 
 
 def free_port() -> int:
@@ -58,3 +64,14 @@ def gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU visible")
     return torch.device("cuda:0")
+
+
+@pytest.fixture(autouse=True)
+def _release_communicators():
+    """Destroy every RCCL communicator a test leaves behind (RcclComm closes itself when
+    collected; optimizer / runtime reference cycles keep it alive until a collection).  A live
+    communicator in this process stalled the 8-rank single-GPU tests spawned after it."""
+    yield
+    import gc
+
+    gc.collect()

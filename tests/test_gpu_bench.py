@@ -8,6 +8,7 @@ import sys
 import pytest
 
 from conftest import REPO, free_port
+from _zero_run import spawn_ranks
 
 pytestmark = pytest.mark.gpu
 
@@ -115,7 +116,7 @@ def test_comm_selfcheck_logic(gpu, ws):
     test-only gloo-staged one here; RCCL at N>1 in the driver's multi-GPU runs)."""
     import torch.multiprocessing as mp
 
-    mp.spawn(_selfcheck_worker, args=(ws, _port()), nprocs=ws, join=True)
+    spawn_ranks(_selfcheck_worker, ws, (ws, _port()))
 
 
 def test_comm_backends_selfcheck_ws1(gpu):

@@ -13,7 +13,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import free_port
-from _zero_run import init_pg
+from _zero_run import spawn_ranks, init_pg
 
 pytestmark = pytest.mark.gpu
 
@@ -114,4 +114,4 @@ def _mr(rank, ws, port):
 
 @pytest.mark.parametrize("ws", [2, 3])
 def test_zero3_fp8_gather_multirank(gpu, ws):
-    mp.spawn(_mr, args=(ws, _port()), nprocs=ws, join=True)
+    spawn_ranks(_mr, ws, (ws, _port()))

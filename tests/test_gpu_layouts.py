@@ -15,7 +15,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import GOLDEN, free_port
-from _zero_run import init_pg, rel
+from _zero_run import spawn_ranks, init_pg, rel
 
 pytestmark = pytest.mark.gpu
 
@@ -70,10 +70,9 @@ def test_layout_matches_reference_zero2(gpu, layout, ws, mode, buckets):
     name = f"traj_z2_ws{ws}_d16_{mode}.npz"
     if not (GOLDEN / name).exists():
         pytest.skip(f"no fixture {name}")
-    mp.spawn(_worker, args=(ws, free_port(), layout, name, buckets, 64), nprocs=ws, join=True)
+    spawn_ranks(_worker, ws, (ws, free_port(), layout, name, buckets, 64))
 
 
 def test_chunk_layout_small_windows_many_buckets(gpu):
     """Windows smaller than most chunks: every parameter's chunk is split across buckets."""
-    mp.spawn(_worker, args=(4, free_port(), "chunk", "traj_z2_ws4_d64_distinct.npz", "ragged", 64),
-             nprocs=4, join=True)
+    spawn_ranks(_worker, 4, (4, free_port(), "chunk", "traj_z2_ws4_d64_distinct.npz", "ragged", 64))

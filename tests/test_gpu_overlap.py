@@ -14,7 +14,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import GOLDEN, free_port
-from _zero_run import init_pg, run_backward
+from _zero_run import spawn_ranks, init_pg, run_backward
 
 pytestmark = pytest.mark.gpu
 
@@ -107,7 +107,7 @@ def _mr_worker(rank, ws, port, variant, name, views):
 @pytest.mark.parametrize("ws,views", [(2, True), (3, True), (3, False)])
 def test_multirank_overlap_backward(gpu, variant, ws, views):
     name = f"traj_z{variant}_ws{ws}_d16_distinct.npz"
-    mp.spawn(_mr_worker, args=(ws, _port(), variant, name, views), nprocs=ws, join=True)
+    spawn_ranks(_mr_worker, ws, (ws, _port(), variant, name, views))
 
 
 # ---------------------------------------------------------------------------------------------
@@ -170,7 +170,7 @@ def _ddp_worker(rank, ws, port, dtype_name):
 @pytest.mark.parametrize("ws", [1, 2, 3])
 @pytest.mark.parametrize("dtype_name", ["float32", "bfloat16"])
 def test_ddp_sync_gradients(gpu, ws, dtype_name):
-    mp.spawn(_ddp_worker, args=(ws, _port(), dtype_name), nprocs=ws, join=True)
+    spawn_ranks(_ddp_worker, ws, (ws, _port(), dtype_name))
 
 
 @pytest.mark.parametrize("n", [1, 7, 1000, 4099, 1 << 20])

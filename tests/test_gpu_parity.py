@@ -13,7 +13,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import GOLDEN, free_port
-from _zero_run import init_pg, rel, run_injected
+from _zero_run import spawn_ranks, init_pg, rel, run_injected
 
 pytestmark = pytest.mark.gpu
 
@@ -106,19 +106,18 @@ MR_CASES = [(v, f"traj_z{v}_ws{ws}_d16_{m}.npz") for v in (1, 2) for ws in (2, 3
 @pytest.mark.parametrize("variant,name", MR_CASES)
 def test_multirank_injected(gpu, variant, name):
     ws = int(name.split("_ws")[1].split("_")[0])
-    mp.spawn(_mr_worker, args=(ws, _port(), variant, name), nprocs=ws, join=True)
+    spawn_ranks(_mr_worker, ws, (ws, _port(), variant, name))
 
 
 @pytest.mark.parametrize("variant", [1, 2])
 def test_multirank_padded_buckets(gpu, variant):
     """The zero-padded bucket schedule (ablation) gives the same trajectory."""
-    mp.spawn(_mr_worker, args=(3, _port(), variant, f"traj_z{variant}_ws3_d16_distinct.npz", "padded"),
-             nprocs=3, join=True)
+    spawn_ranks(_mr_worker, 3, (3, _port(), variant, f"traj_z{variant}_ws3_d16_distinct.npz", "padded"))
 
 
 def test_multirank_ws8_ragged(gpu):
     """ws=8 over the 12-param MLP: most buckets are ragged (one reduce / broadcast per owner)."""
-    mp.spawn(_mr_worker, args=(8, _port(), 2, "traj_z2_ws8_d16_distinct.npz"), nprocs=8, join=True)
+    spawn_ranks(_mr_worker, 8, (8, _port(), 2, "traj_z2_ws8_d16_distinct.npz"))
 
 
 def _edge_worker(rank, ws, port, variant, buckets):
@@ -164,7 +163,7 @@ def _edge_worker(rank, ws, port, variant, buckets):
 def test_multirank_fewer_params_than_ranks(gpu, variant, buckets):
     """Edge cases of the reference's ownership rule on the device path: n < ws (empty ranks) and a
     zero-element parameter, against the oracle's restatement of the reference."""
-    mp.spawn(_edge_worker, args=(4, _port(), variant, buckets), nprocs=4, join=True)
+    spawn_ranks(_edge_worker, 4, (4, _port(), variant, buckets))
 
 
 HP_CASES = {
@@ -227,7 +226,7 @@ def _hp_worker(rank, ws, port, variant, case):
 def test_multirank_hyperparameters(gpu, variant, case):
     """AdamW / L2 weight decay / amsgrad / maximize and per-group lr through the bucketed ws=3
     path (ragged buckets included) against the oracle's restatement of the reference."""
-    mp.spawn(_hp_worker, args=(3, _port(), variant, case), nprocs=3, join=True)
+    spawn_ranks(_hp_worker, 3, (3, _port(), variant, case))
 
 
 def test_profiler_ranges_match_reference_names(gpu, pg1):

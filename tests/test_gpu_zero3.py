@@ -13,7 +13,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import GOLDEN, free_port
-from _zero_run import init_pg, rel
+from _zero_run import spawn_ranks, init_pg, rel
 
 pytestmark = pytest.mark.gpu
 
@@ -189,8 +189,13 @@ def test_ws1_update_mode_hooks(gpu, pg1):
 
 
 def _mr(rank, ws, port, fn, name):
+    import faulthandler
+    import sys
+
     from _gloo_comm import GlooStagedComm
 
+    if rank:  # spawned ranks: a hang names its line (rank 0 is the pytest process itself)
+        faulthandler.dump_traceback_later(120, exit=True, file=sys.stderr)
     torch.cuda.set_device(0)
     init_pg(rank, ws, port)
     globals()[fn](rank, ws, name, torch.device("cuda:0"), comm=GlooStagedComm())
@@ -200,25 +205,24 @@ def _mr(rank, ws, port, fn, name):
 
 @pytest.mark.parametrize("ws", [2, 4, 8])
 def test_multirank_reference_mode_hooks(gpu, ws):
-    mp.spawn(_mr, args=(ws, _port(), "_ref_mode", f"traj_z3_ws{ws}_d16_distinct.npz"), nprocs=ws)
+    spawn_ranks(_mr, ws, (ws, _port(), "_ref_mode", f"traj_z3_ws{ws}_d16_distinct.npz"))
 
 
 @pytest.mark.parametrize("ws", [2, 4, 8])
 def test_multirank_reference_mode_injected(gpu, ws):
-    mp.spawn(_mr, args=(ws, _port(), "_ref_injected", f"traj_z3_ws{ws}_d16_ref.npz"), nprocs=ws)
+    spawn_ranks(_mr, ws, (ws, _port(), "_ref_injected", f"traj_z3_ws{ws}_d16_ref.npz"))
 
 
 @pytest.mark.parametrize("ws", [2, 3, 4, 8])
 def test_multirank_update_mode(gpu, ws):
     """ws=3 exercises uneven torch.chunk (16 rows → 6,6,4), which deadlocks the reference."""
-    mp.spawn(_mr, args=(ws, _port(), "_update_injected", f"traj_z2_ws{ws}_d16_distinct.npz"),
-             nprocs=ws)
+    spawn_ranks(_mr, ws, (ws, _port(), "_update_injected", f"traj_z2_ws{ws}_d16_distinct.npz"))
 
 
 @pytest.mark.parametrize("ws,mode", [(2, "distinct"), (3, "distinct"), (4, "distinct"), (8, "ref"),
                                      (8, "distinct")])
 def test_multirank_update_mode_hooks(gpu, ws, mode):
-    mp.spawn(_mr, args=(ws, _port(), "_update_hooks", f"traj_z2_ws{ws}_d16_{mode}.npz"), nprocs=ws)
+    spawn_ranks(_mr, ws, (ws, _port(), "_update_hooks", f"traj_z2_ws{ws}_d16_{mode}.npz"))
 
 
 def _mem_worker(rank, ws, port):
@@ -255,15 +259,16 @@ def _mem_worker(rank, ws, port):
         loss.backward()
         torch.cuda.synchronize()
         peak = torch.cuda.max_memory_allocated(dev) - base
-        # one layer's full weight gathered + one full grad in flight (+ slack), never all L grads
-        assert peak <= 4 * D * D * 4 + (1 << 20), (peak, full_bytes)
+        # a gathered weight, the next one prefetched, a full grad in flight and the staging copies
+        # of one reduce-scatter — a few layers' worth, never the L full grads of DP
+        assert peak <= 5 * D * D * 4 + (1 << 20), (peak, full_bytes)
         opt.step()
     dist.barrier()
     dist.destroy_process_group()
 
 
 def test_update_mode_gradient_memory_is_sharded(gpu):
-    mp.spawn(_mem_worker, args=(4, _port()), nprocs=4)
+    spawn_ranks(_mem_worker, 4, (4, _port()))
 
 
 def test_update_mode_double_backward_raises(gpu, pg1):
