@@ -95,10 +95,12 @@ def collective_summary(events, steps, world, red_dev):
 
     acc = {}
     for kind, even, e0, e1, bus in events:
-        key = ("reduce" if kind == "rs" else "gather") + ("_even" if even else "_ragged")
+        label = even if isinstance(even, str) else ("even" if even else "ragged")
+        key = ("reduce" if kind == "rs" else "gather") + "_" + label
         ms, b, n = acc.get(key, (0.0, 0.0, 0))
         acc[key] = (ms + e0.elapsed_time(e1), b + bus, n + 1)
-    keys = ["reduce_even", "reduce_ragged", "gather_even", "gather_ragged"]
+    keys = ["reduce_even", "reduce_ragged", "reduce_flat", "gather_even", "gather_ragged",
+            "gather_flat"]
     t = torch.tensor([acc.get(k, (0.0, 0.0, 0))[0] for k in keys], dtype=torch.float64, device=red_dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     out = {"source": "HIP events around each collective on the comm stream, max over ranks",
@@ -220,6 +222,19 @@ def _teardown(opt):
         comm = getattr(opt, name, None)
         if comm is not None and hasattr(comm, "close"):
             comm.close()
+
+
+def _teardown_engine(opt):
+    """Drop an optimizer built for the arena calibration (its communicator is the bench's own,
+    shared, and stays open)."""
+    import gc
+
+    import torch
+
+    torch.cuda.synchronize()
+    opt.engine = None
+    gc.collect()
+    torch.cuda.empty_cache()
 
 
 def _checked_comm(kw, world, rank, dev):
@@ -349,6 +364,12 @@ class _NoComm:
         pass
 
     def all_reduce(self, t, stream):
+        pass
+
+    def reduce_out(self, send, recv, root, stream):
+        pass
+
+    def broadcast(self, t, root, stream):
         pass
 
 
@@ -556,6 +577,106 @@ def zero3_gather_check(opt, model, shapes, full_copies, dev, world, rank, red_de
         _fail_check("ZeRO-3 backward reduce-scatter of layer 1", rank, rs_bad)
     if not res["all_ranks_ok"]:
         _fail_check("ZeRO-3 exchange", rank, "another rank failed")
+    return res
+
+
+def _bits(t):
+    return t.reshape(-1).view(torch_int_of(t))
+
+
+def torch_int_of(t):
+    import torch
+
+    return {2: torch.int16, 4: torch.int32}[t.element_size()]
+
+
+def _adam_step1_restated(master, gsum, world, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8):
+    """torch.optim.Adam's first step (adam.py:457-547, fresh state) in fp32 torch ops, in the
+    fused kernel's rounding order: g = sum / ws; m = (1-b1)*g (lerp from 0); v = ((1-b2)*g)*g;
+    p += (-(lr/bc1) * m) / (sqrt(v)/sqrt(bc2) + eps).  A plain-PyTorch restatement for the
+    bench's exchange check (the C oracle stays in tests/)."""
+    import math
+
+    import torch
+
+    f = lambda x: torch.tensor(x, dtype=torch.float32, device=master.device)  # noqa: E731
+    g = gsum.float() / f(float(world))
+    m = f(1.0 - b1) * g
+    v = (f(1.0 - b2) * g) * g
+    denom = torch.sqrt(v) / f(math.sqrt(1.0 - b2)) + f(eps)
+    return master.float() + (f(-(lr / (1.0 - b1))) * m) / denom
+
+
+def zero12_exchange_check(opt, step, params, shapes, dev, world, rank, red_dev):
+    """Before timing at N>1: ONE real engine step on the real arena and communicator, with the
+    bench's known per-rank synthetic grads (seed = rank).  Checks, on every rank:
+      (1) the reduced gradient of every owned parameter (captured right after the reduce) equals
+          the exact fp32 sum of all ranks' grads within the ring bound ws·2^-8·Σ|g_r| (bf16; fp32:
+          ws·2^-22·Σ|g_r|);
+      (2) the owned parameters after the step equal the plain-PyTorch restatement of Adam's first
+          step applied to that reduced gradient, within 1 bf16 ulp (fp32: 1e-6 relative);
+      (3) the all-gather / broadcast left every rank with bit-identical parameters (two checksums
+          per tensor, MIN == MAX over ranks).
+    A failure ends the run (exit 4) naming the rank and tensor."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    eng = opt.engine
+    pc = eng.pieces
+    own = [int(i) for i, n in zip(pc.param, pc.length) if n > 0]
+    so_of = {int(i): int(so) for i, so, n in zip(pc.param, pc.stream_off, pc.length) if n > 0}
+    cap = torch.zeros(max(eng.L, 1), dtype=eng.dtype, device=dev)
+    before = {i: params[i].detach().clone() for i in own}
+    eng.capture_reduced = cap
+    step()
+    torch.cuda.synchronize()
+    eng.capture_reduced = None
+    exact, absum = _regen_grads(shapes, world, dev, {i: slice(None) for i in own})
+    bf16 = eng.dtype == torch.bfloat16
+    tol = _bf16_sum_tolerance(world) if bf16 else world * 2.0 ** -22
+    worst_sum, worst_ulp, bad = 0.0, 0, []
+    for i in own:
+        n = params[i].numel()
+        got = cap[so_of[i]:so_of[i] + n]
+        ratio = float(((got.float() - exact[i]).abs() / (tol * absum[i] + 1e-30)).max())
+        worst_sum = max(worst_sum, ratio)
+        if ratio > 1.0:
+            bad.append(("reduced grad", i, ratio))
+        want = _adam_step1_restated(before[i].reshape(-1), got, world)
+        p = params[i].detach().reshape(-1)
+        if bf16:
+            d = (_bits(p).int() - _bits(want.to(torch.bfloat16)).int()).abs().max()
+            worst_ulp = max(worst_ulp, int(d))
+            if int(d) > 1:
+                bad.append(("adam update (bf16 ulp)", i, int(d)))
+        else:
+            r = float((p - want).abs().max() / want.abs().max().clamp_min(1e-30))
+            if r > 1e-6:
+                bad.append(("adam update (rel)", i, r))
+    sums = []
+    for p in params:
+        b = _bits(p.detach()).long()
+        sums += [int(b.sum()), int((b * torch.arange(1, b.numel() + 1, device=dev) % 65521).sum())]
+    t = torch.tensor(sums, dtype=torch.int64, device=red_dev)
+    lo, hi = t.clone(), t.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    diverged = sorted(set(int(k) // 2 for k in np.nonzero((lo != hi).cpu().numpy())[0]))
+    ok = torch.tensor([0.0 if (bad or diverged) else 1.0], device=red_dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    res = {"arena": getattr(eng, "arena_kind", "buckets"), "owned_tensors": len(own),
+           "reduce_max_err_over_bound": worst_sum,
+           "reduce_bound": (f"|sum - exact fp32 sum| <= {world} * 2^-8 * sum_r |g_r| (bf16 ring: one "
+                            "rounding per hop)") if bf16 else f"{world} * 2^-22 * sum_r |g_r|",
+           "adam_max_bf16_ulp" if bf16 else "adam_rel_tol": worst_ulp if bf16 else 1e-6,
+           "params_identical_across_ranks": not diverged, "all_ranks_ok": bool(ok.item() == 1.0)}
+    if bad:
+        _fail_check("ZeRO step exchange", rank, bad[:8])
+    if diverged:
+        _fail_check("ZeRO step parameter broadcast", rank, f"tensors {diverged[:8]} differ across ranks")
+    if not res["all_ranks_ok"]:
+        _fail_check("ZeRO step exchange", rank, "another rank failed")
     return res
 
 
@@ -785,6 +906,11 @@ def main():
                          "ZeRO-1/2); chunk = dim-0 chunks of every param (zero3.py:107-108, forced "
                          "by --zero 3 on C4/C5); flat = balanced 1/N slices (ablation)")
     ap.add_argument("--bucket-mb", type=float, default=256.0)
+    ap.add_argument("--arena", default="auto", choices=["auto", "flat", "buckets"],
+                    help="ZeRO-1/2 exchange at N>1: flat = params and grads are views of one "
+                         "owner-major arena, grouped reduce / broadcast rounds, no pack / unpack; "
+                         "buckets = rank-major bucket arena, pack / RS / AG / unpack; auto = "
+                         "calibrate both after their exchange checks and time the faster")
     ap.add_argument("--buckets", default="ragged", choices=["ragged", "padded"],
                     help="ragged: equal-count RS/AG over the shortest stream + one grouped "
                          "reduce/broadcast per owner for the rest; padded: every window padded")
@@ -888,14 +1014,68 @@ def main():
         _phase("communicator self-check")
         selfcheck = _checked_comm(kw, world, rank, dev)
         comm_used = selfcheck.pop("comm_used", comm_used)
-    opt = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), layout=args.layout,
-                               bucket_mb=args.bucket_mb, sync=False, buckets=args.buckets,
-                               master=args.master, **kw)
+    red_dev = dev if use_nccl else "cpu"
+    multi = world > 1 or args.simulate_ws > 1
+    arenas = ["flat", "buckets"] if (args.arena == "auto" and multi) else \
+        [args.arena if args.arena != "auto" else "flat"]
 
-    def step():
-        for p, g in zip(params, grads):
-            p.grad = g
-        opt.step()
+    def build(arena):
+        o = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), layout=args.layout,
+                                 bucket_mb=args.bucket_mb, sync=False, buckets=args.buckets,
+                                 master=args.master, arena=arena, **kw)
+        if getattr(o.engine, "arena_kind", None) == "flat":
+            # grads resident in HBM where a backward puts them: in the arena's grad views
+            o.zero_grad()
+            with torch.no_grad():
+                for p, g in zip(params, grads):
+                    p.grad.copy_(g)
+
+            def st():
+                o.step()
+        else:
+            def st():
+                for p, g in zip(params, grads):
+                    p.grad = g
+                o.step()
+        return o, st
+
+    def timed(st, n):
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            st()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=red_dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()) / n * 1e3
+
+    exchange_check, arena_ab = {}, {}
+    opt = step = None
+    for arena in arenas:
+        if opt is not None:
+            _teardown_engine(opt)
+            opt = step = None
+        opt, step = build(arena)
+        kind = getattr(opt.engine, "arena_kind", "buckets") if opt.engine is not None else arena
+        if world > 1:
+            _phase(f"exchange check ({kind} arena)")
+            exchange_check[kind] = zero12_exchange_check(opt, step, params, shapes, dev, world, rank,
+                                                         red_dev)
+        if len(arenas) > 1:  # calibrate: the same step through each exchange, the faster is timed
+            _phase(f"arena calibration ({kind})")
+            for _ in range(args.warmup):
+                step()
+            arena_ab[kind] = timed(step, max(3, min(args.steps, 5)))
+    if len(arenas) > 1:
+        best = min(arena_ab, key=arena_ab.get)
+        if best != arenas[-1]:
+            _teardown_engine(opt)
+            opt, step = build(best)
+    arena_used = getattr(opt.engine, "arena_kind", "buckets") if opt.engine is not None else arenas[0]
 
     _phase("warmup")
     for _ in range(args.warmup):
@@ -919,7 +1099,6 @@ def main():
     eng.timing_events = None
     comm_events, eng.comm_events = eng.comm_events, None
     copy_events, eng.copy_events = eng.copy_events, None
-    red_dev = dev if use_nccl else "cpu"
     el_t = torch.tensor([el], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
@@ -971,7 +1150,8 @@ def main():
         collectives = collective_summary(comm_events, args.steps, world, red_dev)
         if args.comm in ("rccl", "c10d") and not args.no_comm_sweep:
             _phase("bucket-size sweep")
-            collectives["sweep"] = comm_sweep(opt._comm, eng.arena, world, red_dev)
+            sweep_buf = eng.arena if getattr(eng, "arena", None) is not None else eng.R
+            collectives["sweep"] = comm_sweep(opt._comm, sweep_buf, world, red_dev)
 
     if rank == 0 and args.simulate_ws > 1:
         print(json.dumps({"diagnostic": f"simulate-ws {args.simulate_ws}: rank-0 compute of the "
@@ -1012,6 +1192,7 @@ def main():
                 "zero": args.zero, "layout": args.layout, "bucket_mb": args.bucket_mb,
                 "bucket_mode": args.buckets,
                 "buckets": eng.K, "parallelism": f"dp{world}", "comm": comm_used,
+                "arena": arena_used,
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -1027,6 +1208,12 @@ def main():
                             "arena": getattr(eng, "arena_placement", None)}
         if selfcheck is not None:
             out["rccl_selfcheck"] = selfcheck
+        if exchange_check:
+            out["exchange_check"] = exchange_check[arena_used] if arena_used in exchange_check \
+                else exchange_check
+            out["exchange_check_all_arenas"] = exchange_check
+        if arena_ab:
+            out["arena_calibration_ms_per_step"] = arena_ab
         out["host_enqueue_ms_per_step"] = host_ms  # rank 0's Python + launch time per step
         if collectives is not None:
             out["collectives"] = collectives

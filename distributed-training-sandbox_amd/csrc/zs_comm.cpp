@@ -150,6 +150,68 @@ int zs_broadcast(zs_comm* c, const void* send, void* recv, int64_t count, int dt
   return ZS_OK;
 }
 
+// One RCCL group of n reduces / in-place broadcasts: the reduce-scatter-v and all-gather-v of a
+// flat-arena round (each owner's contiguous window reduced to it, then broadcast from it).  One
+// call per round instead of one per owner; the group launches every transfer together, so each
+// rank is the root of one and forwards for the others.
+int zs_reduce_group(zs_comm* c, int64_t n, const uint64_t* send, const uint64_t* recv,
+                    const int64_t* count, const int32_t* root, int dtype, uintptr_t stream) {
+  ZS_REQUIRE(c && c->comm, "zs_reduce_group: NULL communicator");
+  ZS_REQUIRE(n >= 0 && (n == 0 || (send && recv && count && root)), "zs_reduce_group: bad table");
+  ncclDataType_t t;
+  int rc = to_nccl(dtype, &t);
+  if (rc) return rc;
+  for (int64_t i = 0; i < n; ++i) {
+    ZS_REQUIRE(count[i] >= 0 && root[i] >= 0 && root[i] < c->ws,
+               "zs_reduce_group: entry %lld: count %lld root %d", (long long)i,
+               (long long)count[i], root[i]);
+    ZS_REQUIRE(count[i] == 0 || (send[i] && (recv[i] || root[i] != c->rank)),
+               "zs_reduce_group: entry %lld: NULL buffer", (long long)i);
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  ZS_NCCL(ncclGroupStart());
+  for (int64_t i = 0; i < n; ++i) {
+    if (count[i] == 0) continue;
+    ncclResult_t r = ncclReduce(reinterpret_cast<const void*>(send[i]),
+                                reinterpret_cast<void*>(recv[i]), size_t(count[i]), t, ncclSum,
+                                root[i], c->comm, st);
+    if (r != ncclSuccess) {
+      (void)ncclGroupEnd();
+      return zs::fail(ZS_ERR_RCCL, "ncclReduce (group entry %lld) failed: %s", (long long)i,
+                      ncclGetErrorString(r));
+    }
+  }
+  ZS_NCCL(ncclGroupEnd());
+  return ZS_OK;
+}
+
+int zs_broadcast_group(zs_comm* c, int64_t n, const uint64_t* buf, const int64_t* count,
+                       const int32_t* root, int dtype, uintptr_t stream) {
+  ZS_REQUIRE(c && c->comm, "zs_broadcast_group: NULL communicator");
+  ZS_REQUIRE(n >= 0 && (n == 0 || (buf && count && root)), "zs_broadcast_group: bad table");
+  ncclDataType_t t;
+  int rc = to_nccl(dtype, &t);
+  if (rc) return rc;
+  for (int64_t i = 0; i < n; ++i)
+    ZS_REQUIRE(count[i] >= 0 && root[i] >= 0 && root[i] < c->ws && (count[i] == 0 || buf[i]),
+               "zs_broadcast_group: entry %lld: count %lld root %d", (long long)i,
+               (long long)count[i], root[i]);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  ZS_NCCL(ncclGroupStart());
+  for (int64_t i = 0; i < n; ++i) {
+    if (count[i] == 0) continue;
+    void* p = reinterpret_cast<void*>(buf[i]);
+    ncclResult_t r = ncclBroadcast(p, p, size_t(count[i]), t, root[i], c->comm, st);
+    if (r != ncclSuccess) {
+      (void)ncclGroupEnd();
+      return zs::fail(ZS_ERR_RCCL, "ncclBroadcast (group entry %lld) failed: %s", (long long)i,
+                      ncclGetErrorString(r));
+    }
+  }
+  ZS_NCCL(ncclGroupEnd());
+  return ZS_OK;
+}
+
 int zs_group_start(void) {
   ZS_NCCL(ncclGroupStart());
   return ZS_OK;

@@ -40,7 +40,8 @@ class ShardedOptimizerBase:
 
     def __init__(self, optimizer: Optimizer, *, layout: str = "reference",
                  bucket_mb: float = 256.0, comm=None, sync: bool = True, buckets: str = "ragged",
-                 overlap: bool = False, overlap_bucket_mb: float = 64.0, master: str = "split"):
+                 overlap: bool = False, overlap_bucket_mb: float = 64.0, master: str = "split",
+                 arena: str = "flat"):
         if not isinstance(optimizer, torch.optim.Adam):
             raise TypeError("zero_amd ShardedOptimizer wraps torch.optim.Adam / AdamW "
                             f"(got {type(optimizer).__name__})")
@@ -73,6 +74,12 @@ class ShardedOptimizerBase:
         self._comm = comm
         self._sync = sync
         self._master = master  # bf16 params: "split" (bf16 param + int16 residual) or "fp32"
+        if arena not in ("flat", "buckets"):
+            raise ValueError(f"arena must be 'flat' or 'buckets' (got {arena!r})")
+        # ws > 1 exchange: "flat" = params and grads are views of one owner-major arena, rounds of
+        # grouped reduce / broadcast, no pack / unpack (flat.py); "buckets" = the rank-major
+        # bucket arena with pack / reduce-scatter / all-gather / unpack (engine.py)
+        self._arena = arena
         self.engine: ShardEngine | None = None
         self._step_tensors = {}
         self._overlap = bool(overlap)
@@ -83,6 +90,14 @@ class ShardedOptimizerBase:
             self._build_engine()
             gb = self.engine.enable_overlap(int(overlap_bucket_mb * (1 << 20)))
             self._overlap_hooks = gb.register_hooks()
+        elif self._flat():
+            # params become views of the arena now, so zero_grad() can hand out grad views
+            # before the first step (every rank builds it: the communicator is a collective)
+            self._build_engine()
+
+    def _flat(self) -> bool:
+        return (self._arena == "flat" and self.world_size > 1 and not self._overlap
+                and self._layout == "reference")
 
     def _shard_optimizer_params(self):
         """zero1.py:71-74: drop non-owned params from the inner optimizer's groups."""
@@ -96,13 +111,20 @@ class ShardedOptimizerBase:
             from .comm import RcclComm
             comm = RcclComm()
             self._comm = comm
-        self.engine = ShardEngine(self.params, self._group_of, self.world_size, self.rank,
-                                  # ws=1 owns every param, so zero_grad clears them all and
-                                  # there is no carry (zero1.py:107-108): no buffer, no 0·A term
-                                  layout=self._layout, carry=self._carry and self.world_size > 1,
-                                  comm=comm,
-                                  bucket_bytes=self._bucket_bytes, buckets=self._buckets,
-                                  master=self._master)
+        # ws=1 owns every param, so zero_grad clears them all and there is no carry
+        # (zero1.py:107-108): no buffer, no 0·A term
+        carry = self._carry and self.world_size > 1
+        if self._flat():
+            from .flat import FlatEngine
+
+            self.engine = FlatEngine(self.params, self._group_of, self.world_size, self.rank,
+                                     carry=carry, comm=comm, bucket_bytes=self._bucket_bytes,
+                                     master=self._master)
+        else:
+            self.engine = ShardEngine(self.params, self._group_of, self.world_size, self.rank,
+                                      layout=self._layout, carry=carry, comm=comm,
+                                      bucket_bytes=self._bucket_bytes, buckets=self._buckets,
+                                      master=self._master)
         if self.engine.plan.layout != 0:
             return
         self._expose_state()
@@ -161,7 +183,8 @@ class ShardedOptimizerBase:
         self._release_grads()
         if self._sync:
             torch.cuda.synchronize(self.engine.device)
-            self.communication_time += self.engine.comm_time_s()
+            if self._variant != 1:  # zero1.py:67-68: ZeRO-1 never counts communication time
+                self.communication_time += self.engine.comm_time_s()
             self.engine.release_retired()
         elif self.engine.n_retired() > 64:
             torch.cuda.synchronize(self.engine.device)
@@ -171,7 +194,10 @@ class ShardedOptimizerBase:
 
     def _release_grads(self):
         # zero2.py:113 frees non-owned grads; the reduced grads live in the bucket arena, so
-        # every grad is released (the next backward allocates fresh ones).
+        # every grad is released (the next backward allocates fresh ones).  The flat arena keeps
+        # every p.grad as its view of G (this rank's local gradient).
+        if self._flat():
+            return
         if self._overlap:
             self.engine.gb.release()
             return
@@ -181,6 +207,9 @@ class ShardedOptimizerBase:
     def zero_grad(self, set_to_none: bool = True):
         if self._overlap:  # grads become zeroed views of the overlap buckets (no pack copy)
             self.engine.gb.install_views()
+            return
+        if self._flat():  # zeroed views of the grad arena (backward accumulates in place)
+            self.engine.zero_grad()
             return
         for p in self.params:
             if p.grad is not None:

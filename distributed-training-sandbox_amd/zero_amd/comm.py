@@ -125,6 +125,31 @@ class RcclComm:
         _lib.call("zs_all_reduce", self._h, t.data_ptr(), t.data_ptr(), t.numel(),
                   zs_dtype(t.dtype), stream_handle(stream))
 
+    def reduce_out(self, send: torch.Tensor, recv: torch.Tensor, root: int, stream) -> None:
+        """SUM-reduce ``send`` into ``recv`` on ``root`` (recv untouched elsewhere)."""
+        _lib.call("zs_reduce", self._h, send.data_ptr(), recv.data_ptr(), send.numel(),
+                  zs_dtype(send.dtype), int(root), stream_handle(stream))
+
+    def reduce_group(self, send, recv, count, root, dtype: int, stream) -> None:
+        """One RCCL group of reduces from device-pointer tables (flat-arena rounds): entry i sums
+        ``count[i]`` elements at ``send[i]`` into ``recv[i]`` on rank ``root[i]``."""
+        n = len(count)
+        _lib.call("zs_reduce_group", self._h, n, send.ctypes.data_as(_PU64), recv.ctypes.data_as(_PU64),
+                  count.ctypes.data_as(_PI64), root.ctypes.data_as(_PI32), int(dtype),
+                  stream_handle(stream))
+
+    def broadcast_group(self, buf, count, root, dtype: int, stream) -> None:
+        """One RCCL group of in-place broadcasts: ``count[i]`` elements at ``buf[i]`` from
+        ``root[i]``."""
+        _lib.call("zs_broadcast_group", self._h, len(count), buf.ctypes.data_as(_PU64),
+                  count.ctypes.data_as(_PI64), root.ctypes.data_as(_PI32), int(dtype),
+                  stream_handle(stream))
+
+
+_PU64 = ctypes.POINTER(ctypes.c_uint64)
+_PI64 = ctypes.POINTER(ctypes.c_int64)
+_PI32 = ctypes.POINTER(ctypes.c_int32)
+
 
 class C10dComm:
     """The same interface over torch.distributed's own communicator of ``group`` (RCCL under the
@@ -170,6 +195,15 @@ class C10dComm:
     def broadcast(self, t, root, stream):
         with torch.cuda.stream(stream):
             dist.broadcast(t, src=self._root(root), group=self.group_)
+
+    def reduce_out(self, send, recv, root, stream):
+        with torch.cuda.stream(stream):
+            if root == self.rank:
+                if recv.data_ptr() != send.data_ptr():
+                    recv.copy_(send)
+                dist.reduce(recv, dst=self._root(root), group=self.group_)
+            else:  # c10d's reduce is in place; a non-root's buffer is only read (ncclReduce)
+                dist.reduce(send, dst=self._root(root), group=self.group_)
 
     def reduce_v(self, buf, win_off, win_len, stream):
         for root, (off, n) in enumerate(zip(win_off, win_len)):

@@ -163,6 +163,7 @@ class ShardEngine:
         self.timing_events = None  # optional list of (start, end) events around each Adam launch
         self.comm_events = None    # optional list of (kind, even, start, end, bus_bytes) per collective
         self.copy_events = None    # optional list of (kind, start, end, bytes) per pack / unpack
+        self.capture_reduced = None  # optional tensor (stream-long): the reduced grads, for checks
         self.last_adam_bytes = 0
 
     # ------------------------------------------------------------------------------------------
@@ -245,15 +246,20 @@ class ShardEngine:
         mst = np.uint64(self.master.data_ptr()) + so64 * np.uint64(4)
         return self._adam_rows(idx, g, mst, mst, p_out, so, n)
 
-    def _run_adam(self, tag, rows, param_idx, hparams_of, stream):
-        """Partition rows by (group, step) — torch's bias correction is per param — and launch."""
+    def _run_adam(self, tag, rows, param_idx, hparams_of, stream, carry_mul=None):
+        """Partition rows by (group, step, carry multiplier) — torch's bias correction is per param,
+        and the ZeRO-1 carry weight depends on which grads survived since the last step — and
+        launch one fused-Adam set per part."""
         if len(rows) == 0:
             return
-        keys = np.stack([np.asarray(self.group_of)[param_idx], self.steps[param_idx]], axis=1)
+        if carry_mul is None:
+            carry_mul = np.full(len(param_idx), self.ws - 1 if self.carry is not None else 0, np.int64)
+        keys = np.stack([np.asarray(self.group_of)[param_idx], self.steps[param_idx],
+                         np.asarray(carry_mul, np.int64)], axis=1)
         for key in np.unique(keys, axis=0):
             sel = np.nonzero((keys == key).all(axis=1))[0]
             sub = np.ascontiguousarray(rows[sel])
-            gidx, step = int(key[0]), int(key[1])
+            gidx, step, cmul = int(key[0]), int(key[1]), int(key[2])
             aset = self._cached(("adam", tag, gidx, len(sel), int(sel[0])), sub.tobytes(),
                                 lambda: AdamSet(sub, self.zdtype, self.p_dtype))
             hpd = hparams_of(gidx)
@@ -263,7 +269,7 @@ class ShardEngine:
                               hpd["weight_decay"], step, decoupled=hpd["decoupled"],
                               amsgrad=hpd["amsgrad"], maximize=hpd["maximize"],
                               grad_div=float(self.ws),
-                              carry_mul=float(self.ws - 1) if self.carry is not None else 0.0)
+                              carry_mul=float(cmul) if self.carry is not None else 0.0)
             if self.timing_events is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
@@ -354,6 +360,10 @@ class ShardEngine:
             else:
                 self.comm.broadcast_v(buf, b.win_off, b.win_len, cs)
             bus = int(b.win_len.sum()) * self.es  # reduce / broadcast bus bytes = message bytes
+        if kind == "rs" and self.capture_reduced is not None and int(b.win_len[r]):
+            o, n, so = int(b.win_off[r]), int(b.win_len[r]), int(b.win_stream[r])
+            with torch.cuda.stream(cs):  # this rank's reduced window, in stream order
+                self.capture_reduced[so:so + n].copy_(buf[o:o + n])
         if self.comm_events is not None:
             e1.record(cs)
             self.comm_events.append((kind, bool(b.even), e0, e1, bus))
@@ -367,7 +377,7 @@ class ShardEngine:
         base = np.uint64(self.arena.data_ptr())
         r = self.rank
         cs = self.comm_stream
-        self.ev_c0.record(cs)
+        self.ev_c0.record(stream)  # communication_time: step entry → last gradient reduction
         with _lib.phase_range("all_reduce_gradients"):  # zero1.py:80-84: pack + reduce-scatter
             for k in range(self.K):  # pack every bucket on the compute stream
                 s, b = self.segs[k], self.buckets[k]
@@ -382,6 +392,7 @@ class ShardEngine:
                 cs.wait_event(self.ev_pack[k])
                 self._collective(k, "rs")
                 self.ev_rs[k].record(cs)
+            self.ev_c1.record(cs)
         with _lib.phase_range("optimizer_step"):  # zero1.py:88
             for k in range(self.K):  # fused Adam on this rank's window
                 stream.wait_event(self.ev_rs[k])
@@ -411,7 +422,6 @@ class ShardEngine:
                 cs.wait_event(self.ev_adam[k])
                 self._collective(k, "ag")
                 self.ev_ag[k].record(cs)
-            self.ev_c1.record(cs)
             for k in range(self.K):  # scatter every bucket back into module storage
                 stream.wait_event(self.ev_ag[k])
                 s, b = self.segs[k], self.buckets[k]
@@ -452,9 +462,11 @@ class ShardEngine:
 
     def _step_overlap(self, has, hparams_of, stream):
         gb, r, es = self.gb, self.rank, np.uint64(self.es)
+        cs = gb.comm_stream
+        self.ev_c0.record(stream)  # communication_time: step entry → last gradient reduction
         with _lib.phase_range("all_reduce_gradients"):  # zero1.py:80-84: reduces left by backward
             gb.flush()
-        cs = gb.comm_stream
+        self.ev_c1.record(cs)
         base = np.uint64(gb.buf.data_ptr())
         with _lib.phase_range("optimizer_step"):  # zero1.py:88
             for k in range(gb.K):  # fused Adam on the owned buckets, reading the reduced grads
@@ -485,7 +497,6 @@ class ShardEngine:
                 self.ev_oadam[k].record(stream)
         with _lib.phase_range("broadcast_parameters"):  # zero1.py:91-102: broadcast + unpack
             if self.ws > 1:
-                self.ev_c0.record(cs)
                 for k in range(gb.K):  # every rank, same order: broadcast each bucket from its owner
                     cs.wait_event(self.ev_oadam[k] if gb.key[k] == r else gb.ev_done[k])
                     region = gb.region(k)
@@ -498,7 +509,6 @@ class ShardEngine:
                         e1.record(cs)
                         self.comm_events.append(("ag", False, e0, e1, region.numel() * self.es))
                     self.ev_obc[k].record(cs)
-                self.ev_c1.record(cs)
             for k in range(gb.K if self.ws > 1 else 0):  # unpack updated params into module storage
                 stream.wait_event(self.ev_obc[k])
                 g = gb.groups[k]
@@ -510,8 +520,9 @@ class ShardEngine:
         gb.reset()
 
     def comm_time_s(self) -> float:
-        """Seconds between the first reduce-scatter and the last all-gather of the last step
-        (valid after a synchronize)."""
+        """The reference's communication_time of the last step (zero2.py:92,116): from step()
+        entry until the gradient reduction is done, on the device clock (valid after a
+        synchronize; 0 when backward had already finished the reductions)."""
         if self.ws == 1:
             return 0.0
-        return self.ev_c0.elapsed_time(self.ev_c1) / 1e3
+        return max(0.0, self.ev_c0.elapsed_time(self.ev_c1) / 1e3)

@@ -1,0 +1,288 @@
+"""The flat-parameter-arena ZeRO-1/2 step (ws > 1): no pack, no unpack.
+
+``ShardEngine``'s bucket path copies every gradient into a rank-major bucket arena (pack), runs
+the collectives there and copies every parameter back (unpack): at the ws=8 SmolLM3-3B layout
+those copies were 24.6 GB of HBM traffic per step, more than the Adam update itself
+(profiles/r01_c4_sim8_diagnostic.json).  They exist only because parameters and gradients live
+outside the arena.  ``FlatEngine`` moves them in:
+
+* **P** — every parameter is a view of one flat buffer (``param.data`` re-pointed once, at
+  construction, like an FSDP flat parameter), laid out *owner-major*: the reference's ownership
+  assigns rank r the contiguous index range [start_r, end_r) (zero1.py:55-62), so rank r's
+  parameters — its optimizer shard, its *stream* — are one contiguous region of P, each slot
+  64-element aligned;
+* **G** — the gradients, the same layout; ``zero_grad()`` zeroes G and makes every ``p.grad`` a
+  view of its slot, so backward accumulates straight into it;
+* **R** — this rank's reduced gradient, one stream long.
+
+A step is cut into *rounds*; round j is window j (``W`` elements) of every owner's stream.  Per
+round: one RCCL group of ``ncclReduce`` — owner r's window of G, summed over ranks, into R on r
+(the reduce-scatter-v, zero2.py:94-113) — the fused Adam on the own window (reads R and the
+master, writes the updated bf16 / fp32 parameter straight into P), and one RCCL group of in-place
+``ncclBroadcast`` of every owner's window of P (the all-gather-v, zero2.py:122-133).  In a group
+each rank is the root of one transfer and forwards the others', so the bus bytes per rank are
+those of a ring reduce-scatter / all-gather of the round.  The reduce is out of place, so G still
+holds this rank's local gradients after the step.
+
+ZeRO-1's gradient carry (zero1.py:107-108) follows the grads the caller left:
+the reference's non-owners keep last step's averaged gradient A_{t-1} in ``p.grad`` unless the
+caller clears it.  Here A_{t-1} lives in the owner's carry buffer, and the owner weights it by
+(ws-1) when ``p.grad`` at step() is still the arena view (cleared only by ``opt.zero_grad()``,
+which in the reference clears owned grads only) and by 0 when the caller replaced the grad (e.g.
+``model.zero_grad()`` → None → a fresh tensor from backward), per parameter, on the assumption
+that every rank treats its grads alike.  Zeroing a view in place
+(``model.zero_grad(set_to_none=False)``) cannot be told apart from ``opt.zero_grad()``.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from .engine import ALIGN_ELEMS, ShardEngine, _ptr
+from .kernels import CopySet
+
+_I32P = np.int32
+
+
+class _Round:
+    """Round j: per owner the window [lo, hi) of its stream and the device pointers of its
+    reduce / broadcast; this rank's Adam rows for the window."""
+
+    def __init__(self, j, send, recv, count, bcast, rows, idx):
+        self.j = j
+        self.send = np.ascontiguousarray(send, np.uint64)
+        self.recv = np.ascontiguousarray(recv, np.uint64)
+        self.count = np.ascontiguousarray(count, np.int64)
+        self.root = np.ascontiguousarray(np.arange(len(count)), _I32P)
+        self.bcast = np.ascontiguousarray(bcast, np.uint64)
+        self.rows = rows
+        self.idx = idx
+
+
+class FlatEngine(ShardEngine):
+    def __init__(self, params, group_of, ws: int, rank: int, *, carry=False, comm=None,
+                 bucket_bytes: int = 256 << 20, master: str = "split", placement_tries: int = 5):
+        if ws < 2:
+            raise ValueError("FlatEngine is the ws > 1 exchange; ws == 1 needs no arena")
+        # the base class gives the reference layout's streams, the optimizer state and the Adam
+        # launch machinery; its bucket plan (one bucket) is unused
+        super().__init__(params, group_of, ws, rank, layout="reference", carry=carry, comm=comm,
+                         bucket_bytes=1 << 62, buckets="ragged", placement_tries=placement_tries,
+                         master=master)
+        self.arena_kind = "flat"
+        plan, es, dev, dt = self.plan, self.es, self.device, self.dtype
+        n = len(self.params)
+        self.Ls = np.array([plan.stream_len(r) for r in range(ws)], np.int64)
+        self.base = np.concatenate([[0], np.cumsum(self.Ls)[:-1]]).astype(np.int64)
+        self.slot = np.zeros(n, np.int64)
+        self.numel = np.array([p.numel() for p in self.params], np.int64)
+        owner = np.zeros(n, np.int64)
+        for r in range(ws):
+            pc = plan.pieces(r)
+            self.slot[pc.param] = self.base[r] + pc.stream_off
+            owner[pc.param] = r
+        self.owner = owner
+        self.owned = owner == rank
+        total = int(max(self.Ls.sum(), ALIGN_ELEMS))
+        self.P, self.arena_placement = _zeros_placed(total, dt, dev, placement_tries)
+        with torch.no_grad():
+            for i, p in enumerate(self.params):
+                s = int(self.slot[i])
+                self.P[s:s + int(self.numel[i])].copy_(p.detach().reshape(-1))
+                p.data = self.P[s:s + int(self.numel[i])].view(p.shape)
+        self.G, _ = _zeros_placed(total, dt, dev, placement_tries)
+        self.R = torch.zeros(max(int(self.Ls[rank]), ALIGN_ELEMS), dtype=dt, device=dev)
+        self.dirty = np.zeros(n, bool)  # G slot may hold a stale gradient
+        self.zero_grad_calls = 0
+        W = max(ALIGN_ELEMS, (int(bucket_bytes) // (ws * es)) // ALIGN_ELEMS * ALIGN_ELEMS)
+        self.W = W
+        self.K = max(1, -(-int(self.Ls.max()) // W))
+        self.rounds = [self._make_round(j) for j in range(self.K)]
+        mk = lambda: [torch.cuda.Event() for _ in range(self.K)]  # noqa: E731
+        self.ev_red, self.ev_adam, self.ev_bc = mk(), mk(), mk()
+        self.ev_grads = torch.cuda.Event()
+        self.ev_c0 = torch.cuda.Event(enable_timing=True)
+        self.ev_c1 = torch.cuda.Event(enable_timing=True)
+        self.capture_reduced = None  # optional tensor: a copy of R after the reduces (checks)
+
+    # ------------------------------------------------------------------------------------------
+    def _make_round(self, j: int) -> _Round:
+        ws, es, W, r0 = self.ws, self.es, self.W, self.rank
+        lo = j * W
+        count = np.clip(self.Ls - lo, 0, W)
+        gb, pb, rb = self.G.data_ptr(), self.P.data_ptr(), self.R.data_ptr()
+        send = np.uint64(gb) + ((self.base + lo) * es).astype(np.uint64)
+        recv = send.copy()
+        recv[r0] = np.uint64(rb + lo * es)
+        bcast = np.uint64(pb) + ((self.base + lo) * es).astype(np.uint64)
+        # this rank's Adam rows: its pieces clipped to [lo, lo + count[rank])
+        pc = self.pieces
+        hi = lo + int(count[r0])
+        a = np.maximum(pc.stream_off, lo)
+        b = np.minimum(pc.stream_off + pc.length, hi)
+        keep = b > a
+        idx, a, b = pc.param[keep], a[keep], b[keep]
+        so = a.astype(np.int64)
+        ln = (b - a).astype(np.int64)
+        g = np.uint64(rb) + (so * es).astype(np.uint64)
+        pslot = np.uint64(pb) + ((self.base[r0] + so) * es).astype(np.uint64)
+        if self.mixed:  # master from P (split: + residual) or the fp32 master; bf16 param out to P
+            rows = self._mixed_rows(idx, g, pslot, pslot, so, ln)
+        else:  # fp32: P is the master, updated in place
+            rows = self._adam_rows(idx, g, pslot, pslot, 0, so, ln)
+        return _Round(j, send, recv, count, bcast, rows, idx)
+
+    def slot_view(self, buf: torch.Tensor, i: int) -> torch.Tensor:
+        s, n = int(self.slot[i]), int(self.numel[i])
+        return buf[s:s + n].view(self.params[i].shape)
+
+    def grad_view(self, i: int) -> torch.Tensor:
+        return self.slot_view(self.G, i)
+
+    def is_view(self, i: int, g) -> bool:
+        return (g is not None and g.data_ptr() == self.G.data_ptr() + int(self.slot[i]) * self.es
+                and g.shape == self.params[i].shape)
+
+    def install_views(self):
+        for i, p in enumerate(self.params):
+            if not self.is_view(i, p.grad):
+                p.grad = self.grad_view(i)
+
+    def zero_grad(self):
+        """The wrapper's zero_grad(): zero G and make every p.grad its arena view."""
+        self.G.zero_()
+        self.dirty[:] = False
+        self.install_views()
+        self.zero_grad_calls += 1
+
+    def rebuild_rows(self):
+        """Adam rows again (after the amsgrad buffer appeared)."""
+        self.rounds = [self._make_round(j) for j in range(self.K)]
+
+    # ------------------------------------------------------------------------------------------
+    def _reduce_round(self, rd: _Round, cs):
+        comm = self.comm
+        if hasattr(comm, "reduce_group"):
+            comm.reduce_group(rd.send, rd.recv, rd.count, rd.root, self.zdtype, cs)
+            return
+        with _group(comm):  # tensor-level fallback (test communicators)
+            for r in range(self.ws):
+                c = int(rd.count[r])
+                if c == 0:
+                    continue
+                s0 = int(self.base[r]) + rd.j * self.W
+                src = self.G[s0:s0 + c]
+                dst = self.R[rd.j * self.W:rd.j * self.W + c] if r == self.rank else src
+                comm.reduce_out(src, dst, r, cs)
+
+    def _bcast_round(self, rd: _Round, cs):
+        comm = self.comm
+        if hasattr(comm, "broadcast_group"):
+            comm.broadcast_group(rd.bcast, rd.count, rd.root, self.zdtype, cs)
+            return
+        with _group(comm):
+            for r in range(self.ws):
+                c = int(rd.count[r])
+                if c:
+                    s0 = int(self.base[r]) + rd.j * self.W
+                    comm.broadcast(self.P[s0:s0 + c], r, cs)
+
+    def step(self, grads, hparams_of, stream=None):
+        stream = torch.cuda.current_stream(self.device) if stream is None else stream
+        n = len(self.params)
+        es = self.es
+        has = np.fromiter((g is not None for g in grads), bool, n)
+        view = np.fromiter((self.is_view(i, g) for i, g in enumerate(grads)), bool, n)
+        if any(hparams_of(g)["amsgrad"] for g in set(self.group_of)) and self.vmax is None:
+            self.ensure_vmax()
+            self.rebuild_rows()
+        self.ev_c0.record(stream)
+        # gradients not accumulated into the arena (assigned tensors, fresh grads after the caller
+        # cleared the views) are copied in; a stale slot whose grad is gone is zero-filled
+        copy = np.nonzero(has & ~view)[0]
+        zero = np.nonzero(~has & self.dirty)[0]
+        if len(copy) or len(zero):
+            src = np.concatenate([np.fromiter((_ptr(grads[i]) for i in copy), np.uint64, len(copy)),
+                                  np.zeros(len(zero), np.uint64)])
+            idx = np.concatenate([copy, zero]).astype(np.int64)
+            dst = np.uint64(self.G.data_ptr()) + (self.slot[idx] * es).astype(np.uint64)
+            nb = self.numel[idx] * es
+            cs_ = self._cached(("gcopy",), src.tobytes() + dst.tobytes(), lambda: CopySet(src, dst, nb))
+            self._run_copy("pack", cs_, stream)
+        self.dirty = has.copy()
+        # ZeRO-1: the carry weight per owned param (see the module docstring)
+        cmul = np.where(view, self.ws - 1, 0).astype(np.int64)
+        self.steps[self.owned & has] += 1
+        self.last_adam_bytes = 0
+        self.ev_grads.record(stream)
+        cs = self.comm_stream
+        cs.wait_event(self.ev_grads)
+        with _lib.phase_range("all_reduce_gradients"):  # zero1.py:80-84 / zero2.py:94-113
+            for rd in self.rounds:
+                e0 = self._timed_start(cs)
+                self._reduce_round(rd, cs)
+                self.ev_red[rd.j].record(cs)
+                self._timed_end(e0, cs, "rs", int(rd.count.sum()))
+            self.ev_c1.record(cs)
+            if self.capture_reduced is not None:
+                with torch.cuda.stream(cs):
+                    self.capture_reduced.copy_(self.R[:self.capture_reduced.numel()])
+        with _lib.phase_range("optimizer_step"):  # zero1.py:88
+            for rd in self.rounds:
+                stream.wait_event(self.ev_red[rd.j])
+                if len(rd.idx):
+                    live = has[rd.idx]
+                    rows, idx = (rd.rows, rd.idx) if live.all() else (rd.rows[live], rd.idx[live])
+                    self._run_adam(("flat", rd.j), rows, idx, hparams_of, stream,
+                                   carry_mul=cmul[idx])
+                self.ev_adam[rd.j].record(stream)
+        with _lib.phase_range("broadcast_parameters"):  # zero1.py:91-102
+            for rd in self.rounds:
+                cs.wait_event(self.ev_adam[rd.j])
+                e0 = self._timed_start(cs)
+                self._bcast_round(rd, cs)
+                self.ev_bc[rd.j].record(cs)
+                self._timed_end(e0, cs, "ag", int(rd.count.sum()))
+        stream.wait_event(self.ev_bc[self.K - 1])  # the parameters are P: next forward reads it
+        # every p.grad is (again) its arena view, holding this step's local gradient
+        for i in np.nonzero(has & ~view)[0]:
+            self.params[i].grad = self.grad_view(int(i))
+
+    def _timed_start(self, cs):
+        if self.comm_events is None:
+            return None
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record(cs)
+        return e0
+
+    def _timed_end(self, e0, cs, kind, elems):
+        if e0 is None:
+            return
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record(cs)
+        # bus bytes of the round as a ring reduce-scatter / all-gather of all owners' windows
+        self.comm_events.append((kind, "flat", e0, e1, elems * self.es * (self.ws - 1) / self.ws))
+
+    def comm_time_s(self) -> float:
+        """zero2.py:92,116: from step() entry until the gradient reduction is done."""
+        return max(0.0, self.ev_c0.elapsed_time(self.ev_c1) / 1e3)
+
+
+class _nullgroup:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def _group(comm):
+    grp = getattr(comm, "group", None)
+    return grp() if grp is not None else _nullgroup()
+
+
+def _zeros_placed(n, dtype, device, tries):
+    from .engine import probed_zeros
+
+    return probed_zeros(n, dtype, device, tries)

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ZS_ABI_VERSION 4
+#define ZS_ABI_VERSION 5
 
 enum zs_status {
   ZS_OK = 0,
@@ -263,6 +263,15 @@ int zs_reduce(zs_comm* comm, const void* send, void* recv, int64_t count, int dt
               uintptr_t stream);
 int zs_broadcast(zs_comm* comm, const void* send, void* recv, int64_t count, int dtype, int root,
                  uintptr_t stream);
+/* One RCCL group of n SUM-reduces (entry i: send[i] -> recv[i] on root[i], count[i] elements;
+ * recv[i] is only written on its root and may equal send[i]) or of n in-place broadcasts
+ * (buf[i] from root[i]).  The reduce-scatter-v / all-gather-v of one round of the flat
+ * parameter arena: each owner's contiguous window reduced to it (zero2.py:94-113) and its
+ * updated parameters broadcast from it (zero2.py:122-133), one call per round. */
+int zs_reduce_group(zs_comm* comm, int64_t n, const uint64_t* send, const uint64_t* recv,
+                    const int64_t* count, const int32_t* root, int dtype, uintptr_t stream);
+int zs_broadcast_group(zs_comm* comm, int64_t n, const uint64_t* buf, const int64_t* count,
+                       const int32_t* root, int dtype, uintptr_t stream);
 int zs_group_start(void);
 int zs_group_end(void);
 /* RCCL version the library is bound to at run time (e.g. 22606). */

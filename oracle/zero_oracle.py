@@ -131,7 +131,7 @@ def _sum_ranks(arrs):
 
 
 def simulate(variant: int, ws: int, init, xs=None, ys=None, steps: int = 10, lr: float = 1e-3,
-             local_grads=None, adam_kw=None):
+             local_grads=None, adam_kw=None, zero_grad: str = "optimizer"):
     """Restate a ``steps``-long run of reference ZeRO-``variant`` at world size ``ws``.
 
     init: list of fp32 param arrays (identical on every rank, torch.manual_seed(0) in the fixture).
@@ -140,6 +140,9 @@ def simulate(variant: int, ws: int, init, xs=None, ys=None, steps: int = 10, lr:
                  (from the fixture), replacing the forward/backward.
     adam_kw: optional callable i -> keyword arguments of ``adam_update`` for param i (its param
              group's lr / betas / eps / weight_decay / amsgrad / maximize / decoupled).
+    zero_grad: what the training loop clears before each backward — "optimizer" (the
+             reference harness: ShardedOptimizer.zero_grad(), owned grads only, zero1.py:107-108)
+             or "model" (model.zero_grad(): every grad, so nothing carries over).
     Returns dict with per-step params per rank, per-step reduced grads per rank (list in the
     reference's collective order), and final Adam state per rank.
     """
@@ -151,7 +154,7 @@ def simulate(variant: int, ws: int, init, xs=None, ys=None, steps: int = 10, lr:
     for t in range(steps):
         # zero_grad: inner optimizer only holds owned params (zero1.py:107-108, 71-74)
         for r in range(ws):
-            s, e = owner_range(n, ws, r)
+            s, e = (0, n) if zero_grad == "model" else owner_range(n, ws, r)
             for i in range(s, e):
                 held[r][i] = None
         for r in range(ws):

@@ -83,6 +83,17 @@ class GlooStagedComm:
                 t.copy_(h.to(t.device).to(t.dtype))
         self.calls.append(("reduce", t.numel()))
 
+    def reduce_out(self, send, recv, root, stream):
+        if self._defer(self.reduce_out, send, recv, root, stream):
+            return
+        stream.synchronize()
+        h = send.detach().to("cpu", torch.float32)
+        dist.reduce(h, dst=self._root(root), group=self.group)
+        if root == self.rank:
+            with torch.cuda.stream(stream):
+                recv.copy_(h.to(recv.device).to(recv.dtype))
+        self.calls.append(("reduce_out", send.numel()))
+
     def broadcast(self, t, root, stream):
         if self._defer(self.broadcast, t, root, stream):
             return

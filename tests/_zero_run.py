@@ -35,8 +35,18 @@ def module_for(variant: int):
     return mod
 
 
+def set_grad(p, g):
+    """Deliver a step's local gradient the way backward does: into the existing grad (the flat
+    arena's view after zero_grad(), which keeps ZeRO-1's carry as the reference's surviving grads
+    do), or as a new grad when there is none."""
+    if p.grad is not None and p.grad.shape == g.shape and p.grad.dtype == g.dtype:
+        p.grad.copy_(g)
+    else:
+        p.grad = g
+
+
 def run_injected(z, variant: int, rank: int, ws: int, device, comm=None, window_elems=64, tol=1e-6,
-                 buckets=None):
+                 buckets=None, arena=None):
     """Replay the fixture's grads through ShardedOptimizer; assert params match every step."""
     mod = module_for(variant)
     steps = int(z["steps"])
@@ -46,12 +56,14 @@ def run_injected(z, variant: int, rank: int, ws: int, device, comm=None, window_
         kw["comm"] = comm
     if buckets is not None:
         kw["buckets"] = buckets
+    if arena is not None:
+        kw["arena"] = arena
     opt = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), **kw)
     worst = 0.0
     for t in range(steps):
         opt.zero_grad()
         for i, p in enumerate(params):
-            p.grad = torch.from_numpy(z[f"r{rank}_t{t}_lg{i}"].copy()).to(device)
+            set_grad(p, torch.from_numpy(z[f"r{rank}_t{t}_lg{i}"].copy()).to(device))
         opt.step()
         key0 = f"r{rank}_t{t}_p0"
         if key0 in z.files:

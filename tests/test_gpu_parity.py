@@ -13,7 +13,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import GOLDEN, free_port
-from _zero_run import spawn_ranks, init_pg, rel, run_injected
+from _zero_run import spawn_ranks, init_pg, rel, run_injected, set_grad
 
 pytestmark = pytest.mark.gpu
 
@@ -84,7 +84,7 @@ def test_rccl_comm_ws1(gpu, pg1):
     comm.close()
 
 
-def _mr_worker(rank, ws, port, variant, name, buckets="ragged"):
+def _mr_worker(rank, ws, port, variant, name, buckets="ragged", arena=None):
     import sys
     from conftest import PKG, REPO  # noqa: F401  (sets sys.path in the child)
     from _gloo_comm import GlooStagedComm
@@ -92,35 +92,41 @@ def _mr_worker(rank, ws, port, variant, name, buckets="ragged"):
     torch.cuda.set_device(0)
     init_pg(rank, ws, port)
     z = np.load(GOLDEN / name)
-    run_injected(z, variant, rank, ws, torch.device("cuda:0"), comm=GlooStagedComm(), buckets=buckets)
+    run_injected(z, variant, rank, ws, torch.device("cuda:0"), comm=GlooStagedComm(), buckets=buckets,
+                 arena=arena)
     dist.barrier()
     dist.destroy_process_group()
     sys.stdout.flush()
 
 
-MR_CASES = [(v, f"traj_z{v}_ws{ws}_d16_{m}.npz") for v in (1, 2) for ws in (2, 3, 4)
+MR_CASES = [(v, f"traj_z{v}_ws{ws}_d16_{m}.npz") for v in (1, 2) for ws in (2, 3, 4, 8)
             for m in ("ref", "distinct")] + [(1, "traj_z1_ws2_d64_ref.npz"),
                                              (2, "traj_z2_ws4_d64_distinct.npz")]
 
 
 @pytest.mark.parametrize("variant,name", MR_CASES)
 def test_multirank_injected(gpu, variant, name):
+    """The default ws > 1 exchange (flat parameter arena: grouped reduce / broadcast rounds, no
+    pack / unpack) against the reference's trajectories, ws 2-8 incl. ZeRO-1's carry."""
     ws = int(name.split("_ws")[1].split("_")[0])
     spawn_ranks(_mr_worker, ws, (ws, _port(), variant, name))
+
+
+@pytest.mark.parametrize("variant,ws", [(1, 3), (2, 4), (1, 8), (2, 8)])
+def test_multirank_injected_bucket_arena(gpu, variant, ws):
+    """The rank-major bucket arena (pack / reduce-scatter / all-gather / unpack, ablation)."""
+    name = f"traj_z{variant}_ws{ws}_d16_distinct.npz"
+    spawn_ranks(_mr_worker, ws, (ws, _port(), variant, name, "ragged", "buckets"))
 
 
 @pytest.mark.parametrize("variant", [1, 2])
 def test_multirank_padded_buckets(gpu, variant):
     """The zero-padded bucket schedule (ablation) gives the same trajectory."""
-    spawn_ranks(_mr_worker, 3, (3, _port(), variant, f"traj_z{variant}_ws3_d16_distinct.npz", "padded"))
+    spawn_ranks(_mr_worker, 3, (3, _port(), variant, f"traj_z{variant}_ws3_d16_distinct.npz", "padded",
+                                "buckets"))
 
 
-def test_multirank_ws8_ragged(gpu):
-    """ws=8 over the 12-param MLP: most buckets are ragged (one reduce / broadcast per owner)."""
-    spawn_ranks(_mr_worker, 8, (8, _port(), 2, "traj_z2_ws8_d16_distinct.npz"))
-
-
-def _edge_worker(rank, ws, port, variant, buckets):
+def _edge_worker(rank, ws, port, variant, buckets, arena="flat"):
     import sys
     from conftest import PKG, REPO  # noqa: F401
     from _gloo_comm import GlooStagedComm
@@ -139,13 +145,14 @@ def _edge_worker(rank, ws, port, variant, buckets):
     want = zo.simulate(variant, ws, init, steps=steps, local_grads=lambda t, r, i: lg[(t, r, i)])
     params = [torch.nn.Parameter(torch.from_numpy(a.copy()).to(dev)) for a in init]
     opt = module_for(variant).ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=GlooStagedComm(),
-                                               bucket_mb=ws * 64 * 4 / (1 << 20), buckets=buckets)
+                                               bucket_mb=ws * 64 * 4 / (1 << 20), buckets=buckets,
+                                               arena=arena)
     if rank == 3:
         assert opt.local_param_indices == []
     for t in range(steps):
         opt.zero_grad()
         for i, p in enumerate(params):
-            p.grad = torch.from_numpy(lg[(t, rank, i)].copy()).to(dev)
+            set_grad(p, torch.from_numpy(lg[(t, rank, i)].copy()).to(dev))
         opt.step()
         for i, p in enumerate(params):
             ref = want["params"][t][rank][i]
@@ -159,11 +166,12 @@ def _edge_worker(rank, ws, port, variant, buckets):
 
 
 @pytest.mark.parametrize("variant", [1, 2])
-@pytest.mark.parametrize("buckets", ["ragged", "padded"])
-def test_multirank_fewer_params_than_ranks(gpu, variant, buckets):
+@pytest.mark.parametrize("buckets,arena", [("ragged", "flat"), ("ragged", "buckets"),
+                                           ("padded", "buckets")])
+def test_multirank_fewer_params_than_ranks(gpu, variant, buckets, arena):
     """Edge cases of the reference's ownership rule on the device path: n < ws (empty ranks) and a
     zero-element parameter, against the oracle's restatement of the reference."""
-    spawn_ranks(_edge_worker, 4, (4, _port(), variant, buckets))
+    spawn_ranks(_edge_worker, 4, (4, _port(), variant, buckets, arena))
 
 
 HP_CASES = {
@@ -206,7 +214,7 @@ def _hp_worker(rank, ws, port, variant, case):
     for t in range(steps):
         opt.zero_grad()
         for i, p in enumerate(params):
-            p.grad = torch.from_numpy(lg[(t, rank, i)].copy()).to(dev)
+            set_grad(p, torch.from_numpy(lg[(t, rank, i)].copy()).to(dev))
         opt.step()
         for i, p in enumerate(params):
             assert rel(p.detach().cpu().numpy(), want["params"][t][rank][i]) <= 1e-6, (case, rank, t, i)
@@ -259,3 +267,48 @@ def test_reference_harness_runs(gpu, variant):
                        timeout=180, env=env, cwd=str(PKG))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "Memory Usage Summary" in r.stdout and "Average step time" in r.stdout
+
+
+def _carry_worker(rank, ws, port, clear):
+    """ZeRO-1's carry follows what the loop clears (zero1.py:107-108): opt.zero_grad() clears only
+    owned grads, so the others' surviving averaged grads carry into the next all-reduce;
+    model.zero_grad() clears every grad, so nothing carries.  Both against the oracle."""
+    import sys
+    from conftest import PKG, REPO  # noqa: F401
+    from _gloo_comm import GlooStagedComm
+    from zero_amd import zero1
+    from oracle import zero_oracle as zo
+
+    torch.cuda.set_device(0)
+    init_pg(rank, ws, port)
+    dev = torch.device("cuda:0")
+    shapes = [(40, 6), (40,), (17, 3), (5,), (64,)]
+    g = torch.Generator().manual_seed(11)
+    init = [torch.randn(s, generator=g).numpy() for s in shapes]
+    steps = 4
+    lg = {(t, r, i): (torch.randn(s, generator=torch.Generator().manual_seed(97 * t + 13 * r + i))
+                      * 1e-2).numpy() for t in range(steps) for r in range(ws) for i, s in enumerate(shapes)}
+    want = zo.simulate(1, ws, init, steps=steps, local_grads=lambda t, r, i: lg[(t, r, i)],
+                       zero_grad=clear)
+    model = torch.nn.ParameterList([torch.nn.Parameter(torch.from_numpy(a.copy()).to(dev)) for a in init])
+    params = list(model)
+    opt = zero1.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=GlooStagedComm(),
+                                 bucket_mb=ws * 64 * 4 / (1 << 20))
+    for t in range(steps):
+        if clear == "model":
+            model.zero_grad()  # set_to_none: backward then hands over fresh grads
+        else:
+            opt.zero_grad()
+        for i, p in enumerate(params):
+            set_grad(p, torch.from_numpy(lg[(t, rank, i)].copy()).to(dev))
+        opt.step()
+        for i, p in enumerate(params):
+            assert rel(p.detach().cpu().numpy(), want["params"][t][rank][i]) <= 1e-6, (clear, rank, t, i)
+    dist.barrier()
+    dist.destroy_process_group()
+    sys.stdout.flush()
+
+
+@pytest.mark.parametrize("clear", ["optimizer", "model"])
+def test_zero1_carry_follows_zero_grad(gpu, clear):
+    spawn_ranks(_carry_worker, 3, (3, _port(), clear))

@@ -116,6 +116,87 @@ def test_ws8_ragged_buckets_match_reference():
     mp.spawn(_worker, args=(8, _port(), 2, "traj_z2_ws8_d16_distinct.npz", 64), nprocs=8, join=True)
 
 
+def _flat_worker(rank, ws, port, variant, name, window):
+    """The flat-arena exchange (flat.py FlatEngine) restated with numpy + gloo: owner-major arena
+    G / P (rank r's stream = its reference-owned params, 64-aligned), per round j one reduce of
+    every owner's window [jW, (j+1)W) onto its owner (out of place, into R), Adam on the own
+    window (ZeRO-1: carry weight ws-1, the opt.zero_grad() loop), one broadcast per owner."""
+    import os
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    from oracle import zero_oracle as zo
+    from zero_amd.plan import Plan
+
+    z = np.load(GOLDEN / name)
+    init = [z[f"init_{i}"].copy().reshape(-1) for i in range(12)]
+    n = len(init)
+    plan = Plan([p.size for p in init], ws, rank, "reference")
+    Ls = np.array([plan.stream_len(r) for r in range(ws)])
+    base = np.concatenate([[0], np.cumsum(Ls)[:-1]])
+    slot = np.zeros(n, np.int64)
+    for r in range(ws):
+        pc = plan.pieces(r)
+        slot[pc.param] = base[r] + pc.stream_off
+    P = np.zeros(int(Ls.sum()), np.float32)
+    for i, a in enumerate(init):
+        P[slot[i]:slot[i] + a.size] = a
+    L = int(Ls[rank])
+    R = np.zeros(L, np.float32)
+    m, v, carry = (np.zeros(L, np.float32) for _ in range(3))
+    pc = plan.pieces(rank)
+    K = max(1, -(-int(Ls.max()) // window))
+    for t in range(int(z["steps"])):
+        G = np.zeros_like(P)
+        for i in range(n):
+            g = z[f"r{rank}_t{t}_lg{i}"].reshape(-1)
+            G[slot[i]:slot[i] + g.size] = g
+        for j in range(K):  # reduce-scatter-v: one reduce per owner window
+            lo = j * window
+            for r in range(ws):
+                c = int(np.clip(Ls[r] - lo, 0, window))
+                if c:
+                    part = torch.from_numpy(G[base[r] + lo:base[r] + lo + c].copy())
+                    dist.reduce(part, dst=r)
+                    if r == rank:
+                        R[lo:lo + c] = part.numpy()
+        for i, so, ln in zip(pc.param, pc.stream_off, pc.length):  # Adam on the own stream
+            gsum = R[so:so + ln]
+            if variant == 1:
+                g = ((gsum + np.float32(ws - 1) * carry[so:so + ln]) / np.float32(ws)).astype(np.float32)
+                carry[so:so + ln] = g
+            else:
+                g = (gsum / np.float32(ws)).astype(np.float32)
+            p, mm, vv, _ = zo.adam_update(P[base[rank] + so:base[rank] + so + ln], g, m[so:so + ln],
+                                          v[so:so + ln], t + 1)
+            P[base[rank] + so:base[rank] + so + ln] = p
+            m[so:so + ln], v[so:so + ln] = mm, vv
+        for j in range(K):  # all-gather-v: one broadcast per owner window
+            lo = j * window
+            for r in range(ws):
+                c = int(np.clip(Ls[r] - lo, 0, window))
+                if c:
+                    part = torch.from_numpy(P[base[r] + lo:base[r] + lo + c].copy())
+                    dist.broadcast(part, src=r)
+                    P[base[r] + lo:base[r] + lo + c] = part.numpy()
+        if f"r{rank}_t{t}_p0" in z.files:
+            for i in range(n):
+                ref = z[f"r{rank}_t{t}_p{i}"].reshape(-1)
+                got = P[slot[i]:slot[i] + ref.size]
+                assert np.max(np.abs(got - ref)) / np.max(np.abs(ref)) <= 1e-6, (name, rank, t, i)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("ws,window", [(2, 64), (3, 128), (4, 64), (8, 64), (4, 1 << 20)])
+def test_flat_arena_exchange_matches_reference(variant, ws, window):
+    name = f"traj_z{variant}_ws{ws}_d16_distinct.npz"
+    mp.spawn(_flat_worker, args=(ws, _port(), variant, name, window), nprocs=ws, join=True)
+
+
 def test_collective_kats_gloo():
     """02-operations.ipynb:1853-2109 known answers through the same gloo calls the tests use."""
     z = np.load(GOLDEN / "collective_kat.npz")
