@@ -492,7 +492,7 @@ def _bf16_sum_tolerance(world: int) -> float:
     return world * 2.0 ** -8
 
 
-def _regen_grads(shapes, world, dev, keep):
+def _regen_grads(shapes, world, dev, keep, dtype=None):
     """The bench's synthetic gradients of every rank (seed = rank, N(0,1)*1e-3, one generator
     pass over the set, as generated in main / bench_zero3_paramset), reduced on the fly to the
     exact fp32 sum and sum of |g| of the tensors in ``keep`` (index -> flat element slice)."""
@@ -507,7 +507,7 @@ def _regen_grads(shapes, world, dev, keep):
             t = (torch.empty(s, dtype=torch.float32, device=dev).normal_(generator=gen) * 1e-3)
             if i not in keep:
                 continue
-            v = t.to(torch.bfloat16).float().reshape(-1)[keep[i]]
+            v = t.to(dtype or torch.bfloat16).float().reshape(-1)[keep[i]]
             exact[i] = v.clone() if exact[i] is None else exact[i] + v
             absum[i] = v.abs() if absum[i] is None else absum[i] + v.abs()
     return exact, absum
@@ -542,12 +542,12 @@ def zero3_gather_check(opt, model, shapes, full_copies, dev, world, rank, red_de
     for i in idx:
         r0, r1, row = ar.rows[i]
         keep[i] = slice(r0 * row, r1 * row)
-    exact, absum = _regen_grads(shapes, world, dev, keep)
+    exact, absum = _regen_grads(shapes, world, dev, keep, ar.dtype)
     x = torch.zeros(1, device=dev, requires_grad=True)
     opt.zero_grad()
     model(x).sum().backward()
     torch.cuda.synchronize()
-    tol = _bf16_sum_tolerance(world)
+    tol = _bf16_sum_tolerance(world) if ar.dtype == torch.bfloat16 else world * 2.0 ** -22
     worst = 0.0
     rs_bad = []
     params = list(model.parameters())
@@ -632,7 +632,7 @@ def zero12_exchange_check(opt, step, params, shapes, dev, world, rank, red_dev):
     step()
     torch.cuda.synchronize()
     eng.capture_reduced = None
-    exact, absum = _regen_grads(shapes, world, dev, {i: slice(None) for i in own})
+    exact, absum = _regen_grads(shapes, world, dev, {i: slice(None) for i in own}, eng.dtype)
     bf16 = eng.dtype == torch.bfloat16
     tol = _bf16_sum_tolerance(world) if bf16 else world * 2.0 ** -22
     worst_sum, worst_ulp, bad = 0.0, 0, []
@@ -1023,6 +1023,8 @@ def main():
         o = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), layout=args.layout,
                                  bucket_mb=args.bucket_mb, sync=False, buckets=args.buckets,
                                  master=args.master, arena=arena, **kw)
+        if o.engine is None:
+            o._build_engine()  # (the bucket engine is otherwise built by the first step)
         if getattr(o.engine, "arena_kind", None) == "flat":
             # grads resident in HBM where a backward puts them: in the arena's grad views
             o.zero_grad()
@@ -1060,7 +1062,7 @@ def main():
             _teardown_engine(opt)
             opt = step = None
         opt, step = build(arena)
-        kind = getattr(opt.engine, "arena_kind", "buckets") if opt.engine is not None else arena
+        kind = getattr(opt.engine, "arena_kind", "buckets")
         if world > 1:
             _phase(f"exchange check ({kind} arena)")
             exchange_check[kind] = zero12_exchange_check(opt, step, params, shapes, dev, world, rank,
@@ -1075,7 +1077,7 @@ def main():
         if best != arenas[-1]:
             _teardown_engine(opt)
             opt, step = build(best)
-    arena_used = getattr(opt.engine, "arena_kind", "buckets") if opt.engine is not None else arenas[0]
+    arena_used = getattr(opt.engine, "arena_kind", "buckets") if multi else "none (ws=1: no exchange)"
 
     _phase("warmup")
     for _ in range(args.warmup):

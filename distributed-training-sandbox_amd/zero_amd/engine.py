@@ -83,7 +83,10 @@ def probed_zeros(n: int, dtype, device, tries: int = 5):
         info["gbs"].append(round(gbs, 1))
     best = max(range(len(cands)), key=lambda i: cands[i][0])
     buf = cands[best][1]
-    del cands
+    del cands, probe
+    # hand the rejected candidates back to the device (not just to torch's cache), so later
+    # allocations outside torch (RCCL buffers, segment tables) and mem_get_info see them
+    torch.cuda.empty_cache()
     info.update(tries=tries, chosen=best)
     return buf, info
 

@@ -30,9 +30,18 @@ class IdentityComm:
     def broadcast_v(self, buf, win_off, win_len, stream):
         pass
 
+    def reduce_out(self, send, recv, root, stream):  # flat arena: the sum of own + zeros
+        if root == self.rank and send.data_ptr() != recv.data_ptr():
+            with torch.cuda.stream(stream):
+                recv.copy_(send)
 
-@pytest.mark.parametrize("ws,buckets", [(8, "ragged"), (4, "padded")])
-def test_c4_rank0_bucket_path_full_scale(gpu, monkeypatch, ws, buckets):
+    def broadcast(self, t, root, stream):
+        pass
+
+
+@pytest.mark.parametrize("ws,buckets,arena", [(8, "ragged", "buckets"), (4, "padded", "buckets"),
+                                              (8, "ragged", "flat"), (3, "ragged", "flat")])
+def test_c4_rank0_bucket_path_full_scale(gpu, monkeypatch, ws, buckets, arena):
     import torch.distributed as dist
 
     import zero_amd._sharded as sh
@@ -41,7 +50,9 @@ def test_c4_rank0_bucket_path_full_scale(gpu, monkeypatch, ws, buckets):
     from zero_amd import zero2
     from zero_amd.shapes import smollm3_3b_shapes
 
-    init_pg(0, 1, 29640 + ws)
+    from conftest import free_port
+
+    init_pg(0, 1, free_port())
     real_get = sh.get
     monkeypatch.setattr(sh, "get", lambda what, dm=None: {"ws": ws, "rank": 0}[what]
                         if what in ("ws", "rank") else real_get(what, dm))
@@ -55,20 +66,33 @@ def test_c4_rank0_bucket_path_full_scale(gpu, monkeypatch, ws, buckets):
             grads.append((torch.randn(s, device=gpu, generator=gen) * 1e-3).to(torch.bfloat16))
         init = [p.detach().clone() for p in params]
         opt = zero2.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=IdentityComm(ws),
-                                     buckets=buckets)
-        for p, g in zip(params, grads):
-            p.grad = g
+                                     buckets=buckets, arena=arena)
+        if arena == "flat":  # backward's way: into the zeroed arena views
+            opt.zero_grad()
+            for p, g in zip(params, grads):
+                p.grad.copy_(g)
+        else:
+            for p, g in zip(params, grads):
+                p.grad = g
         opt.step()
         torch.cuda.synchronize()
         eng = opt.engine
-        assert eng.K > 1 and (buckets == "padded" or eng.plan.num_even < eng.K)
+        if arena == "flat":
+            assert getattr(eng, "arena_kind", None) == "flat" and eng.K > 1
+            for p in params:  # every parameter is a view of the arena
+                assert p.data.untyped_storage().data_ptr() == eng.P.untyped_storage().data_ptr()
+        else:
+            assert eng.K > 1 and (buckets == "padded" or eng.plan.num_even < eng.K)
         owned = set(opt.local_param_indices)
         hp = c_oracle.hparams(step=1, grad_div=float(ws))
         rng = np.random.default_rng(0)
         for i, (p, g, p0) in enumerate(zip(params, grads, init)):
             bits = p.detach().view(torch.int16).reshape(-1)
-            if i not in owned:  # pack -> window -> unpack round trip
-                assert torch.equal(bits, g.view(torch.int16).reshape(-1)), i
+            if i not in owned:
+                if arena == "flat":  # nothing arrives from the absent owner: unchanged
+                    assert torch.equal(bits, p0.view(torch.int16).reshape(-1)), i
+                else:  # pack -> window -> unpack round trip
+                    assert torch.equal(bits, g.view(torch.int16).reshape(-1)), i
                 continue
             n = p.numel()
             idx = torch.from_numpy(np.unique(rng.integers(0, n, min(n, 4096)))).to(gpu)
