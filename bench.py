@@ -419,7 +419,7 @@ def _zero3_report(args, opt, world, rank, red_dev, el, total, workload, extra):
                       else "fp32"),
             "data": "synthetic",
             "config": dict(workload=workload, params=int(total), param_dtype=args.dtype, zero=3,
-                           update="real ZeRO-3 (update=True)", bucket_mb=args.bucket_mb,
+                           update="real ZeRO-3 (update=True)", bucket_mb=args.bucket_mb or 128.0,
                            gather_dtype=args.gather or args.dtype, parallelism=f"dp{world}"),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -708,7 +708,7 @@ def bench_zero3(args, world, rank, dev, use_nccl):
     comm, chk = _zero3_comm(args, world, rank, dev)
     kw = {} if comm is None else {"comm": comm}
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
-                                 sync=False, gather_dtype=args.gather, bucket_mb=args.bucket_mb, **kw)
+                                 sync=False, gather_dtype=args.gather, bucket_mb=args.bucket_mb or 128.0, **kw)
     zero3.register_zero3_hooks(model, opt.param_managers)
 
     def step():
@@ -772,7 +772,7 @@ def bench_zero3_paramset(args, world, rank, dev, use_nccl):
             if what in ("ws", "rank") else real_get(what, dm)
     kw = {} if comm is None else {"comm": comm}
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
-                                 sync=False, gather_dtype=args.gather, bucket_mb=args.bucket_mb, **kw)
+                                 sync=False, gather_dtype=args.gather, bucket_mb=args.bucket_mb or 128.0, **kw)
     zero3.register_zero3_hooks(model, opt.param_managers)
     gather_check = None
     if world > 1:
@@ -905,7 +905,9 @@ def main():
                     help="optimizer-shard layout: reference = whole params by index (zero1.py:55-62, "
                          "ZeRO-1/2); chunk = dim-0 chunks of every param (zero3.py:107-108, forced "
                          "by --zero 3 on C4/C5); flat = balanced 1/N slices (ablation)")
-    ap.add_argument("--bucket-mb", type=float, default=256.0)
+    ap.add_argument("--bucket-mb", type=float, default=None,
+                    help="MiB per bucket / flat round (default: the optimizer's own — 1024 for the "
+                         "flat arena, 256 for the bucket arena, 128 for ZeRO-3 reduce buckets)")
     ap.add_argument("--arena", default="auto", choices=["auto", "flat", "buckets"],
                     help="ZeRO-1/2 exchange at N>1: flat = params and grads are views of one "
                          "owner-major arena, grouped reduce / broadcast rounds, no pack / unpack; "
@@ -1191,7 +1193,8 @@ def main():
                 if args.dtype == "bf16" and args.master == "split"
                 else "fp32 (master, exp_avg, exp_avg_sq)",
                 "master": args.master if args.dtype == "bf16" else "param",
-                "zero": args.zero, "layout": args.layout, "bucket_mb": args.bucket_mb,
+                "zero": args.zero, "layout": args.layout,
+                "bucket_mb": opt._bucket_bytes / (1 << 20),
                 "bucket_mode": args.buckets,
                 "buckets": eng.K, "parallelism": f"dp{world}", "comm": comm_used,
                 "arena": arena_used,

@@ -39,7 +39,7 @@ class ShardedOptimizerBase:
     _variant = 2
 
     def __init__(self, optimizer: Optimizer, *, layout: str = "reference",
-                 bucket_mb: float = 256.0, comm=None, sync: bool = True, buckets: str = "ragged",
+                 bucket_mb: float | None = None, comm=None, sync: bool = True, buckets: str = "ragged",
                  overlap: bool = False, overlap_bucket_mb: float = 64.0, master: str = "split",
                  arena: str = "flat"):
         if not isinstance(optimizer, torch.optim.Adam):
@@ -70,6 +70,11 @@ class ShardedOptimizerBase:
         self.world_size, self.rank = world_size, rank
         self._layout = layout
         self._buckets = buckets
+        # bytes per bucket (bucket arena) / per round (flat arena, all owners' windows together);
+        # default 256 MiB / 1 GiB: a flat round has no pack to pipeline, so fewer, larger rounds
+        # cost only the last round's Adam as exposed tail and cut the launches per step
+        if bucket_mb is None:
+            bucket_mb = 1024.0 if arena == "flat" else 256.0
         self._bucket_bytes = int(bucket_mb * (1 << 20))
         self._comm = comm
         self._sync = sync
@@ -82,6 +87,7 @@ class ShardedOptimizerBase:
         self._arena = arena
         self.engine: ShardEngine | None = None
         self._step_tensors = {}
+        self._validated = [None] * len(self.params)
         self._overlap = bool(overlap)
         self._overlap_hooks = []
         if self._overlap:
@@ -171,10 +177,14 @@ class ShardedOptimizerBase:
             self._build_engine()
         had_vmax = self.engine.vmax is not None
         grads = [p.grad for p in self.params]
-        for g, p in zip(grads, self.params):
-            if g is not None and (g.dtype != p.dtype or g.shape != p.shape or not g.is_contiguous()):
+        seen = self._validated
+        for i, (g, p) in enumerate(zip(grads, self.params)):
+            if g is None or g is seen[i]:  # the same grad tensor as last step: already checked
+                continue
+            if g.dtype != p.dtype or g.shape != p.shape or not g.is_contiguous():
                 raise ValueError("zero_amd: grads must be contiguous and match their param's "
                                  "dtype and shape")
+            seen[i] = g
         with torch.no_grad():
             self.engine.step(grads, self._hparams_of)
         if not had_vmax and self.engine.vmax is not None:

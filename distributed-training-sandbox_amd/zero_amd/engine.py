@@ -175,7 +175,11 @@ class ShardEngine:
         return pc.param.tolist(), pc.param_off.tolist(), pc.stream_off.tolist(), pc.length.tolist()
 
     def owned_param_indices(self):
-        return sorted(set(int(i) for i, n in zip(self.pieces.param, self.pieces.length) if n > 0))
+        own = getattr(self, "_owned_idx", None)
+        if own is None:
+            own = self._owned_idx = sorted(set(int(i) for i, n in zip(self.pieces.param,
+                                                                     self.pieces.length) if n > 0))
+        return own
 
     def state_views(self, i: int):
         """exp_avg / exp_avg_sq views of param i's shard (Layout R: the whole param)."""
@@ -299,8 +303,10 @@ class ShardEngine:
             has &= gb.marked | ~is_view
         if any(hparams_of(g)["amsgrad"] for g in set(self.group_of)):
             self.ensure_vmax()
-        owned = np.zeros(n, bool)
-        owned[self.owned_param_indices()] = True
+        owned = getattr(self, "_owned_mask", None)
+        if owned is None:
+            owned = self._owned_mask = np.zeros(n, bool)
+            owned[self.owned_param_indices()] = True
         self.steps[owned & has] += 1
         self.last_adam_bytes = 0
         if getattr(self, "gb", None) is not None:

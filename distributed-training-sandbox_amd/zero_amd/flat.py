@@ -99,6 +99,7 @@ class FlatEngine(ShardEngine):
         self.W = W
         self.K = max(1, -(-int(self.Ls.max()) // W))
         self.rounds = [self._make_round(j) for j in range(self.K)]
+        self._views = [None] * n  # the grad views handed out (identity = "still the view")
         mk = lambda: [torch.cuda.Event() for _ in range(self.K)]  # noqa: E731
         self.ev_red, self.ev_adam, self.ev_bc = mk(), mk(), mk()
         self.ev_grads = torch.cuda.Event()
@@ -141,13 +142,18 @@ class FlatEngine(ShardEngine):
         return self.slot_view(self.G, i)
 
     def is_view(self, i: int, g) -> bool:
-        return (g is not None and g.data_ptr() == self.G.data_ptr() + int(self.slot[i]) * self.es
+        if g is None:
+            return False
+        if g is self._views[i]:
+            return True
+        return (g.data_ptr() == self.G.data_ptr() + int(self.slot[i]) * self.es
                 and g.shape == self.params[i].shape)
 
     def install_views(self):
         for i, p in enumerate(self.params):
             if not self.is_view(i, p.grad):
                 p.grad = self.grad_view(i)
+            self._views[i] = p.grad
 
     def zero_grad(self):
         """The wrapper's zero_grad(): zero G and make every p.grad its arena view."""
@@ -159,6 +165,42 @@ class FlatEngine(ShardEngine):
     def rebuild_rows(self):
         """Adam rows again (after the amsgrad buffer appeared)."""
         self.rounds = [self._make_round(j) for j in range(self.K)]
+
+    def _static_sets(self, rd: _Round):
+        """The round's Adam sets when every owned param has a grad, one per param group (the
+        common case: built once, the rows never change because every pointer is the arena's)."""
+        sets = getattr(rd, "sets", None)
+        if sets is None:
+            from .kernels import AdamSet
+
+            groups = np.asarray(self.group_of)[rd.idx]
+            sets = []
+            for gi in np.unique(groups):
+                sel = np.nonzero(groups == gi)[0]
+                sets.append((int(gi), rd.idx[sel], AdamSet(np.ascontiguousarray(rd.rows[sel]),
+                                                           self.zdtype, self.p_dtype)))
+            rd.sets = sets
+        return sets
+
+    def _adam_round_fast(self, rd: _Round, hps, stream) -> bool:
+        """Launch the round's static sets if every param in them shares its group's (step,
+        carry) key this step; returns False to fall back to the general partitioning."""
+        sets = self._static_sets(rd)
+        for gi, idx, aset in sets:
+            hp = hps.get(gi)
+            if hp is None:
+                return False
+        for gi, idx, aset in sets:
+            if self.timing_events is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                aset.run(hps[gi], stream)
+                e1.record(stream)
+                self.timing_events.append((e0, e1, aset.bytes))
+            else:
+                aset.run(hps[gi], stream)
+            self.last_adam_bytes += aset.bytes
+        return True
 
     # ------------------------------------------------------------------------------------------
     def _reduce_round(self, rd: _Round, cs):
@@ -193,7 +235,9 @@ class FlatEngine(ShardEngine):
         n = len(self.params)
         es = self.es
         has = np.fromiter((g is not None for g in grads), bool, n)
-        view = np.fromiter((self.is_view(i, g) for i, g in enumerate(grads)), bool, n)
+        vw = self._views
+        view = np.fromiter((g is not None and (g is vw[i] or self.is_view(i, g))
+                            for i, g in enumerate(grads)), bool, n)
         if any(hparams_of(g)["amsgrad"] for g in set(self.group_of)) and self.vmax is None:
             self.ensure_vmax()
             self.rebuild_rows()
@@ -215,6 +259,26 @@ class FlatEngine(ShardEngine):
         cmul = np.where(view, self.ws - 1, 0).astype(np.int64)
         self.steps[self.owned & has] += 1
         self.last_adam_bytes = 0
+        # fast path: every owned param has a grad and, per param group, one (step, carry) key
+        own = self.owned
+        hps = {}
+        if has[own].all():
+            from .kernels import adam_hparams
+
+            gof = np.asarray(self.group_of)
+            for gi in np.unique(gof[own]):
+                sel = own & (gof == gi)
+                st, cm = np.unique(self.steps[sel]), np.unique(cmul[sel])
+                if len(st) != 1 or len(cm) != 1:
+                    continue
+                h = hparams_of(int(gi))
+                if h["amsgrad"] and self.vmax is None:
+                    continue
+                hps[int(gi)] = adam_hparams(
+                    h["lr"], h["beta1"], h["beta2"], h["eps"], h["weight_decay"], int(st[0]),
+                    decoupled=h["decoupled"], amsgrad=h["amsgrad"], maximize=h["maximize"],
+                    grad_div=float(self.ws),
+                    carry_mul=float(cm[0]) if self.carry is not None else 0.0)
         self.ev_grads.record(stream)
         cs = self.comm_stream
         cs.wait_event(self.ev_grads)
@@ -231,7 +295,7 @@ class FlatEngine(ShardEngine):
         with _lib.phase_range("optimizer_step"):  # zero1.py:88
             for rd in self.rounds:
                 stream.wait_event(self.ev_red[rd.j])
-                if len(rd.idx):
+                if len(rd.idx) and not (hps and self._adam_round_fast(rd, hps, stream)):
                     live = has[rd.idx]
                     rows, idx = (rd.rows, rd.idx) if live.all() else (rd.rows[live], rd.idx[live])
                     self._run_adam(("flat", rd.j), rows, idx, hparams_of, stream,
@@ -248,6 +312,7 @@ class FlatEngine(ShardEngine):
         # every p.grad is (again) its arena view, holding this step's local gradient
         for i in np.nonzero(has & ~view)[0]:
             self.params[i].grad = self.grad_view(int(i))
+            self._views[i] = self.params[i].grad
 
     def _timed_start(self, cs):
         if self.comm_events is None:
