@@ -381,6 +381,65 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(T* __restrict__ x, int6
 }
 
 // ----------------------------------------------------------------------------------------------
+// fp32 <-> bf16 conversion (the bf16 gradient exchange of fp32-parameter models)
+// ----------------------------------------------------------------------------------------------
+// 8 elements per lane per iteration: 32 B of fp32 (two 16-B loads) <-> 16 B of bf16 (one 16-B
+// store), non-temporal (each byte is touched once); grid-stride; the n % 8 tail by block 0.
+// fp32 -> bf16 rounds to nearest even (v_cvt_pk_bf16_f32), NaN stays NaN; bf16 -> fp32 is exact.
+template <bool TO_BF16>
+__global__ __launch_bounds__(kThreads) void convert_kernel(const void* __restrict__ src,
+                                                           void* __restrict__ dst, int64_t n) {
+  const int64_t n8 = n / 8;
+  const int64_t stride = int64_t(gridDim.x) * kThreads;
+  for (int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x; i < n8; i += stride) {
+    if constexpr (TO_BF16) {
+      const float* s = static_cast<const float*>(src) + i * 8;
+      const float4 a = ld4(s, 0), b = ld4(s, 4);
+      const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      uint32_t w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        w[j] = uint32_t(f32_to_bf16(v[2 * j])) | (uint32_t(f32_to_bf16(v[2 * j + 1])) << 16);
+      nt_st16(static_cast<unsigned short*>(dst) + i * 8, make_uint4(w[0], w[1], w[2], w[3]));
+    } else {
+      const uint4 h = nt_ld16(static_cast<const unsigned short*>(src) + i * 8);
+      const uint32_t w[4] = {h.x, h.y, h.z, h.w};
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[2 * j] = __uint_as_float(w[j] << 16);
+        v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+      }
+      float* d = static_cast<float*>(dst) + i * 8;
+      st4(d, 0, make_float4(v[0], v[1], v[2], v[3]));
+      st4(d, 4, make_float4(v[4], v[5], v[6], v[7]));
+    }
+  }
+  if (blockIdx.x == 0) {
+    const int64_t i = n8 * 8 + threadIdx.x;
+    if (i < n) {
+      if constexpr (TO_BF16)
+        glob(static_cast<unsigned short*>(dst))[i] = f32_to_bf16(glob(static_cast<const float*>(src))[i]);
+      else
+        glob(static_cast<float*>(dst))[i] = bf16_to_f32(glob(static_cast<const unsigned short*>(src))[i]);
+    }
+  }
+}
+
+// scalar variant for unaligned buffers
+template <bool TO_BF16>
+__global__ __launch_bounds__(kThreads) void convert_scalar_kernel(const void* __restrict__ src,
+                                                                  void* __restrict__ dst, int64_t n) {
+  for (int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x; i < n;
+       i += int64_t(gridDim.x) * kThreads) {
+    if constexpr (TO_BF16)
+      glob(static_cast<unsigned short*>(dst))[i] = f32_to_bf16(glob(static_cast<const float*>(src))[i]);
+    else
+      glob(static_cast<float*>(dst))[i] = bf16_to_f32(glob(static_cast<const unsigned short*>(src))[i]);
+  }
+}
+
+// ----------------------------------------------------------------------------------------------
 // row-wise fp8 (OCP E4M3) quantise / dequantise for the low-precision parameter all-gather
 // ----------------------------------------------------------------------------------------------
 constexpr float kE4M3Max = 448.0f;
@@ -696,6 +755,30 @@ int zs_scale(void* x, int64_t n, int dtype, double div, uintptr_t stream) {
   else
     hipLaunchKernelGGL(scale_kernel<unsigned short>, dim3(grid), dim3(kThreads), 0, st,
                        static_cast<unsigned short*>(x), n, fdiv, inv, pow2);
+  ZS_HIP(hipGetLastError());
+  return ZS_OK;
+}
+
+int zs_convert(const void* src, int src_dtype, void* dst, int dst_dtype, int64_t n,
+               uintptr_t stream) {
+  ZS_REQUIRE(n >= 0, "zs_convert: n < 0");
+  ZS_REQUIRE((src_dtype == ZS_F32 && dst_dtype == ZS_BF16) ||
+                 (src_dtype == ZS_BF16 && dst_dtype == ZS_F32),
+             "zs_convert: only fp32 <-> bf16 (got %d -> %d)", src_dtype, dst_dtype);
+  if (n == 0) return ZS_OK;
+  ZS_REQUIRE(src && dst, "zs_convert: NULL buffer");
+  const bool to_bf16 = src_dtype == ZS_F32;
+  const bool vec = aligned(uint64_t(src), 16) && aligned(uint64_t(dst), 16);
+  const int64_t work = vec ? std::max<int64_t>(1, n / 8) : n;
+  const int grid = int(std::min<int64_t>((work + kThreads - 1) / kThreads, grid_cap()));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (vec) {
+    if (to_bf16) hipLaunchKernelGGL(convert_kernel<true>, dim3(grid), dim3(kThreads), 0, st, src, dst, n);
+    else hipLaunchKernelGGL(convert_kernel<false>, dim3(grid), dim3(kThreads), 0, st, src, dst, n);
+  } else {
+    if (to_bf16) hipLaunchKernelGGL(convert_scalar_kernel<true>, dim3(grid), dim3(kThreads), 0, st, src, dst, n);
+    else hipLaunchKernelGGL(convert_scalar_kernel<false>, dim3(grid), dim3(kThreads), 0, st, src, dst, n);
+  }
   ZS_HIP(hipGetLastError());
   return ZS_OK;
 }

@@ -31,7 +31,7 @@ EXPORTED = (
     "zs_plan_num_segments", "zs_plan_segments", "zs_plan_num_buckets", "zs_plan_bucket_bytes",
     "zs_pack", "zs_unpack",
     "zs_copyset_create", "zs_copyset_run", "zs_copyset_destroy", "zs_scale",
-    "zs_fp8_quantize_rows", "zs_fp8_dequantize_rows",
+    "zs_convert", "zs_fp8_quantize_rows", "zs_fp8_dequantize_rows",
     "zs_adam_hparams_init", "zs_adamset_create", "zs_adamset_run", "zs_adamset_destroy",
     "zs_adamset_stats", "zs_adam_step",
     "zs_comm_unique_id", "zs_comm_init", "zs_comm_destroy", "zs_reduce_scatter", "zs_all_gather",
@@ -95,6 +95,7 @@ _SIGS = {
     "zs_copyset_run": ([_P, _U], ctypes.c_int),
     "zs_copyset_destroy": ([_P], ctypes.c_int),
     "zs_scale": ([_P, _I64, ctypes.c_int, ctypes.c_double, _U], ctypes.c_int),
+    "zs_convert": ([_P, ctypes.c_int, _P, ctypes.c_int, _I64, _U], ctypes.c_int),
     "zs_fp8_quantize_rows": ([_P, ctypes.c_int, _P, _P, _I64, _I64, _U], ctypes.c_int),
     "zs_fp8_dequantize_rows": ([_P, _P, _P, ctypes.c_int, _I64, _I64, _U], ctypes.c_int),
     "zs_adam_hparams_init": ([ctypes.c_double] * 5 + [ctypes.c_int] * 3 +

@@ -41,7 +41,7 @@ class ShardedOptimizerBase:
     def __init__(self, optimizer: Optimizer, *, layout: str = "reference",
                  bucket_mb: float | None = None, comm=None, sync: bool = True, buckets: str = "ragged",
                  overlap: bool = False, overlap_bucket_mb: float = 64.0, master: str = "split",
-                 arena: str = "flat"):
+                 arena: str = "flat", grad_comm: str | None = None):
         if not isinstance(optimizer, torch.optim.Adam):
             raise TypeError("zero_amd ShardedOptimizer wraps torch.optim.Adam / AdamW "
                             f"(got {type(optimizer).__name__})")
@@ -85,6 +85,11 @@ class ShardedOptimizerBase:
         # grouped reduce / broadcast, no pack / unpack (flat.py); "buckets" = the rank-major
         # bucket arena with pack / reduce-scatter / all-gather / unpack (engine.py)
         self._arena = arena
+        # grad_comm="bf16": fp32 grads cross the interconnect as bf16 (flat
+        # arena only); opt-in, since the sum is then rounded to bf16 before Adam sees it
+        self._grad_comm = grad_comm
+        if grad_comm is not None and arena != "flat":
+            raise ValueError("grad_comm='bf16' needs the flat arena")
         self.engine: ShardEngine | None = None
         self._step_tensors = {}
         self._validated = [None] * len(self.params)
@@ -125,7 +130,7 @@ class ShardedOptimizerBase:
 
             self.engine = FlatEngine(self.params, self._group_of, self.world_size, self.rank,
                                      carry=carry, comm=comm, bucket_bytes=self._bucket_bytes,
-                                     master=self._master)
+                                     master=self._master, grad_comm=self._grad_comm)
         else:
             self.engine = ShardEngine(self.params, self._group_of, self.world_size, self.rank,
                                       layout=self._layout, carry=carry, comm=comm,

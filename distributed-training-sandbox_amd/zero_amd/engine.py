@@ -267,8 +267,9 @@ class ShardEngine:
             sel = np.nonzero((keys == key).all(axis=1))[0]
             sub = np.ascontiguousarray(rows[sel])
             gidx, step, cmul = int(key[0]), int(key[1]), int(key[2])
+            gz = getattr(self, "czdtype", self.zdtype)  # dtype of the reduced grad Adam reads
             aset = self._cached(("adam", tag, gidx, len(sel), int(sel[0])), sub.tobytes(),
-                                lambda: AdamSet(sub, self.zdtype, self.p_dtype))
+                                lambda: AdamSet(sub, gz, self.p_dtype))
             hpd = hparams_of(gidx)
             if hpd["amsgrad"] and self.vmax is None:
                 raise RuntimeError("amsgrad state buffer missing")

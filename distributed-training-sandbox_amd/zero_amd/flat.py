@@ -62,7 +62,8 @@ class _Round:
 
 class FlatEngine(ShardEngine):
     def __init__(self, params, group_of, ws: int, rank: int, *, carry=False, comm=None,
-                 bucket_bytes: int = 256 << 20, master: str = "split", placement_tries: int = 5):
+                 bucket_bytes: int = 256 << 20, master: str = "split", placement_tries: int = 5,
+                 grad_comm: str | None = None):
         if ws < 2:
             raise ValueError("FlatEngine is the ws > 1 exchange; ws == 1 needs no arena")
         # the base class gives the reference layout's streams, the optimizer state and the Adam
@@ -92,7 +93,19 @@ class FlatEngine(ShardEngine):
                 self.P[s:s + int(self.numel[i])].copy_(p.detach().reshape(-1))
                 p.data = self.P[s:s + int(self.numel[i])].view(p.shape)
         self.G, _ = _zeros_placed(total, dt, dev, placement_tries)
-        self.R = torch.zeros(max(int(self.Ls[rank]), ALIGN_ELEMS), dtype=dt, device=dev)
+        # bf16 gradient exchange for fp32 parameters: G is converted into Gc
+        # (bf16, same layout) before the reduces, which then move and sum 2 B per element; Adam
+        # reads the bf16 sum (its fp32 master is the fp32 parameter itself)
+        if grad_comm not in (None, "bf16"):
+            raise ValueError(f"grad_comm must be None or 'bf16' (got {grad_comm!r})")
+        self.grad_comm = grad_comm if dt == torch.float32 else None
+        if grad_comm == "bf16" and dt != torch.float32:
+            raise ValueError("grad_comm='bf16' is for fp32 parameters (bf16 grads already are)")
+        cdt = torch.bfloat16 if self.grad_comm else dt
+        self.Gc = torch.zeros(total, dtype=cdt, device=dev) if self.grad_comm else self.G
+        self.ces = self.Gc.element_size()
+        self.czdtype = _lib.ZS_BF16 if self.grad_comm else self.zdtype
+        self.R = torch.zeros(max(int(self.Ls[rank]), ALIGN_ELEMS), dtype=cdt, device=dev)
         self.dirty = np.zeros(n, bool)  # G slot may hold a stale gradient
         self.zero_grad_calls = 0
         W = max(ALIGN_ELEMS, (int(bucket_bytes) // (ws * es)) // ALIGN_ELEMS * ALIGN_ELEMS)
@@ -112,10 +125,11 @@ class FlatEngine(ShardEngine):
         ws, es, W, r0 = self.ws, self.es, self.W, self.rank
         lo = j * W
         count = np.clip(self.Ls - lo, 0, W)
-        gb, pb, rb = self.G.data_ptr(), self.P.data_ptr(), self.R.data_ptr()
-        send = np.uint64(gb) + ((self.base + lo) * es).astype(np.uint64)
+        gb, pb, rb = self.Gc.data_ptr(), self.P.data_ptr(), self.R.data_ptr()
+        ces = self.ces  # element size on the wire (bf16 exchange of fp32 grads: 2)
+        send = np.uint64(gb) + ((self.base + lo) * ces).astype(np.uint64)
         recv = send.copy()
-        recv[r0] = np.uint64(rb + lo * es)
+        recv[r0] = np.uint64(rb + lo * ces)
         bcast = np.uint64(pb) + ((self.base + lo) * es).astype(np.uint64)
         # this rank's Adam rows: its pieces clipped to [lo, lo + count[rank])
         pc = self.pieces
@@ -126,7 +140,7 @@ class FlatEngine(ShardEngine):
         idx, a, b = pc.param[keep], a[keep], b[keep]
         so = a.astype(np.int64)
         ln = (b - a).astype(np.int64)
-        g = np.uint64(rb) + (so * es).astype(np.uint64)
+        g = np.uint64(rb) + (so * ces).astype(np.uint64)
         pslot = np.uint64(pb) + ((self.base[r0] + so) * es).astype(np.uint64)
         if self.mixed:  # master from P (split: + residual) or the fp32 master; bf16 param out to P
             rows = self._mixed_rows(idx, g, pslot, pslot, so, ln)
@@ -178,7 +192,7 @@ class FlatEngine(ShardEngine):
             for gi in np.unique(groups):
                 sel = np.nonzero(groups == gi)[0]
                 sets.append((int(gi), rd.idx[sel], AdamSet(np.ascontiguousarray(rd.rows[sel]),
-                                                           self.zdtype, self.p_dtype)))
+                                                           self.czdtype, self.p_dtype)))
             rd.sets = sets
         return sets
 
@@ -206,7 +220,7 @@ class FlatEngine(ShardEngine):
     def _reduce_round(self, rd: _Round, cs):
         comm = self.comm
         if hasattr(comm, "reduce_group"):
-            comm.reduce_group(rd.send, rd.recv, rd.count, rd.root, self.zdtype, cs)
+            comm.reduce_group(rd.send, rd.recv, rd.count, rd.root, self.czdtype, cs)
             return
         with _group(comm):  # tensor-level fallback (test communicators)
             for r in range(self.ws):
@@ -214,7 +228,7 @@ class FlatEngine(ShardEngine):
                 if c == 0:
                     continue
                 s0 = int(self.base[r]) + rd.j * self.W
-                src = self.G[s0:s0 + c]
+                src = self.Gc[s0:s0 + c]
                 dst = self.R[rd.j * self.W:rd.j * self.W + c] if r == self.rank else src
                 comm.reduce_out(src, dst, r, cs)
 
@@ -279,6 +293,10 @@ class FlatEngine(ShardEngine):
                     decoupled=h["decoupled"], amsgrad=h["amsgrad"], maximize=h["maximize"],
                     grad_div=float(self.ws),
                     carry_mul=float(cm[0]) if self.carry is not None else 0.0)
+        if self.grad_comm:  # the exchange moves bf16: convert every local grad once (2 launches' worth
+            from .kernels import convert  # of bytes: read 4 + write 2 B per element)
+
+            convert(self.G, self.Gc, stream)
         self.ev_grads.record(stream)
         cs = self.comm_stream
         cs.wait_event(self.ev_grads)
@@ -327,7 +345,8 @@ class FlatEngine(ShardEngine):
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record(cs)
         # bus bytes of the round as a ring reduce-scatter / all-gather of all owners' windows
-        self.comm_events.append((kind, "flat", e0, e1, elems * self.es * (self.ws - 1) / self.ws))
+        es = self.ces if kind == "rs" else self.es
+        self.comm_events.append((kind, "flat", e0, e1, elems * es * (self.ws - 1) / self.ws))
 
     def comm_time_s(self) -> float:
         """zero2.py:92,116: from step() entry until the gradient reduction is done."""

@@ -115,3 +115,16 @@ def adam_step(p, g, m, v, *, step, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, we
     _lib.call("zs_adam_step", ptr(p), ptr(p_bf16), ptr(g), g_dtype, ptr(m), ptr(v), n, float(lr),
               float(beta1), float(beta2), float(eps), float(weight_decay), int(bool(decoupled)),
               int(step), float(grad_div), ptr(carry), float(carry_mul), stream_handle(st))
+
+
+def convert(src, dst, stream=None) -> None:
+    """dst[:] = src converted fp32 -> bf16 (round to nearest even) or bf16 -> fp32 (zs_convert);
+    contiguous tensors of equal element count, enqueued on ``stream``."""
+    import torch
+
+    from .comm import zs_dtype
+
+    assert src.numel() == dst.numel() and src.is_contiguous() and dst.is_contiguous()
+    st = torch.cuda.current_stream(src.device) if stream is None else stream
+    _lib.call("zs_convert", src.data_ptr(), zs_dtype(src.dtype), dst.data_ptr(), zs_dtype(dst.dtype),
+              src.numel(), stream_handle(st))

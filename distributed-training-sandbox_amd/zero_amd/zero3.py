@@ -445,7 +445,8 @@ class _GradReducer:
         if self.K:
             cur.wait_event(self.ev_done[self.K - 1])
         for i, p in enumerate(opt.params):
-            if self.had_grad[i] and p.data.shape == opt._arena.shard_shapes[i]:
+            if (self.had_grad[i] and p.data.shape == opt._arena.shard_shapes[i]
+                    and opt._G.dtype == p.dtype):  # (a bf16 exchange's chunks stay internal)
                 s, n = int(opt._arena.slot[i]), int(opt._arena.ln[i])
                 p.grad = opt._G[s:s + n].view(opt._arena.shard_shapes[i])
 
@@ -464,23 +465,30 @@ class _GradReducer:
             return
         dev = ar.device
         cur = torch.cuda.current_stream(dev)
+        wdt = opt._G.dtype  # on the wire: the param dtype, or bf16 for grad_comm="bf16"
         sends = []  # (param index, send buffer): alive until the RCCL group has been enqueued
         for i in self.groups[k]:
             p = opt.params[i]
             g = p.grad
             S, N = int(ar.S[i]), int(ar.numel[i])
             if g is None:
-                send = torch.zeros(ws * S, dtype=ar.dtype, device=dev)  # every rank takes part
+                send = torch.zeros(ws * S, dtype=wdt, device=dev)  # every rank takes part
             else:
                 if g.numel() != N or g.dtype != ar.dtype:
                     raise ValueError("zero_amd ZeRO-3 update mode needs the full-size gradient "
                                      "(param %d: got %s)" % (i, tuple(g.shape)))
                 self.had_grad[i] = True
                 flat = g.reshape(-1) if g.is_contiguous() else g.contiguous().reshape(-1)
-                if N == ws * S:
+                if wdt != ar.dtype:  # bf16 exchange: gfx950 RNE conversion into the send buffer
+                    from .kernels import convert
+
+                    send = torch.empty(ws * S, dtype=wdt, device=dev) if N == ws * S else \
+                        torch.zeros(ws * S, dtype=wdt, device=dev)
+                    convert(flat, send[:N], cur)
+                elif N == ws * S:
                     send = flat  # zero-copy: rows of torch.chunk are contiguous
                 else:  # uneven chunks: every rank sends ws*S elements
-                    send = torch.zeros(ws * S, dtype=ar.dtype, device=dev)
+                    send = torch.zeros(ws * S, dtype=wdt, device=dev)
                     send[:N].copy_(flat)
             sends.append((i, send))
         ready = torch.cuda.Event()
@@ -500,7 +508,7 @@ class _GradReducer:
             opt.params[i].grad = None
         self.ev_done[k].record(cs)
         if self.timing is not None:
-            bus = sum(int(ar.S[i]) * ws for i, _ in sends) * ar.P.element_size() * (ws - 1) / ws
+            bus = sum(int(ar.S[i]) * ws for i, _ in sends) * opt._G.element_size() * (ws - 1) / ws
             self.timing.append((e0, _timed_after(cs), bus))
         del sends
 
@@ -509,7 +517,7 @@ class ShardedOptimizer:
     """zero3.py:81-168 with ``update`` selecting reference (no-op) or real ZeRO-3 updates."""
 
     def __init__(self, optimizer: Optimizer, *, update: bool = False, comm=None, sync: bool = True,
-                 gather_dtype=None, bucket_mb: float = 128.0):
+                 gather_dtype=None, bucket_mb: float = 128.0, grad_comm: str | None = None):
         if not isinstance(optimizer, torch.optim.Adam):
             raise TypeError("zero_amd ShardedOptimizer wraps torch.optim.Adam / AdamW")
         self.optimizer = optimizer
@@ -528,6 +536,14 @@ class ShardedOptimizer:
         self.world_size, self.rank = world_size, rank
         self.update = bool(update)
         self._sync = sync
+        # grad_comm="bf16" (update mode, fp32 params): full grads are converted to bf16 before the
+        # reduce-scatter, so the exchange moves 2 B per element; opt-in
+        if grad_comm not in (None, "bf16"):
+            raise ValueError(f"grad_comm must be None or 'bf16' (got {grad_comm!r})")
+        if grad_comm and not update:
+            raise ValueError("grad_comm='bf16' applies to update mode (reference mode keeps the "
+                             "reference's fp32 all-reduce)")
+        self._grad_comm = grad_comm if self.params[0].dtype == torch.float32 else None
 
         dev = self.params[0].device
         if dev.type != "cuda":
@@ -582,7 +598,8 @@ class ShardedOptimizer:
         self._lo = state[2 * L:].view(torch.int16)[:L] if split else None
         self._vmax = None
         self._split = split
-        self._G = torch.zeros(L, dtype=ar.dtype, device=ar.device) if self.world_size > 1 else None
+        gdt = torch.bfloat16 if self._grad_comm else ar.dtype
+        self._G = torch.zeros(L, dtype=gdt, device=ar.device) if self.world_size > 1 else None
         self._steps = np.zeros(len(self.params), np.int64)
         self._adam_cache = {}
         self._retired = []
@@ -642,7 +659,7 @@ class ShardedOptimizer:
         so = ar.slot[idx].astype(np.uint64)
         rows = np.zeros((len(idx), 9), np.uint64)
         if self.world_size > 1:
-            rows[:, 0] = np.uint64(self._G.data_ptr()) + so * np.uint64(es)
+            rows[:, 0] = np.uint64(self._G.data_ptr()) + so * np.uint64(self._G.element_size())
         else:
             rows[:, 0] = [red.local_grads[i].data_ptr() for i in idx]
         pp = np.uint64(ar.P.data_ptr()) + so * np.uint64(es)
@@ -685,8 +702,10 @@ class ShardedOptimizer:
                 if hit is None or hit[0] != sub.tobytes():
                     if hit is not None:  # keep until the device is idle (hipFree would sync it)
                         self._retired.append(hit[1])
+                    gz = ZS_BF16 if (self._split or (self._grad_comm and self.world_size > 1)) \
+                        else ZS_F32
                     hit = (sub.tobytes(), AdamSet(sub, ZS_BF16, ZS_BF16_SPLIT) if self._split
-                           else AdamSet(sub, ZS_F32))
+                           else AdamSet(sub, gz))
                     self._adam_cache[ck] = hit
                 h = hps[int(key[0])]
                 hp = adam_hparams(h["lr"], h["beta1"], h["beta2"], h["eps"], h["weight_decay"],

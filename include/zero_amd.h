@@ -154,6 +154,12 @@ int zs_copyset_destroy(zs_copyset* cs);
  * of two, which is exact); bf16: computed in fp32, rounded to nearest even. */
 int zs_scale(void* x, int64_t n, int dtype, double div, uintptr_t stream);
 
+/* n elements fp32 -> bf16 (round to nearest even, NaN stays NaN) or bf16 -> fp32 (exact).  The
+ * bf16 gradient exchange of fp32-parameter models: the reference reduces fp32
+ * grads (zero2.py:107); converting them first halves the bytes every collective moves.  16-B
+ * vector path when both buffers are 16-byte aligned, scalar otherwise. */
+int zs_convert(const void* src, int src_dtype, void* dst, int dst_dtype, int64_t n, uintptr_t stream);
+
 /* Row-wise fp8 (OCP E4M3, the gfx950 format) quantisation for the low-precision parameter
  * all-gather (the reference's torchao float8 all-gather, fp8/fp8_benchmark.py:79-81).
  * Row r of src (row_len elements, dtype ZS_F32 / ZS_BF16): amax = max|x|, inv = 448/amax,

@@ -130,8 +130,13 @@ def _sum_ranks(arrs):
     return acc
 
 
+def bf16_round(x):
+    """fp32 → bf16 (round to nearest even) → fp32."""
+    return bf16_bits_to_f32(f32_to_bf16_bits(np.asarray(x, F32))).reshape(np.shape(x))
+
+
 def simulate(variant: int, ws: int, init, xs=None, ys=None, steps: int = 10, lr: float = 1e-3,
-             local_grads=None, adam_kw=None, zero_grad: str = "optimizer"):
+             local_grads=None, adam_kw=None, zero_grad: str = "optimizer", grad_comm=None):
     """Restate a ``steps``-long run of reference ZeRO-``variant`` at world size ``ws``.
 
     init: list of fp32 param arrays (identical on every rank, torch.manual_seed(0) in the fixture).
@@ -143,6 +148,9 @@ def simulate(variant: int, ws: int, init, xs=None, ys=None, steps: int = 10, lr:
     zero_grad: what the training loop clears before each backward — "optimizer" (the
              reference harness: ShardedOptimizer.zero_grad(), owned grads only, zero1.py:107-108)
              or "model" (model.zero_grad(): every grad, so nothing carries over).
+    grad_comm: None, or "bf16" (variant 2 only): the build's bf16 gradient exchange of fp32
+             params — every rank's grad rounded to bf16, summed in fp32, the sum rounded to bf16
+             (a reduce that accumulates in fp32 and delivers bf16).  Not a reference behaviour.
     Returns dict with per-step params per rank, per-step reduced grads per rank (list in the
     reference's collective order), and final Adam state per rank.
     """
@@ -179,7 +187,11 @@ def simulate(variant: int, ws: int, init, xs=None, ys=None, steps: int = 10, lr:
         elif variant == 2:  # zero2.py:94-113: reduce_scatter of ws copies == all-reduce; owner /ws
             own_grad = [dict() for _ in range(ws)]
             for i in range(n):
-                ssum = _sum_ranks([held[r][i].reshape(-1) for r in range(ws)])
+                if grad_comm == "bf16":
+                    ssum = bf16_round(_sum_ranks([bf16_round(held[r][i].reshape(-1))
+                                                  for r in range(ws)]))
+                else:
+                    ssum = _sum_ranks([held[r][i].reshape(-1) for r in range(ws)])
                 for r in range(ws):
                     s, e = owner_range(n, ws, r)
                     if s <= i < e:

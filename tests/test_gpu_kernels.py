@@ -346,3 +346,35 @@ def test_pack_unpack_through_plan_bit_exact(gpu, dtype):
         torch.cuda.synchronize()
         for g, o in zip(grads, outs):
             assert torch.equal(o, torch.zeros_like(o) if g is None else g)
+
+
+@pytest.mark.parametrize("n", [1, 7, 8, 1000, 4099, 1 << 20])
+@pytest.mark.parametrize("offset", [0, 1])
+def test_convert_fp32_bf16_bit_exact(gpu, n, offset):
+    """zs_convert fp32 → bf16 is round-to-nearest-even bit for bit (numpy restatement), including
+    ties, subnormals, the overflow edge and infinities; NaN stays NaN; bf16 → fp32 is exact.
+    offset 1 makes the buffers unaligned (scalar path)."""
+    from oracle import zero_oracle as zo
+    from zero_amd.kernels import convert
+
+    rng = np.random.default_rng(n + offset)
+    x = (rng.standard_normal(n + offset) * 10.0 ** rng.integers(-40, 39, n + offset)).astype(np.float32)
+    special = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 3.3895314e38, 3.4028235e38, 1e-45,
+                        -1e-40, 1.0 + 2.0 ** -8, 1.0 + 3 * 2.0 ** -8, 1.0 + 2.0 ** -8 + 2.0 ** -20],
+                       np.float32)
+    k = min(len(special), n)
+    x[offset:offset + k] = special[:k]
+    src = torch.from_numpy(x).to(gpu)[offset:]
+    dst = torch.empty(n + offset, dtype=torch.bfloat16, device=gpu)[offset:]
+    convert(src, dst)
+    torch.cuda.synchronize()
+    got = dst.view(torch.int16).cpu().numpy().view(np.uint16)
+    want = zo.f32_to_bf16_bits(x[offset:])
+    nan = np.isnan(x[offset:])
+    assert np.array_equal(got[~nan], want[~nan])
+    assert np.isnan(zo.bf16_bits_to_f32(got[nan])).all()
+    back = torch.empty(n + offset, dtype=torch.float32, device=gpu)[offset:]
+    convert(dst, back)
+    torch.cuda.synchronize()
+    b = back.cpu().numpy()
+    assert np.array_equal(b[~nan].view(np.uint32), zo.bf16_bits_to_f32(got[~nan]).view(np.uint32))

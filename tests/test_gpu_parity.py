@@ -312,3 +312,56 @@ def _carry_worker(rank, ws, port, clear):
 @pytest.mark.parametrize("clear", ["optimizer", "model"])
 def test_zero1_carry_follows_zero_grad(gpu, clear):
     spawn_ranks(_carry_worker, 3, (3, _port(), clear))
+
+
+def _bf16comm_worker(rank, ws, port, which):
+    """grad_comm="bf16" (SURVEY.md §8(f) 4): fp32 params, fp32 grads converted to bf16 for the
+    exchange.  The trajectory follows the oracle's emulation of that exchange (each rank's grad
+    rounded to bf16, summed, the sum rounded to bf16) within summation-order noise, and stays
+    within 2e-2 of the reference's fp32 trajectory (the price of bf16 gradients; opt-in)."""
+    import sys
+    from conftest import PKG, REPO  # noqa: F401
+    from _gloo_comm import GlooStagedComm
+    from oracle import zero_oracle as zo
+    from zero_amd import zero2, zero3
+
+    torch.cuda.set_device(0)
+    init_pg(rank, ws, port)
+    dev = torch.device("cuda:0")
+    z = np.load(GOLDEN / f"traj_z2_ws{ws}_d16_distinct.npz")
+    init = [z[f"init_{i}"] for i in range(12)]
+    want = zo.simulate(2, ws, init, local_grads=lambda t, r, i: z[f"r{r}_t{t}_lg{i}"], grad_comm="bf16")
+    params = [torch.nn.Parameter(torch.from_numpy(a.copy()).to(dev)) for a in init]
+    if which == "zero2":
+        opt = zero2.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=GlooStagedComm(),
+                                     bucket_mb=ws * 64 * 4 / (1 << 20), grad_comm="bf16")
+        assert opt.engine.R.dtype == torch.bfloat16
+    else:
+        opt = zero3.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), update=True,
+                                     comm=GlooStagedComm(), grad_comm="bf16")
+        assert opt.grad_arena().dtype == torch.bfloat16
+    cs = lambda a: a if which == "zero2" else a[rank * -(-a.shape[0] // ws):(rank + 1) * -(-a.shape[0] // ws)]  # noqa: E731
+    for t in range(int(z["steps"])):
+        opt.zero_grad()
+        for i, p in enumerate(params):
+            g = torch.from_numpy(z[f"r{rank}_t{t}_lg{i}"].copy()).to(dev)
+            if which == "zero2":
+                set_grad(p, g)
+            else:  # a full-size grad on a sharded param, as autograd leaves it
+                shard = p.data
+                p.data = torch.empty(g.shape, device=dev)
+                p.grad = g
+                p.data = shard
+        opt.step()
+        for i, p in enumerate(params):
+            got = p.detach().cpu().numpy()
+            assert rel(got, cs(want["params"][t][rank][i])) <= 1e-4, (which, rank, t, i)
+            assert rel(got, cs(z[f"r{rank}_t{t}_p{i}"])) <= 2e-2, (which, rank, t, i)
+    dist.barrier()
+    dist.destroy_process_group()
+    sys.stdout.flush()
+
+
+@pytest.mark.parametrize("which,ws", [("zero2", 3), ("zero2", 4), ("zero3", 3), ("zero3", 4)])
+def test_bf16_gradient_exchange_for_fp32_params(gpu, which, ws):
+    spawn_ranks(_bf16comm_worker, ws, (ws, _port(), which))
