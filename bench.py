@@ -821,18 +821,28 @@ def bench_zero3_paramset(args, world, rank, dev, use_nccl):
 def bench_train_smollm3(args, world, rank, dev, use_nccl):
     """SmolLM3-3B training (fsdp/train_fsdp.py's loop on random-init weights and synthetic
     tokens): tokens/s over all ranks (per-rank batch fixed → weak scaling) and the reference's
-    MFU accounting.  Optimizer: zero2.ShardedOptimizer(AdamW(lr=1e-5), overlap=True)."""
+    MFU accounting.  Optimizer: zero2.ShardedOptimizer(AdamW(lr=1e-5), overlap=True) — the FSDP2
+    reshard_after_forward=False analogue — or, with --zero 3, zero3.ShardedOptimizer(AdamW,
+    update=True) with the gather / release hooks on every module (reshard_after_forward=True,
+    train_fsdp.py:92-94)."""
     import torch
     import torch.distributed as dist
 
-    from zero_amd import zero2
+    from zero_amd import zero2, zero3
     from zero_amd.training_utils import smollm3 as sm
 
     cfg = sm.smollm3_config(layers=args.train_layers)
     model = sm.build_model(cfg, dev)
     params = sum(p.numel() for p in model.parameters())
-    opt = zero2.ShardedOptimizer(torch.optim.AdamW(model.parameters(), lr=1e-5), overlap=True,
-                                 sync=False)
+    if args.zero == 3:
+        comm, _ = _zero3_comm(args, world, rank, dev)
+        kw = {} if comm is None else {"comm": comm}
+        opt = zero3.ShardedOptimizer(torch.optim.AdamW(model.parameters(), lr=1e-5), update=True,
+                                     sync=False, bucket_mb=args.bucket_mb or 128.0, **kw)
+        zero3.register_zero3_hooks(model, opt.param_managers)
+    else:
+        opt = zero2.ShardedOptimizer(torch.optim.AdamW(model.parameters(), lr=1e-5), overlap=True,
+                                     sync=False)
     batch = args.batch or 1
     g = torch.Generator(device=dev).manual_seed(42 + rank)  # each rank its own data shard
     ids = torch.randint(0, cfg.vocab_size, (batch, args.seq), device=dev, generator=g)
@@ -858,12 +868,16 @@ def bench_train_smollm3(args, world, rank, dev, use_nccl):
     fpt = sm.model_flops_per_token(cfg, args.seq)
     if rank == 0:
         print(json.dumps({
-            "metric": "SmolLM3-3B ZeRO-2 training throughput (SURVEY §8(f) 3; not the headline)",
+            "metric": f"SmolLM3-3B ZeRO-{3 if args.zero == 3 else 2} training throughput "
+                      "(SURVEY §8(f) 3; not the headline)",
             "value": tok_s, "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random tokens, random init)",
-            "config": {"workload": "SmolLM3 causal-LM training step, ZeRO-2 AdamW(lr=1e-5) "
-                                   "backward-overlapped", "params": int(params),
+            "config": {"workload": ("SmolLM3 causal-LM training step, ZeRO-3 AdamW(lr=1e-5), "
+                                    "per-module gathers, backward reduce-scatters"
+                                    if args.zero == 3 else
+                                    "SmolLM3 causal-LM training step, ZeRO-2 AdamW(lr=1e-5) "
+                                    "backward-overlapped"), "params": int(params),
                        "layers": cfg.num_hidden_layers, "seq_len": args.seq,
                        "global_batch": world * batch, "parallelism": f"dp{world}"},
             "mfu_flops_per_token": fpt,

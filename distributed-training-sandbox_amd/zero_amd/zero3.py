@@ -306,6 +306,11 @@ def register_zero3_hooks(model, param_managers):
 
     handles = []
     for m in model.modules():
+        # the reference hooks every module (zero3.py:73-77); a module without managed parameters
+        # has nothing to gather or release, so it is left unhooked (a full backward hook would
+        # only wrap its inputs and outputs in autograd nodes for nothing)
+        if not mod_managers[id(m)]:
+            continue
         handles.append(m.register_forward_pre_hook(make_pre("fwd")))
         handles.append(m.register_forward_hook(post_hook))
         handles.append(m.register_full_backward_pre_hook(make_pre("bwd")))

@@ -365,3 +365,55 @@ def _bf16comm_worker(rank, ws, port, which):
 @pytest.mark.parametrize("which,ws", [("zero2", 3), ("zero2", 4), ("zero3", 3), ("zero3", 4)])
 def test_bf16_gradient_exchange_for_fp32_params(gpu, which, ws):
     spawn_ranks(_bf16comm_worker, ws, (ws, _port(), which))
+
+
+def _comm_time_worker(rank, ws, port):
+    """The counters mean what the reference's mean: ZeRO-1 never counts
+    communication (zero1.py:67-68); ZeRO-2 counts from step() entry to the end of the gradient
+    reduction (zero2.py:92,116) — part of, never more than, step_time; ZeRO-3 likewise for its
+    shard all-reduce (zero3.py:125,158)."""
+    import sys
+    from conftest import PKG, REPO  # noqa: F401
+    from _gloo_comm import GlooStagedComm
+    from zero_amd import zero1, zero2, zero3
+
+    torch.cuda.set_device(0)
+    init_pg(rank, ws, port)
+    dev = torch.device("cuda:0")
+    shapes = [(256, 64), (256,), (64, 32)]
+
+    def run(make, steps=3, full_grads=False):
+        g = torch.Generator().manual_seed(3)
+        params = [torch.nn.Parameter(torch.randn(s, generator=g).to(dev)) for s in shapes]
+        opt = make(params)
+        for _ in range(steps):
+            opt.zero_grad()
+            for p, s in zip(params, shapes):
+                gr = torch.randn(s, generator=g).to(dev)
+                if full_grads and gr.shape != p.shape:
+                    shard = p.data
+                    p.data = torch.empty(gr.shape, device=dev)
+                    p.grad = gr
+                    p.data = shard
+                else:
+                    set_grad(p, gr)
+            opt.step()
+        torch.cuda.synchronize()
+        return opt
+
+    o1 = run(lambda ps: zero1.ShardedOptimizer(torch.optim.Adam(ps), comm=GlooStagedComm()))
+    assert o1.communication_time == 0.0 and o1.step_time > 0
+    for arena in ("flat", "buckets"):
+        o2 = run(lambda ps: zero2.ShardedOptimizer(torch.optim.Adam(ps), comm=GlooStagedComm(),
+                                                   arena=arena))
+        assert 0.0 < o2.communication_time <= o2.step_time, (arena, o2.communication_time, o2.step_time)
+    o3 = run(lambda ps: zero3.ShardedOptimizer(torch.optim.Adam(ps), comm=GlooStagedComm()),
+             full_grads=True)
+    assert 0.0 < o3.communication_time <= o3.step_time
+    dist.barrier()
+    dist.destroy_process_group()
+    sys.stdout.flush()
+
+
+def test_timing_counters_follow_reference(gpu):
+    spawn_ranks(_comm_time_worker, 2, (2, _port()))

@@ -52,3 +52,80 @@ def test_smollm3_zero2_adamw_overlap_bit_exact(gpu):
             assert torch.isfinite(loss)
     finally:
         dist.destroy_process_group()
+
+
+def _zero3_smollm3(rank, ws, port, dev):
+    """One rank of a SmolLM3 ZeRO-3 run (update mode, AdamW, hooks on every module with
+    parameters).  Every rank trains on the SAME batch, so the reduce-scattered sum of a chunk is
+    exactly ws times this rank's own gradient and the mean is exact: each rank's chunks then equal
+    the C oracle's split-master AdamW of its own full gradient (captured by a hook registered
+    before the optimizer's), bit for bit, every step."""
+    from oracle import c_oracle
+    from zero_amd import zero3
+    from zero_amd.training_utils import smollm3 as sm
+
+    cfg = sm.smollm3_config(layers=2, hidden=128, intermediate=256, heads=4, kv_heads=2, vocab=512)
+    model = sm.build_model(cfg, dev)
+    params = list(model.parameters())
+    full = {}  # full gradient of every param as backward produced it (before the reduce-scatter)
+    for i, p in enumerate(params):
+        p.register_post_accumulate_grad_hook(
+            lambda q, i=i: full.__setitem__(i, q.grad.detach().reshape(-1).view(torch.int16)
+                                            .cpu().numpy().view(np.uint16).copy()))
+    lr, wd = 1e-3, 0.01
+    kw = {}
+    if ws > 1:
+        from _gloo_comm import GlooStagedComm
+
+        kw["comm"] = GlooStagedComm()
+    opt = zero3.ShardedOptimizer(torch.optim.AdamW(params, lr=lr, weight_decay=wd), update=True,
+                                 bucket_mb=0.05, **kw)
+    zero3.register_zero3_hooks(model, opt.param_managers)
+    ar = opt._arena
+    hi, lo, m, v = [], [], [], []
+    for i, p in enumerate(params):
+        x = p.detach().reshape(-1).view(torch.int16).cpu().numpy().view(np.uint16).copy()
+        hi.append(x)
+        lo.append(np.zeros_like(x))
+        m.append(np.zeros(x.size, np.float32))
+        v.append(np.zeros(x.size, np.float32))
+    g = torch.Generator(device=dev).manual_seed(1)
+    ids = torch.randint(0, cfg.vocab_size, (2, 64), device=dev, generator=g)
+    for t in range(1, 4):
+        full.clear()
+        loss = sm.train_step(model, opt, ids)
+        assert torch.isfinite(loss) and len(full) == len(params)
+        hp = c_oracle.hparams(lr=lr, weight_decay=wd, step=t, decoupled=True)
+        for i, p in enumerate(params):
+            r0, r1, row = ar.rows[i]
+            gch = full[i][r0 * row:r1 * row].copy()
+            c_oracle.adam_bf16_split(hi[i], lo[i], gch, m[i], v[i], hp)
+            got = p.detach().reshape(-1).view(torch.int16).cpu().numpy().view(np.uint16)
+            assert np.array_equal(got, hi[i]), (rank, t, i)
+    assert opt.runtime.n_prefetch_hits > 0
+
+
+def test_smollm3_zero3_adamw_bit_exact(gpu):
+    """SURVEY.md §8(f) 3, the ZeRO-3 half (fsdp/train_fsdp.py:92-94 reshard_after_forward=True)."""
+    init_pg(0, 1, 29657)
+    try:
+        _zero3_smollm3(0, 1, None, gpu)
+    finally:
+        dist.destroy_process_group()
+
+
+def _mr_zero3(rank, ws, port):
+    torch.cuda.set_device(0)
+    init_pg(rank, ws, port)
+    try:
+        _zero3_smollm3(rank, ws, port, torch.device("cuda:0"))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_smollm3_zero3_two_ranks_bit_exact(gpu):
+    from conftest import free_port
+    from _zero_run import spawn_ranks
+
+    spawn_ranks(_mr_zero3, 2, (2, free_port()))
