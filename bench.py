@@ -41,10 +41,53 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(shapes, sample_elems: int, min_seconds: float = 10.0, split: bool = True):
-    """The C oracle (oracle/adam_oracle.c, a restatement of torch.optim.Adam + ZeRO /ws) doing the
-    same N=1 ZeRO-2 step (bf16 grads → fp32 master (split: bf16 param + int16 residual) and m/v →
-    bf16 params) on a bounded sample."""
+def cpu_baseline(shapes, sample_elems: int, variant: int = 2, min_seconds: float = 10.0):
+    """SURVEY.md §8(d) CPU baseline (2): the reference's own ZeRO step algorithm restated on the
+    host cores — per-tensor flatten / cat x ws / gloo reduce_scatter_tensor, /ws on the owner,
+    torch.optim.Adam on CPU (single-tensor path, fp32 as the reference), per-tensor broadcast
+    (oracle/zero_cpu_step.py, checked against the reference's trajectories by
+    tests/test_oracle.py) — on a bounded sample: the leading tensors of the set, fp32."""
+    import numpy as np
+    import torch
+
+    from oracle.zero_cpu_step import ReferenceStepCPU
+
+    sel, n = [], 0
+    for s in shapes:
+        k = int(np.prod(s))
+        if n + k > sample_elems and sel:
+            break
+        n += k
+        sel.append(s)
+    g = torch.Generator().manual_seed(0)
+    ps = [torch.nn.Parameter(torch.randn(s, generator=g) * 0.02) for s in sel]
+    grads = [torch.randn(s, generator=g) * 1e-3 for s in sel]
+    opt = ReferenceStepCPU(ps, variant=variant if variant in (1, 2) else 2)
+
+    def one():
+        opt.zero_grad()
+        for p, gr in zip(ps, grads):
+            p.grad = gr.clone() if p.grad is None else p.grad.add_(gr)
+        opt.step()
+
+    one()  # Adam state allocation outside the timing
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        one()
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= min_seconds or steps >= 100:
+            break
+    return dict(value=n * steps / el, unit="params/s", cores=torch.get_num_threads(), kind="port",
+                sample=f"first {n:,} params ({len(sel)} leading tensors of the set, fp32), "
+                       f"{steps} steps of the reference's ZeRO-{variant if variant in (1, 2) else 2} "
+                       f"step restated on CPU (per-tensor gloo collectives + torch.optim.Adam, "
+                       f"oracle/zero_cpu_step.py), {el:.1f} s; torch {torch.__version__}")
+
+
+def cpu_oracle_adam(shapes, sample_elems: int, min_seconds: float = 6.0, split: bool = True):
+    """The C oracle (oracle/adam_oracle.c, OpenMP) doing the N=1 bf16 update on a bounded sample:
+    the fastest CPU restatement of the arithmetic itself, for scale (not the baseline)."""
     import numpy as np
 
     from oracle import c_oracle
@@ -76,9 +119,7 @@ def cpu_baseline(shapes, sample_elems: int, min_seconds: float = 10.0, split: bo
         if el >= min_seconds or steps >= 200:
             break
     return dict(value=n * steps / el, unit="params/s", cores=c_oracle.num_threads(), kind="port",
-                sample=f"first {n:,} params (leading {ntens} tensors of the set), "
-                       f"{steps} steps of the ws=1 ZeRO-2 step (bf16 grads, fp32 m/v, "
-                       f"{'split' if split else 'fp32'} master, bf16 params out) by "
+                sample=f"first {n:,} params, {steps} steps of the bf16 update by "
                        f"oracle/adam_oracle.c, {el:.1f} s")
 
 
@@ -309,40 +350,6 @@ def comm_sweep(comm, arena, world, red_dev, sizes_mb=(4, 16, 64, 256), iters=5):
     torch.cuda.synchronize()
     arena.zero_()  # the sweep scribbled over the arena; padding must stay zero
     return rows
-
-
-def cpu_reference_adam(shapes, sample_elems: int, min_seconds: float = 8.0):
-    """The reference's own inner optimizer on the host: torch.optim.Adam on CPU (the math
-    zero2.py:120 runs on its owned params; single-tensor CPU path of torch/optim/adam.py) over the
-    same leading tensors as cpu_baseline, fp32 params + grads (the reference is fp32-only)."""
-    import numpy as np
-    import torch
-
-    n = 0
-    sel = []
-    for s in shapes:
-        k = int(np.prod(s))
-        if n + k > sample_elems and sel:
-            break
-        n += k
-        sel.append(s)
-    g = torch.Generator().manual_seed(0)
-    ps = [torch.nn.Parameter(torch.randn(s, generator=g) * 0.02) for s in sel]
-    for p in ps:
-        p.grad = torch.randn(p.shape, generator=g) * 1e-3
-    opt = torch.optim.Adam(ps, lr=1e-3)
-    opt.step()  # state allocation outside the timing
-    steps, t0 = 0, time.perf_counter()
-    while True:
-        opt.step()
-        steps += 1
-        el = time.perf_counter() - t0
-        if el >= min_seconds or steps >= 100:
-            break
-    return dict(value=n * steps / el, unit="params/s", cores=torch.get_num_threads(),
-                kind="reference-inner-optimizer",
-                sample=f"torch.optim.Adam (CPU, fp32) over the first {n:,} params "
-                       f"({len(sel)} tensors), {steps} steps, {el:.1f} s; torch {torch.__version__}")
 
 
 class _NoComm:
@@ -1239,9 +1246,9 @@ def main():
         if copy_kernels is not None:
             out["copy_kernels"] = copy_kernels
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(shapes, args.cpu_sample,
-                                               split=args.dtype == "bf16" and args.master == "split")
-            out["cpu_reference_adam"] = cpu_reference_adam(shapes, args.cpu_sample)
+            out["cpu_baseline"] = cpu_baseline(shapes, args.cpu_sample, variant=args.zero)
+            out["cpu_oracle_adam"] = cpu_oracle_adam(
+                shapes, args.cpu_sample, split=args.dtype == "bf16" and args.master == "split")
         print(json.dumps(out), flush=True)
     _teardown(opt)
     dist.destroy_process_group()

@@ -191,3 +191,44 @@ def test_split_master_adam_tracks_fp32_master():
     assert diff.mean() < 1e-3
     assert np.max(np.abs(joined - master)) <= 4 * np.max(np.spacing(np.abs(master)))
     assert np.mean(hi != p_ref) < 1e-3
+
+
+def _cpu_step_worker(rank, ws, port, variant, name):
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from oracle.zero_cpu_step import ReferenceStepCPU
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    z = np.load(GOLDEN / name)
+    params = [torch.nn.Parameter(torch.from_numpy(z[f"init_{i}"].copy())) for i in range(12)]
+    opt = ReferenceStepCPU(params, variant=variant)
+    for t in range(int(z["steps"])):
+        opt.zero_grad()
+        for i, p in enumerate(params):  # backward accumulates into a surviving grad (carry)
+            g = torch.from_numpy(z[f"r{rank}_t{t}_lg{i}"].copy())
+            p.grad = g if p.grad is None else p.grad + g
+        opt.step()
+        if f"r{rank}_t{t}_p0" in z.files:
+            for i, p in enumerate(params):
+                ref = z[f"r{rank}_t{t}_p{i}"]
+                assert np.max(np.abs(p.detach().numpy() - ref)) <= 1e-6 * np.max(np.abs(ref)), (t, i)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("variant,ws", [(1, 2), (2, 2), (1, 3), (2, 4)])
+def test_cpu_reference_step_restatement(variant, ws):
+    """oracle/zero_cpu_step.py (bench.py's cpu_baseline: the reference's per-tensor gloo step +
+    torch.optim.Adam on the host cores) reproduces the reference's own trajectories."""
+    import torch.multiprocessing as mp
+
+    from conftest import free_port
+
+    mp.spawn(_cpu_step_worker, args=(ws, free_port(), variant, f"traj_z{variant}_ws{ws}_d16_distinct.npz"),
+             nprocs=ws, join=True)
