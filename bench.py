@@ -846,7 +846,8 @@ def bench_train_smollm3(args, world, rank, dev, use_nccl):
         kw = {} if comm is None else {"comm": comm}
         opt = zero3.ShardedOptimizer(torch.optim.AdamW(model.parameters(), lr=1e-5), update=True,
                                      sync=False, bucket_mb=args.bucket_mb or 128.0, **kw)
-        zero3.register_zero3_hooks(model, opt.param_managers)
+        # one gather group per decoder layer (FSDP2 fully_shard per block, train_fsdp.py:90-97)
+        zero3.register_zero3_hooks(model, opt.param_managers, units=list(model.model.layers))
     else:
         opt = zero2.ShardedOptimizer(torch.optim.AdamW(model.parameters(), lr=1e-5), overlap=True,
                                      sync=False)

@@ -46,17 +46,25 @@ def _ptr(t: torch.Tensor | None) -> int:
 
 
 PROBE_MIN_BYTES = 1 << 30
+# An in-place stream over an allocation in MI355X's fast VRAM region runs at ~6.2-6.3 TB/s (the
+# guide's float4 copy: 6.29); in the slow regions at ~5.2 (profiles/r02_alloc/).  A candidate at or
+# above this is kept at once, without allocating the remaining ones.
+PROBE_ACCEPT_GBS = 5950.0
 
 
-def probed_zeros(n: int, dtype, device, tries: int = 5):
+def probed_zeros(n: int, dtype, device, tries: int = 5, accept_gbs: float = PROBE_ACCEPT_GBS):
     """A zero-filled buffer for a long-lived, bandwidth-bound stream, placed by measurement.
 
-    The same C4 Adam launch over different allocations of its state measured 13.9 ms on some and
-    15.1-15.6 ms on others in one process, and an in-place copy over the allocation alone predicts
-    which (6.26 vs 5.3-5.7 TB/s; profiles/r01_alloc_probe.log).  So for buffers of 1 GiB or more,
-    up to ``tries`` candidates are allocated (each while the previous ones are still held, so each
-    is new memory), streamed once with the gfx950 copy kernel in place, and the fastest is kept;
-    the others go back to torch's caching allocator.  Skipped when free memory is short.
+    Streaming bandwidth depends on WHERE in VRAM an allocation lands, stably per allocation:
+    8-GiB buffers allocated one after another on one box streamed at 5.2 TB/s up to ~96 GiB of
+    allocated VRAM, 6.3 TB/s between ~96 and ~160 GiB, 5.2 again above (profiles/r02_alloc/
+    alloc_pos8.jsonl); the same launch re-measured later, or after 3 s of warm streaming, keeps its
+    speed (alloc_tlb2.jsonl: not a clock effect), and the fast buffers do not translate better
+    (they see MORE UTCL1 misses; identical DRAM request counts — pmc_pass*.json).  So for buffers
+    of 1 GiB or more, candidates are allocated (each while the previous ones are still held, so
+    each is new memory) and streamed once in place by the gfx950 copy kernel; the first at
+    ``accept_gbs`` or above is kept at once, otherwise the fastest of ``tries``; the rejected
+    ones are handed back to the device.  Skipped when free memory is short.
     Returns (buffer, info dict)."""
     nbytes = n * torch.empty((), dtype=dtype).element_size()
     info = {"tries": 1, "gbs": []}
@@ -81,13 +89,15 @@ def probed_zeros(n: int, dtype, device, tries: int = 5):
         gbs = 2 * nbytes / (e0.elapsed_time(e1) / 1e3) / 1e9
         cands.append((gbs, buf))
         info["gbs"].append(round(gbs, 1))
+        if gbs >= accept_gbs:
+            break
     best = max(range(len(cands)), key=lambda i: cands[i][0])
     buf = cands[best][1]
     del cands, probe
     # hand the rejected candidates back to the device (not just to torch's cache), so later
     # allocations outside torch (RCCL buffers, segment tables) and mem_get_info see them
     torch.cuda.empty_cache()
-    info.update(tries=tries, chosen=best)
+    info.update(tries=len(info["gbs"]), chosen=best, accept_gbs=accept_gbs)
     return buf, info
 
 

@@ -269,13 +269,33 @@ class Zero3ParamManager:
         self.full_data = None
 
 
-def register_zero3_hooks(model, param_managers):
+def register_zero3_hooks(model, param_managers, units=None):
     """zero3.py:56-77: forward / backward pre-hooks materialise a module's direct parameters (one
-    grouped all-gather, prefetched on the side stream), post-hooks release them."""
+    grouped all-gather, prefetched on the side stream), post-hooks release them.
+
+    ``units`` (an extension; None = the reference's per-module hooks): modules gathered as ONE
+    group each — every managed parameter anywhere inside a unit is materialised by the unit's
+    pre-hooks and released by its post-hooks, as FSDP2's ``fully_shard`` of each transformer block
+    does (fsdp/train_fsdp.py:90-97).  One RCCL group and four hooks per block instead of per
+    Linear / norm.  Modules outside every unit keep per-module gathers of their direct params."""
     runtimes = {m.runtime for m in param_managers.values() if m.runtime is not None}
     mod_managers = {}
+    covered = set()
+    unit_ids = set()
+    for u in units or ():
+        ms, seen = [], set()
+        for p in u.parameters():
+            if p in param_managers and id(p) not in seen:
+                seen.add(id(p))
+                ms.append(param_managers[p])
+        mod_managers[id(u)] = ms
+        unit_ids.add(id(u))
+        covered |= seen
     for mod in model.modules():
-        ms = [param_managers[p] for _, p in mod.named_parameters(recurse=False) if p in param_managers]
+        if id(mod) in unit_ids:
+            continue
+        ms = [param_managers[p] for _, p in mod.named_parameters(recurse=False)
+              if p in param_managers and id(p) not in covered]
         mod_managers[id(mod)] = ms
     for rt in runtimes:
         rt.key_managers = {}

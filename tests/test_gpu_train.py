@@ -54,7 +54,7 @@ def test_smollm3_zero2_adamw_overlap_bit_exact(gpu):
         dist.destroy_process_group()
 
 
-def _zero3_smollm3(rank, ws, port, dev):
+def _zero3_smollm3(rank, ws, port, dev, units=False):
     """One rank of a SmolLM3 ZeRO-3 run (update mode, AdamW, hooks on every module with
     parameters).  Every rank trains on the SAME batch, so the reduce-scattered sum of a chunk is
     exactly ws times this rank's own gradient and the mean is exact: each rank's chunks then equal
@@ -80,7 +80,8 @@ def _zero3_smollm3(rank, ws, port, dev):
         kw["comm"] = GlooStagedComm()
     opt = zero3.ShardedOptimizer(torch.optim.AdamW(params, lr=lr, weight_decay=wd), update=True,
                                  bucket_mb=0.05, **kw)
-    zero3.register_zero3_hooks(model, opt.param_managers)
+    zero3.register_zero3_hooks(model, opt.param_managers,
+                               units=list(model.model.layers) if units else None)
     ar = opt._arena
     hi, lo, m, v = [], [], [], []
     for i, p in enumerate(params):
@@ -114,18 +115,20 @@ def test_smollm3_zero3_adamw_bit_exact(gpu):
         dist.destroy_process_group()
 
 
-def _mr_zero3(rank, ws, port):
+def _mr_zero3(rank, ws, port, units):
     torch.cuda.set_device(0)
     init_pg(rank, ws, port)
     try:
-        _zero3_smollm3(rank, ws, port, torch.device("cuda:0"))
+        _zero3_smollm3(rank, ws, port, torch.device("cuda:0"), units)
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-def test_smollm3_zero3_two_ranks_bit_exact(gpu):
+@pytest.mark.parametrize("units", [False, True])
+def test_smollm3_zero3_two_ranks_bit_exact(gpu, units):
+    """units=True: one gather group per decoder layer (FSDP2's per-block fully_shard)."""
     from conftest import free_port
     from _zero_run import spawn_ranks
 
-    spawn_ranks(_mr_zero3, 2, (2, free_port()))
+    spawn_ranks(_mr_zero3, 2, (2, free_port(), units))
