@@ -107,8 +107,7 @@ class ShardedOptimizerBase:
             self._build_engine()
 
     def _flat(self) -> bool:
-        return (self._arena == "flat" and self.world_size > 1 and not self._overlap
-                and self._layout == "reference")
+        return self._arena == "flat" and not self._overlap and self._layout == "reference"
 
     def _shard_optimizer_params(self):
         """zero1.py:71-74: drop non-owned params from the inner optimizer's groups."""

@@ -1,4 +1,4 @@
-"""The flat-parameter-arena ZeRO-1/2 step (ws > 1): no pack, no unpack.
+"""The flat-parameter-arena ZeRO-1/2 step: no pack, no unpack.
 
 ``ShardEngine``'s bucket path copies every gradient into a rank-major bucket arena (pack), runs
 the collectives there and copies every parameter back (unpack): at the ws=8 SmolLM3-3B layout
@@ -64,8 +64,6 @@ class FlatEngine(ShardEngine):
     def __init__(self, params, group_of, ws: int, rank: int, *, carry=False, comm=None,
                  bucket_bytes: int = 256 << 20, master: str = "split", placement_tries: int = 5,
                  grad_comm: str | None = None):
-        if ws < 2:
-            raise ValueError("FlatEngine is the ws > 1 exchange; ws == 1 needs no arena")
         # the base class gives the reference layout's streams, the optimizer state and the Adam
         # launch machinery; its bucket plan (one bucket) is unused
         super().__init__(params, group_of, ws, rank, layout="reference", carry=carry, comm=comm,
@@ -105,10 +103,15 @@ class FlatEngine(ShardEngine):
         self.Gc = torch.zeros(total, dtype=cdt, device=dev) if self.grad_comm else self.G
         self.ces = self.Gc.element_size()
         self.czdtype = _lib.ZS_BF16 if self.grad_comm else self.zdtype
-        self.R = torch.zeros(max(int(self.Ls[rank]), ALIGN_ELEMS), dtype=cdt, device=dev)
+        # ws == 1: nothing to reduce — Adam reads the gradient arena itself (R aliases Gc) and the
+        # step is one round with no collective; the arena still places P and G by probe
+        self.R = (self.Gc if ws == 1 else
+                  torch.zeros(max(int(self.Ls[rank]), ALIGN_ELEMS), dtype=cdt, device=dev))
         self.dirty = np.zeros(n, bool)  # G slot may hold a stale gradient
         self.zero_grad_calls = 0
         W = max(ALIGN_ELEMS, (int(bucket_bytes) // (ws * es)) // ALIGN_ELEMS * ALIGN_ELEMS)
+        if ws == 1:
+            W = total
         self.W = W
         self.K = max(1, -(-int(self.Ls.max()) // W))
         self.rounds = [self._make_round(j) for j in range(self.K)]
@@ -297,6 +300,16 @@ class FlatEngine(ShardEngine):
             from .kernels import convert  # of bytes: read 4 + write 2 B per element)
 
             convert(self.G, self.Gc, stream)
+        if self.ws == 1:  # zero1.py:107-108 / zero2.py:120 at ws=1: Adam on the local grads
+            with _lib.phase_range("optimizer_step"):
+                for rd in self.rounds:
+                    if len(rd.idx) and not (hps and self._adam_round_fast(rd, hps, stream)):
+                        live = has[rd.idx]
+                        rows, idx = (rd.rows, rd.idx) if live.all() else (rd.rows[live], rd.idx[live])
+                        self._run_adam(("flat", rd.j), rows, idx, hparams_of, stream,
+                                       carry_mul=cmul[idx])
+            self._reinstall(has, view)
+            return
         self.ev_grads.record(stream)
         cs = self.comm_stream
         cs.wait_event(self.ev_grads)
@@ -327,7 +340,10 @@ class FlatEngine(ShardEngine):
                 self.ev_bc[rd.j].record(cs)
                 self._timed_end(e0, cs, "ag", int(rd.count.sum()))
         stream.wait_event(self.ev_bc[self.K - 1])  # the parameters are P: next forward reads it
-        # every p.grad is (again) its arena view, holding this step's local gradient
+        self._reinstall(has, view)
+
+    def _reinstall(self, has, view):
+        """Every p.grad is (again) its arena view, holding this step's local gradient."""
         for i in np.nonzero(has & ~view)[0]:
             self.params[i].grad = self.grad_view(int(i))
             self._views[i] = self.params[i].grad
@@ -350,6 +366,8 @@ class FlatEngine(ShardEngine):
 
     def comm_time_s(self) -> float:
         """zero2.py:92,116: from step() entry until the gradient reduction is done."""
+        if self.ws == 1:
+            return 0.0
         return max(0.0, self.ev_c0.elapsed_time(self.ev_c1) / 1e3)
 
 
