@@ -825,6 +825,28 @@ def bench_zero3_paramset(args, world, rank, dev, use_nccl):
     dist.destroy_process_group()
 
 
+def _fresh_buffer_gbs(dev, n=16, nbytes=64 << 20):
+    """In-place copy-kernel GB/s of n buffers freshly taken from torch's allocator (diagnostic)."""
+    import torch
+
+    from zero_amd.kernels import CopySet
+
+    bufs = [torch.empty(nbytes // 4, dtype=torch.float32, device=dev) for _ in range(n)]
+    st = torch.cuda.current_stream(dev)
+    out = []
+    for b in bufs:
+        cs = CopySet([b.data_ptr()], [b.data_ptr()], [nbytes])
+        cs.run(st)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(5):
+            cs.run(st)
+        e1.record(st)
+        e1.synchronize()
+        out.append(round(5 * 2 * nbytes / (e0.elapsed_time(e1) / 1e3) / 1e9))
+    return out
+
+
 def bench_train_smollm3(args, world, rank, dev, use_nccl):
     """SmolLM3-3B training (fsdp/train_fsdp.py's loop on random-init weights and synthetic
     tokens): tokens/s over all ranks (per-rank batch fixed → weak scaling) and the reference's
@@ -874,6 +896,11 @@ def bench_train_smollm3(args, world, rank, dev, use_nccl):
     ms = el / args.steps * 1e3
     tok_s = world * batch * args.seq / (ms / 1e3)
     fpt = sm.model_flops_per_token(cfg, args.seq)
+    if os.environ.get("ZERO_AMD_DIAG_BW"):  # diagnostics: streaming GB/s of fresh 64 MB buffers
+        print(json.dumps({"diag_fresh_64mb_copy_gbs": _fresh_buffer_gbs(dev),
+                          "segments": torch.cuda.memory_stats(dev).get("segment.all.current"),
+                          "reserved_gib": torch.cuda.memory_reserved(dev) / (1 << 30)}),
+              file=sys.stderr, flush=True)
     if rank == 0:
         print(json.dumps({
             "metric": f"SmolLM3-3B ZeRO-{3 if args.zero == 3 else 2} training throughput "

@@ -30,6 +30,8 @@ Segment tables are uploaded once and reused while the tensors' addresses stay th
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -68,6 +70,9 @@ def probed_zeros(n: int, dtype, device, tries: int = 5, accept_gbs: float = PROB
     Returns (buffer, info dict)."""
     nbytes = n * torch.empty((), dtype=dtype).element_size()
     info = {"tries": 1, "gbs": []}
+    env = os.environ.get("ZERO_AMD_PROBE_TRIES")  # diagnostics: 1 = plain allocation
+    if env:
+        tries = int(env)
     if tries <= 1 or nbytes < PROBE_MIN_BYTES:
         return torch.zeros(n, dtype=dtype, device=device), info
     free, total = torch.cuda.mem_get_info(device)

@@ -93,6 +93,11 @@ class _GatherRuntime:
         """Enqueue the all-gather of ``managers`` on the side stream; returns immediately."""
         if key in self.pending or not managers:
             return
+        if self.ws == 1 and not any(m.fp8 for m in managers):
+            # the shard is the whole parameter: nothing to gather, no stream to synchronise with
+            self.pending[key] = ([(m, m._gather_prepare(None)[1]) for m in managers], None)
+            self.n_gathers += 1
+            return
         ev_ready = torch.cuda.Event()
         ev_ready.record(torch.cuda.current_stream(self.device))  # shards may just have been updated
         timed = self.gather_events is not None and self.ws > 1
@@ -135,6 +140,10 @@ class _GatherRuntime:
             self.n_prefetch_hits += 1
         self.launch(key, managers)
         out, ev = self.pending.pop(key)
+        if ev is None:  # ws == 1
+            for m, full in out:
+                m._install_full(full)
+            return
         cur = torch.cuda.current_stream(self.device)
         cur.wait_event(ev)
         for m, full in out:
@@ -254,7 +263,8 @@ class Zero3ParamManager:
         rt.launch(key, [self])
         out, ev = rt.pending.pop(key)
         cur = torch.cuda.current_stream(self.shard.device)
-        cur.wait_event(ev)
+        if ev is not None:
+            cur.wait_event(ev)
         for m, full in out:
             full.record_stream(cur)
             m._install_full(full)
@@ -278,6 +288,10 @@ def register_zero3_hooks(model, param_managers, units=None):
     pre-hooks and released by its post-hooks, as FSDP2's ``fully_shard`` of each transformer block
     does (fsdp/train_fsdp.py:90-97).  One RCCL group and four hooks per block instead of per
     Linear / norm.  Modules outside every unit keep per-module gathers of their direct params."""
+    if all(m.world_size == 1 and not m.fp8 for m in param_managers.values()):
+        # one rank: every shard is its whole parameter, so materialize / release are identities —
+        # hooks would only cost host time (a forward whose host enqueue falls behind the GPU)
+        return []
     runtimes = {m.runtime for m in param_managers.values() if m.runtime is not None}
     mod_managers = {}
     covered = set()

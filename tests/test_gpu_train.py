@@ -103,7 +103,7 @@ def _zero3_smollm3(rank, ws, port, dev, units=False):
             c_oracle.adam_bf16_split(hi[i], lo[i], gch, m[i], v[i], hp)
             got = p.detach().reshape(-1).view(torch.int16).cpu().numpy().view(np.uint16)
             assert np.array_equal(got, hi[i]), (rank, t, i)
-    assert opt.runtime.n_prefetch_hits > 0
+    assert ws == 1 or opt.runtime.n_prefetch_hits > 0  # (ws=1: no hooks, nothing to gather)
 
 
 def test_smollm3_zero3_adamw_bit_exact(gpu):

@@ -77,7 +77,7 @@ def _ref_mode(rank, ws, name, dev, comm=None):
                 assert rel(g.cpu().numpy(), z[f"r{rank}_t{t}_red{k}"]) <= 1e-4  # GEMM noise
         for i, p in enumerate(model.parameters()):  # never updated (zero3.py:150-153)
             assert torch.equal(p.detach().cpu(), torch.from_numpy(_chunk(z[f"init_{i}"], ws, rank)))
-    assert opt.runtime.n_prefetch_hits > 0  # the learned order prefetched later gathers
+    assert ws == 1 or opt.runtime.n_prefetch_hits > 0  # learned order prefetched later gathers
     return opt
 
 
@@ -160,7 +160,7 @@ def _update_hooks(rank, ws, name, dev, comm=None):
             for i, p in enumerate(params):
                 want = _chunk(z[f"r{rank}_t{t}_p{i}"], ws, rank)
                 assert rel(p.detach().cpu().numpy(), want) <= 1e-4, (t, i)
-    assert opt.runtime.n_prefetch_hits > 0
+    assert ws == 1 or opt.runtime.n_prefetch_hits > 0  # (ws=1: no hooks, nothing to gather)
     if ws > 1:
         assert opt.communication_time >= 0.0
 

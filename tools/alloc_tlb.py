@@ -43,6 +43,9 @@ def main():
                     help="comma list of GiB: one buffer per size, interleaved rounds")
     ap.add_argument("--rounds", type=int, default=1,
                     help="measure every held buffer round-robin this many times")
+    ap.add_argument("--many", default=None,
+                    help="MiB,count: hold `count` buffers of MiB each (torch allocator and raw "
+                         "hipMalloc), print every buffer's GB/s and address")
     a = ap.parse_args()
 
     import torch
@@ -53,6 +56,8 @@ def main():
     hip.hipExtMallocWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
     hip.hipExtMallocWithFlags.restype = ctypes.c_int
     hip.hipFree.argtypes = [ctypes.c_void_p]
+    hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    hip.hipMalloc.restype = ctypes.c_int
     hip.hipMemset.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
@@ -74,6 +79,43 @@ def main():
         return 2 * nbytes / (best / 1e3) / 1e9
 
     import time
+
+    if a.many:
+        mib, count = (int(x) for x in a.many.split(","))
+        nb = mib << 20
+        for mode in ("torch", "hipMalloc"):
+            held, rows = [], []
+            for k in range(count):
+                if mode == "torch":
+                    t = torch.empty(nb // 4, dtype=torch.float32, device=dev)
+                    held.append(t)
+                    ptr = t.data_ptr()
+                else:
+                    q = ctypes.c_void_p()
+                    if hip.hipMalloc(ctypes.byref(q), ctypes.c_size_t(nb)) != 0:
+                        break
+                    held.append(q)
+                    ptr = q.value
+                cs = CopySet([ptr], [ptr], [nb])
+                cs.run(st)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                for _ in range(10):
+                    cs.run(st)
+                e1.record(st)
+                e1.synchronize()
+                gbs = 10 * 2 * nb / (e0.elapsed_time(e1) / 1e3) / 1e9
+                rows.append((k, ptr, round(gbs)))
+            for k, ptr, gbs in rows:
+                print(json.dumps({"mode": mode, "mib": mib, "k": k, "addr_hex": hex(ptr),
+                                  "addr_mod_2m": ptr % (2 << 20), "gbs": gbs}), flush=True)
+            torch.cuda.synchronize()
+            for h in held:
+                if isinstance(h, ctypes.c_void_p):
+                    hip.hipFree(h)
+            del held
+            torch.cuda.empty_cache()
+        return
 
     if a.sizes:  # buffer-size effect: one buffer per size, each streamed with its own size
         sizes = [int(float(x) * (1 << 30)) // 256 * 256 for x in a.sizes.split(",")]
