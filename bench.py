@@ -437,7 +437,7 @@ def _zero3_report(args, opt, world, rank, red_dev, el, total, workload, extra):
             "zero3": {"gathers_per_step": opt.runtime.n_gathers / (args.steps + args.warmup),
                       "prefetch_hits": opt.runtime.n_prefetch_hits,
                       "reduce_buckets_per_step": opt._reducer.K,
-                      "reduced_in_backward": opt._reducer.launched_in_backward},
+                      "reduced_in_backward": opt._reducer.last_launched_in_backward},
         }
         if comm is not None:
             out["collectives"] = comm
@@ -928,8 +928,9 @@ def bench_train_smollm3(args, world, rank, dev, use_nccl):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # default: ~4 s of timed GPU work at N=1 (C4), long enough for an outside utilisation sampler
+    ap.add_argument("--steps", type=int, default=None, help="default 300 (--train: 4)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 5 (--train: 2)")
     ap.add_argument("--config", default="C4", choices=["C2", "C3", "C4", "C5"])
     ap.add_argument("--zero", type=int, default=2, choices=[1, 2, 3],
                     help="3 on C2/C3 = a ZeRO-3 training iteration (hooked forward/backward + "
@@ -988,6 +989,10 @@ def main():
                     help="end the process (exit 3) with a diagnostic if the run has not finished "
                          "after this many seconds (a collective that never completes)")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 4 if args.train else 300
+    if args.warmup is None:
+        args.warmup = 2 if args.train else 5
     _start_watchdog(args.watchdog_s)
 
     import numpy as np

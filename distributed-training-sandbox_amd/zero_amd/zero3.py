@@ -437,6 +437,8 @@ class _GradReducer:
 
     def reset(self):
         n = len(self.opt.params)
+        # buckets the last backward launched before it ended (the rest: flushed at its end)
+        self.last_launched_in_backward = getattr(self, "launched_in_backward", 0)
         self.pending = self._size.copy()
         self.marked = np.zeros(n, bool)
         self.had_grad = np.zeros(n, bool)
