@@ -379,6 +379,12 @@ class _NoComm:
     def broadcast(self, t, root, stream):
         pass
 
+    def all_gather_group(self, send, recv, count, dtype, stream):
+        pass
+
+    def reduce_scatter_group(self, send, recv, count, dtype, stream):
+        pass
+
 
 def _zero3_comm_summary(opt, steps, world, red_dev):
     """Per-step time and bus bandwidth of the ZeRO-3 collectives (gathers and gradient
@@ -417,6 +423,13 @@ def _zero3_report(args, opt, world, rank, red_dev, el, total, workload, extra):
     el, achieved = float(t[0]), -float(t[1])
     ms = el / args.steps * 1e3
     comm = _zero3_comm_summary(opt, args.steps, world, red_dev) if world > 1 else None
+    if (comm is not None and args.comm in ("rccl", "c10d") and not args.no_comm_sweep
+            and opt.grad_arena() is not None):
+        # BASELINE.json configs[4]: RS / AG bus bandwidth per bucket size, on the grad chunk arena
+        # (scratch between steps) after the timed region
+        _phase("bucket-size sweep")
+        comm["sweep"] = comm_sweep(opt.comm, opt.grad_arena(), world, red_dev,
+                                   sizes_mb=(4, 8, 16, 32, 64, 128, 256))
     if rank == 0:
         out = {
             "metric": METRIC, "value": total / (ms / 1e3), "unit": "params/s", "n_gpus": world,
@@ -534,7 +547,7 @@ def zero3_gather_check(opt, model, shapes, full_copies, dev, world, rank, red_de
     idx = model.groups[1]
     ms = [opt.param_managers[getattr(layer, f"p{k}")] for k in range(layer.n)]
     rt.launch(("exchange-check",), ms)
-    out, ev = rt.pending.pop(("exchange-check",))
+    out, ev, _hold = rt.pending.pop(("exchange-check",))
     torch.cuda.current_stream(dev).wait_event(ev)
     torch.cuda.synchronize()
     bits = lambda t: t.reshape(-1).view(torch.int16 if t.element_size() == 2 else torch.int32)  # noqa: E731
@@ -614,7 +627,7 @@ def _adam_step1_restated(master, gsum, world, lr=1e-3, b1=0.9, b2=0.999, eps=1e-
     return master.float() + (f(-(lr / (1.0 - b1))) * m) / denom
 
 
-def zero12_exchange_check(opt, step, params, shapes, dev, world, rank, red_dev):
+def zero12_exchange_check(opt, step, params, shapes, dev, world, rank, red_dev, fatal=True):
     """Before timing at N>1: ONE real engine step on the real arena and communicator, with the
     bench's known per-rank synthetic grads (seed = rank).  Checks, on every rank:
       (1) the reduced gradient of every owned parameter (captured right after the reduce) equals
@@ -624,7 +637,9 @@ def zero12_exchange_check(opt, step, params, shapes, dev, world, rank, red_dev):
           step applied to that reduced gradient, within 1 bf16 ulp (fp32: 1e-6 relative);
       (3) the all-gather / broadcast left every rank with bit-identical parameters (two checksums
           per tensor, MIN == MAX over ranks).
-    A failure ends the run (exit 4) naming the rank and tensor."""
+    A failure ends the run (exit 4) naming the rank and tensor — or, with ``fatal=False`` (the
+    arena calibration, which can still measure through the other exchange), is returned in the
+    result ("all_ranks_ok": False, "failure": ...) after being logged."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -678,12 +693,16 @@ def zero12_exchange_check(opt, step, params, shapes, dev, world, rank, red_dev):
                             "rounding per hop)") if bf16 else f"{world} * 2^-22 * sum_r |g_r|",
            "adam_max_bf16_ulp" if bf16 else "adam_rel_tol": worst_ulp if bf16 else 1e-6,
            "params_identical_across_ranks": not diverged, "all_ranks_ok": bool(ok.item() == 1.0)}
-    if bad:
-        _fail_check("ZeRO step exchange", rank, bad[:8])
-    if diverged:
-        _fail_check("ZeRO step parameter broadcast", rank, f"tensors {diverged[:8]} differ across ranks")
-    if not res["all_ranks_ok"]:
-        _fail_check("ZeRO step exchange", rank, "another rank failed")
+    fail = (("ZeRO step exchange", bad[:8]) if bad else
+            ("ZeRO step parameter broadcast", f"tensors {diverged[:8]} differ across ranks")
+            if diverged else ("ZeRO step exchange", "another rank failed")
+            if not res["all_ranks_ok"] else None)
+    if fail is not None:
+        if fatal:
+            _fail_check(fail[0], rank, fail[1])
+        log(f"[bench] EXCHANGE CHECK FAILED on rank {rank} ({res['arena']} arena): {fail[0]}: "
+            f"{fail[1]} — excluded from the calibration")
+        res["failure"] = f"rank {rank}: {fail[0]}: {fail[1]}"[:400]
     return res
 
 
@@ -1122,15 +1141,19 @@ def main():
         if world > 1:
             _phase(f"exchange check ({kind} arena)")
             exchange_check[kind] = zero12_exchange_check(opt, step, params, shapes, dev, world, rank,
-                                                         red_dev)
+                                                         red_dev, fatal=len(arenas) == 1)
+            if not exchange_check[kind]["all_ranks_ok"]:
+                continue  # never time an exchange that computed a wrong step
         if len(arenas) > 1:  # calibrate: the same step through each exchange, the faster is timed
             _phase(f"arena calibration ({kind})")
             for _ in range(args.warmup):
                 step()
             arena_ab[kind] = timed(step, max(3, min(args.steps, 5)))
     if len(arenas) > 1:
+        if not arena_ab:
+            _fail_check("ZeRO step exchange", rank, "every arena failed its exchange check")
         best = min(arena_ab, key=arena_ab.get)
-        if best != arenas[-1]:
+        if best != arenas[-1] or kind != best:
             _teardown_engine(opt)
             opt, step = build(best)
     arena_used = getattr(opt.engine, "arena_kind", "buckets") if multi else "none (ws=1: no exchange)"

@@ -212,6 +212,63 @@ int zs_broadcast_group(zs_comm* c, int64_t n, const uint64_t* buf, const int64_t
   return ZS_OK;
 }
 
+int zs_all_gather_group(zs_comm* c, int64_t n, const uint64_t* send, const uint64_t* recv,
+                        const int64_t* send_count, int dtype, uintptr_t stream) {
+  ZS_REQUIRE(c && c->comm, "zs_all_gather_group: NULL communicator");
+  ZS_REQUIRE(n >= 0 && (n == 0 || (send && recv && send_count)), "zs_all_gather_group: bad table");
+  ncclDataType_t t;
+  int rc = to_nccl(dtype, &t);
+  if (rc) return rc;
+  for (int64_t i = 0; i < n; ++i)
+    ZS_REQUIRE(send_count[i] >= 0 && (send_count[i] == 0 || (send[i] && recv[i])),
+               "zs_all_gather_group: entry %lld: count %lld", (long long)i,
+               (long long)send_count[i]);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  ZS_NCCL(ncclGroupStart());
+  for (int64_t i = 0; i < n; ++i) {
+    if (send_count[i] == 0) continue;
+    ncclResult_t r = ncclAllGather(reinterpret_cast<const void*>(send[i]),
+                                   reinterpret_cast<void*>(recv[i]), size_t(send_count[i]), t,
+                                   c->comm, st);
+    if (r != ncclSuccess) {
+      (void)ncclGroupEnd();
+      return zs::fail(ZS_ERR_RCCL, "ncclAllGather (group entry %lld) failed: %s", (long long)i,
+                      ncclGetErrorString(r));
+    }
+  }
+  ZS_NCCL(ncclGroupEnd());
+  return ZS_OK;
+}
+
+int zs_reduce_scatter_group(zs_comm* c, int64_t n, const uint64_t* send, const uint64_t* recv,
+                            const int64_t* recv_count, int dtype, uintptr_t stream) {
+  ZS_REQUIRE(c && c->comm, "zs_reduce_scatter_group: NULL communicator");
+  ZS_REQUIRE(n >= 0 && (n == 0 || (send && recv && recv_count)),
+             "zs_reduce_scatter_group: bad table");
+  ncclDataType_t t;
+  int rc = to_nccl(dtype, &t);
+  if (rc) return rc;
+  for (int64_t i = 0; i < n; ++i)
+    ZS_REQUIRE(recv_count[i] >= 0 && (recv_count[i] == 0 || (send[i] && recv[i])),
+               "zs_reduce_scatter_group: entry %lld: count %lld", (long long)i,
+               (long long)recv_count[i]);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  ZS_NCCL(ncclGroupStart());
+  for (int64_t i = 0; i < n; ++i) {
+    if (recv_count[i] == 0) continue;
+    ncclResult_t r = ncclReduceScatter(reinterpret_cast<const void*>(send[i]),
+                                       reinterpret_cast<void*>(recv[i]), size_t(recv_count[i]), t,
+                                       ncclSum, c->comm, st);
+    if (r != ncclSuccess) {
+      (void)ncclGroupEnd();
+      return zs::fail(ZS_ERR_RCCL, "ncclReduceScatter (group entry %lld) failed: %s",
+                      (long long)i, ncclGetErrorString(r));
+    }
+  }
+  ZS_NCCL(ncclGroupEnd());
+  return ZS_OK;
+}
+
 int zs_group_start(void) {
   ZS_NCCL(ncclGroupStart());
   return ZS_OK;

@@ -138,6 +138,21 @@ class RcclComm:
                   count.ctypes.data_as(_PI64), root.ctypes.data_as(_PI32), int(dtype),
                   stream_handle(stream))
 
+    def all_gather_group(self, send, recv, count, dtype: int, stream) -> None:
+        """One RCCL group of all-gathers from device-pointer tables (a ZeRO-3 module's gather):
+        entry i gathers ``count[i]`` elements at ``send[i]`` from every rank into ``recv[i]``."""
+        _lib.call("zs_all_gather_group", self._h, len(count), send.ctypes.data_as(_PU64),
+                  recv.ctypes.data_as(_PU64), count.ctypes.data_as(_PI64), int(dtype),
+                  stream_handle(stream))
+
+    def reduce_scatter_group(self, send, recv, count, dtype: int, stream) -> None:
+        """One RCCL group of SUM reduce-scatters (a ZeRO-3 gradient bucket): entry i reduces
+        ``ws * count[i]`` elements at ``send[i]`` and leaves this rank's ``count[i]`` at
+        ``recv[i]``."""
+        _lib.call("zs_reduce_scatter_group", self._h, len(count), send.ctypes.data_as(_PU64),
+                  recv.ctypes.data_as(_PU64), count.ctypes.data_as(_PI64), int(dtype),
+                  stream_handle(stream))
+
     def broadcast_group(self, buf, count, root, dtype: int, stream) -> None:
         """One RCCL group of in-place broadcasts: ``count[i]`` elements at ``buf[i]`` from
         ``root[i]``."""

@@ -80,7 +80,7 @@ class _GatherRuntime:
     def __init__(self, ws, rank, comm, device):
         self.ws, self.rank, self.comm, self.device = ws, rank, comm, device
         self.stream = comm_stream(device)
-        self.pending = {}      # key -> (list[(manager, full_tensor)], event)
+        self.pending = {}      # key -> (list[(manager, full_tensor)], event, holding tensor)
         self.sequence = []     # learned order of group keys
         self.pos = 0
         self.recording = True
@@ -88,6 +88,7 @@ class _GatherRuntime:
         self.n_gathers = 0
         self.n_prefetch_hits = 0
         self.gather_events = None  # optional list of (start, end, bus_bytes) per gather group
+        self._tables = {}          # key -> grouped all-gather pointer table (see _table)
 
     def launch(self, key, managers):
         """Enqueue the all-gather of ``managers`` on the side stream; returns immediately."""
@@ -95,32 +96,68 @@ class _GatherRuntime:
             return
         if self.ws == 1 and not any(m.fp8 for m in managers):
             # the shard is the whole parameter: nothing to gather, no stream to synchronise with
-            self.pending[key] = ([(m, m._gather_prepare(None)[1]) for m in managers], None)
+            self.pending[key] = ([(m, m._gather_prepare(None)[1]) for m in managers], None, None)
             self.n_gathers += 1
             return
         ev_ready = torch.cuda.Event()
         ev_ready.record(torch.cuda.current_stream(self.device))  # shards may just have been updated
         timed = self.gather_events is not None and self.ws > 1
+        plan = self._table(key, managers)
         with torch.cuda.stream(self.stream):
             self.stream.wait_event(ev_ready)
             if timed:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record(self.stream)
-            # kernels (fp8 quantisation) before the RCCL group, dequantisation after: an RCCL
-            # group only launches its collectives at group end; every buffer a collective of the
-            # group touches is referenced from `states` until the group has ended
-            states = [m._gather_prepare(self.stream) for m in managers]
-            with _group_ctx(self.comm):
-                for m, st in zip(managers, states):
-                    m._gather_issue(self.comm, self.stream, st)
-            out = [(m, m._gather_finish(self.stream, st)) for m, st in zip(managers, states)]
+            hold = None
+            if plan is not None:
+                # one allocation for the module's full tensors and ONE library call for its RCCL
+                # group of all-gathers (zero-copy from the chunk-arena slots)
+                send, count, offs, total, dt, es, spans = plan
+                hold = torch.empty(total, dtype=managers[0].shard.dtype, device=self.device)
+                recv = np.uint64(hold.data_ptr()) + offs * np.uint64(es)
+                self.comm.all_gather_group(send, recv, count, dt, self.stream)
+                out = [(m, hold[o:o + n]) for m, (o, n) in zip(managers, spans)]
+            else:
+                # kernels (fp8 quantisation) before the RCCL group, dequantisation after: an RCCL
+                # group only launches its collectives at group end; every buffer a collective of
+                # the group touches is referenced from `states` until the group has ended
+                states = [m._gather_prepare(self.stream) for m in managers]
+                with _group_ctx(self.comm):
+                    for m, st in zip(managers, states):
+                        m._gather_issue(self.comm, self.stream, st)
+                out = [(m, m._gather_finish(self.stream, st)) for m, st in zip(managers, states)]
             ev = torch.cuda.Event()
             ev.record(self.stream)
             if timed:  # ring all-gather bus bytes: (ws-1)/ws of the gathered tensor, per rank
                 bus = sum(m.gather_bytes() for m in managers) * (self.ws - 1)
                 self.gather_events.append((e0, _timed_after(self.stream), bus))
-        self.pending[key] = (out, ev)
+        self.pending[key] = (out, ev, hold)
         self.n_gathers += 1
+
+    def _table(self, key, managers):
+        """The cached pointer table of a module's grouped all-gather (chunk-arena managers with
+        a communicator that takes tables), or None for the per-parameter path."""
+        if key in self._tables:
+            return self._tables[key]
+        plan = None
+        if (hasattr(self.comm, "all_gather_group") and managers
+                and all(m.send_slot is not None and not m.fp8 for m in managers)
+                and len({m.shard.dtype for m in managers}) == 1):
+            ws = self.ws
+            es = managers[0].shard.element_size()
+            sizes = [ws * m.S for m in managers]
+            offs, o = [], 0
+            for n in sizes:
+                offs.append(o)
+                o += -(-n // ALIGN_ELEMS) * ALIGN_ELEMS  # every full tensor 64-element aligned
+            from .comm import zs_dtype
+
+            plan = (np.array([m.send_slot.data_ptr() for m in managers], np.uint64),
+                    np.array([m.S for m in managers], np.int64), np.array(offs, np.uint64),
+                    max(o, 1), zs_dtype(managers[0].shard.dtype), es,
+                    [(off, m.numel) for off, m in zip(offs, managers)])
+        self._tables[key] = plan
+        return plan
 
     def _prefetch(self, i):
         if 0 <= i < len(self.sequence):
@@ -139,15 +176,18 @@ class _GatherRuntime:
         if key in self.pending:
             self.n_prefetch_hits += 1
         self.launch(key, managers)
-        out, ev = self.pending.pop(key)
+        out, ev, hold = self.pending.pop(key)
         if ev is None:  # ws == 1
             for m, full in out:
                 m._install_full(full)
             return
         cur = torch.cuda.current_stream(self.device)
         cur.wait_event(ev)
+        if hold is not None:  # one allocation behind all of the module's full tensors
+            hold.record_stream(cur)
         for m, full in out:
-            full.record_stream(cur)
+            if hold is None:
+                full.record_stream(cur)
             m._install_full(full)
 
     def end_iteration(self):
@@ -261,10 +301,12 @@ class Zero3ParamManager:
         rt = self._runtime()
         key = ("param", id(self))
         rt.launch(key, [self])
-        out, ev = rt.pending.pop(key)
+        out, ev, hold = rt.pending.pop(key)
         cur = torch.cuda.current_stream(self.shard.device)
         if ev is not None:
             cur.wait_event(ev)
+        if hold is not None:
+            hold.record_stream(cur)
         for m, full in out:
             full.record_stream(cur)
             m._install_full(full)
@@ -433,6 +475,7 @@ class _GradReducer:
         self._size = np.array([len(g) for g in groups], np.int64)
         self.ev_done = [torch.cuda.Event() for _ in range(self.K)]
         self.timing = None  # optional list of (start, end, bus_bytes) per launched bucket
+        self._rs_tables = {}
         self.reset()
 
     def reset(self):
@@ -491,6 +534,19 @@ class _GradReducer:
                 s, n = int(opt._arena.slot[i]), int(opt._arena.ln[i])
                 p.grad = opt._G[s:s + n].view(opt._arena.shard_shapes[i])
 
+    def _rs_table(self, k: int):
+        """Bucket k's reduce-scatter destinations (grad chunk-arena slots) and counts, cached."""
+        t = self._rs_tables.get(k)
+        if t is None:
+            from .comm import zs_dtype
+
+            opt, idx = self.opt, np.asarray(self.groups[k], np.int64)
+            G = opt._G
+            t = (np.uint64(G.data_ptr()) + (opt._arena.slot[idx] * G.element_size()).astype(np.uint64),
+                 np.ascontiguousarray(opt._arena.S[idx], np.int64), zs_dtype(G.dtype))
+            self._rs_tables[k] = t
+        return t
+
     def _launch(self, k: int):
         opt = self.opt
         ar, ws = opt._arena, opt.world_size
@@ -539,10 +595,15 @@ class _GradReducer:
         if self.timing is not None:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record(cs)
-        with _group_ctx(opt.comm):
-            for i, send in sends:
-                s = int(ar.slot[i])
-                opt.comm.reduce_scatter(send, opt._G[s:s + int(ar.S[i])], cs)
+        if hasattr(opt.comm, "reduce_scatter_group"):  # the bucket's RCCL group: ONE call
+            recv, count, dt = self._rs_table(k)
+            sp = np.fromiter((t.data_ptr() for _, t in sends), np.uint64, len(sends))
+            opt.comm.reduce_scatter_group(sp, recv, count, dt, cs)
+        else:
+            with _group_ctx(opt.comm):
+                for i, send in sends:
+                    s = int(ar.slot[i])
+                    opt.comm.reduce_scatter(send, opt._G[s:s + int(ar.S[i])], cs)
         # the group has been enqueued: a buffer freed from here on is only reused after it
         for i, send in sends:
             send.record_stream(cs)

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ZS_ABI_VERSION 5
+#define ZS_ABI_VERSION 6
 
 enum zs_status {
   ZS_OK = 0,
@@ -278,6 +278,16 @@ int zs_reduce_group(zs_comm* comm, int64_t n, const uint64_t* send, const uint64
                     const int64_t* count, const int32_t* root, int dtype, uintptr_t stream);
 int zs_broadcast_group(zs_comm* comm, int64_t n, const uint64_t* buf, const int64_t* count,
                        const int32_t* root, int dtype, uintptr_t stream);
+/* One RCCL group of n all-gathers (entry i: send_count[i] elements from send[i] on every rank
+ * into recv[i], rank-major) or of n SUM reduce-scatters (entry i: ws * recv_count[i] elements at
+ * send[i] reduced, this rank's recv_count[i] into recv[i]).  ZeRO-3's per-module gather of every
+ * parameter's dim-0 chunk (Zero3ParamManager.materialize, zero3.py:36-41, one group per module)
+ * and one backward bucket of gradient reduce-scatters into the chunk arena (the reduction of
+ * zero3.py:131-147), each as ONE call instead of one per parameter. */
+int zs_all_gather_group(zs_comm* comm, int64_t n, const uint64_t* send, const uint64_t* recv,
+                        const int64_t* send_count, int dtype, uintptr_t stream);
+int zs_reduce_scatter_group(zs_comm* comm, int64_t n, const uint64_t* send, const uint64_t* recv,
+                            const int64_t* recv_count, int dtype, uintptr_t stream);
 int zs_group_start(void);
 int zs_group_end(void);
 /* RCCL version the library is bound to at run time (e.g. 22606). */

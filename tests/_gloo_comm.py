@@ -19,7 +19,7 @@ import torch.distributed as dist
 
 class GlooStagedComm:
     def __init__(self, group=None):
-        self.group = group
+        self.pg = group  # (not `group`: that name is the RCCL-like group() below)
         self.ws = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.calls = []
@@ -50,7 +50,7 @@ class GlooStagedComm:
         stream.synchronize()
         h = send.detach().to("cpu", torch.float32)
         out = torch.empty(recv.numel(), dtype=torch.float32)
-        dist.reduce_scatter_tensor(out, h, group=self.group)
+        dist.reduce_scatter_tensor(out, h, group=self.pg)
         with torch.cuda.stream(stream):
             recv.copy_(out.to(recv.device).to(recv.dtype))
         self.calls.append(("rs", send.numel()))
@@ -63,21 +63,21 @@ class GlooStagedComm:
         if h.dtype != torch.float32:  # a gather is a byte copy: move bf16 / uint8 as int8 bytes
             h = h.view(torch.int8)
         out = torch.empty(recv.numel() * recv.element_size() // h.element_size(), dtype=h.dtype)
-        dist.all_gather_into_tensor(out, h, group=self.group)
+        dist.all_gather_into_tensor(out, h, group=self.pg)
         out = out.view(recv.dtype)
         with torch.cuda.stream(stream):
             recv.copy_(out.to(recv.device))
         self.calls.append(("ag", recv.numel()))
 
     def _root(self, root):
-        return dist.get_global_rank(self.group, root) if self.group else root
+        return dist.get_global_rank(self.pg, root) if self.pg else root
 
     def reduce(self, t, root, stream):
         if self._defer(self.reduce, t, root, stream):
             return
         stream.synchronize()
         h = t.detach().to("cpu", torch.float32)
-        dist.reduce(h, dst=self._root(root), group=self.group)
+        dist.reduce(h, dst=self._root(root), group=self.pg)
         if root == self.rank:
             with torch.cuda.stream(stream):
                 t.copy_(h.to(t.device).to(t.dtype))
@@ -88,7 +88,7 @@ class GlooStagedComm:
             return
         stream.synchronize()
         h = send.detach().to("cpu", torch.float32)
-        dist.reduce(h, dst=self._root(root), group=self.group)
+        dist.reduce(h, dst=self._root(root), group=self.pg)
         if root == self.rank:
             with torch.cuda.stream(stream):
                 recv.copy_(h.to(recv.device).to(recv.dtype))
@@ -101,7 +101,7 @@ class GlooStagedComm:
         h = t.detach().to("cpu")
         if h.dtype != torch.float32:
             h = h.view(torch.int8)
-        dist.broadcast(h, src=self._root(root), group=self.group)
+        dist.broadcast(h, src=self._root(root), group=self.pg)
         h = h.view(t.dtype)
         with torch.cuda.stream(stream):
             t.copy_(h.to(t.device))
@@ -115,8 +115,8 @@ class GlooStagedComm:
         for root, (off, n) in enumerate(zip(win_off, win_len)):
             if n:
                 part = h[int(off):int(off) + int(n)].clone()
-                dist.reduce(part, dst=dist.get_global_rank(self.group, root) if self.group else root,
-                            group=self.group)
+                dist.reduce(part, dst=dist.get_global_rank(self.pg, root) if self.pg else root,
+                            group=self.pg)
                 if root == self.rank:
                     h[int(off):int(off) + int(n)] = part
         with torch.cuda.stream(stream):
@@ -132,7 +132,7 @@ class GlooStagedComm:
             if n:
                 part = h[int(off):int(off) + int(n)].clone()
                 raw = part if part.dtype == torch.float32 else part.view(torch.int8)
-                dist.broadcast(raw, src=self._root(root), group=self.group)
+                dist.broadcast(raw, src=self._root(root), group=self.pg)
                 h[int(off):int(off) + int(n)] = raw.view(part.dtype)
         with torch.cuda.stream(stream):
             buf.copy_(h.to(buf.device))
@@ -143,10 +143,51 @@ class GlooStagedComm:
             return
         stream.synchronize()
         h = t.detach().to("cpu", torch.float32)
-        dist.all_reduce(h, group=self.group)
+        dist.all_reduce(h, group=self.pg)
         with torch.cuda.stream(stream):
             t.copy_(h.to(t.device).to(t.dtype))
         self.calls.append(("ar", t.numel()))
+
+
+_TYPESTR = {0: "<f4", 1: "<i2", 2: "|u1"}  # ZS_F32, ZS_BF16 (as int16 bits), ZS_U8
+
+
+def _dev_view(ptr, n, dtype_code, device="cuda"):
+    """TEST-ONLY: a tensor over ``n`` elements of device memory at ``ptr`` (the table-driven
+    collectives take raw pointers), through ``__cuda_array_interface__``."""
+    class _Arr:
+        pass
+
+    a = _Arr()
+    a.__cuda_array_interface__ = {"shape": (int(n),), "typestr": _TYPESTR[int(dtype_code)],
+                                  "data": (int(ptr), False), "version": 2}
+    t = torch.as_tensor(a, device=device)
+    return t.view(torch.bfloat16) if int(dtype_code) == 1 else t
+
+
+def _add_table_methods(cls):
+    """all_gather_group / reduce_scatter_group (RcclComm's table forms) over the tensor forms."""
+    def all_gather_group(self, send, recv, count, dtype, stream):
+        with self.group():
+            for s, r, n in zip(send, recv, count):
+                if int(n):
+                    self.all_gather(_dev_view(s, n, dtype), _dev_view(r, int(n) * self.ws, dtype), stream)
+        self.calls.append(("ag_group", len(count)))
+
+    def reduce_scatter_group(self, send, recv, count, dtype, stream):
+        with self.group():
+            for s, r, n in zip(send, recv, count):
+                if int(n):
+                    self.reduce_scatter(_dev_view(s, int(n) * self.ws, dtype), _dev_view(r, n, dtype),
+                                        stream)
+        self.calls.append(("rs_group", len(count)))
+
+    cls.all_gather_group = all_gather_group
+    cls.reduce_scatter_group = reduce_scatter_group
+    return cls
+
+
+_add_table_methods(GlooStagedComm)
 
 
 class SimRankComm:

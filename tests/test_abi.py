@@ -35,7 +35,7 @@ def test_library_is_gfx950_code_object():
 def test_abi_version_and_error_text():
     from zero_amd import _lib
 
-    assert _lib.lib.zs_abi_version() == _lib.ABI_VERSION == 5
+    assert _lib.lib.zs_abi_version() == _lib.ABI_VERSION == 6
     h = ctypes.c_void_p()
     rc = _lib.lib.zs_plan_create(0, None, None, 0, 0, 0, 64, 0, 0, ctypes.byref(h))
     assert rc == _lib.ZS_ERR_INVALID
@@ -93,6 +93,8 @@ def test_new_entry_points_validate_arguments():
     assert lib.zs_broadcast(None, None, None, 4, _lib.ZS_F32, 0, 0) == _lib.ZS_ERR_INVALID
     assert lib.zs_reduce_group(None, 0, None, None, None, None, _lib.ZS_F32, 0) == _lib.ZS_ERR_INVALID
     assert lib.zs_broadcast_group(None, 0, None, None, None, _lib.ZS_F32, 0) == _lib.ZS_ERR_INVALID
+    assert lib.zs_all_gather_group(None, 0, None, None, None, _lib.ZS_F32, 0) == _lib.ZS_ERR_INVALID
+    assert lib.zs_reduce_scatter_group(None, 0, None, None, None, _lib.ZS_F32, 0) == _lib.ZS_ERR_INVALID
     assert b"NULL communicator" in lib.zs_last_error()
     from zero_amd.plan import Plan
 

@@ -57,11 +57,14 @@ def test_bench_simulated_ws8_bucket_path(gpu):
 
 
 def test_bench_zero3_parameter_set_n1(gpu):
-    """--zero 3 on C4 (configs[4]'s step on the 3B set): 38 hooked layer modules, update mode."""
+    """--zero 3 on C4 (configs[4]'s step on the 3B set), update mode, one rank: every shard is its
+    whole parameter, so no hooks are registered and nothing is gathered (the backward still hands
+    each gradient to the reducer, and one fused Adam runs over the chunk arena)."""
     out = _run([sys.executable, "bench.py", "--config", "C4", "--zero", "3", "--steps", "3",
                 "--warmup", "1", "--no-cpu-baseline"])
     assert out["config"]["zero"] == 3 and out["value"] > 0 and out["n_gpus"] == 1
-    assert out["zero3"]["gathers_per_step"] > 0 and out["roofline"]["frac"] > 0
+    assert out["zero3"]["gathers_per_step"] == 0 and out["roofline"]["frac"] > 0
+    assert out["roofline"]["launches_per_step"] == 1
 
 
 def test_bench_zero3_parameter_set_simulated_ws8(gpu):
@@ -90,7 +93,7 @@ def test_bench_zero3_training_iteration(gpu):
     out = _run([sys.executable, "bench.py", "--config", "C2", "--zero", "3", "--dtype", "fp32",
                 "--steps", "3", "--warmup", "1", "--no-cpu-baseline"])
     assert out["config"]["zero"] == 3 and out["value"] > 0
-    assert out["roofline"]["launches_per_step"] >= 1 and out["zero3"]["gathers_per_step"] > 0
+    assert out["roofline"]["launches_per_step"] >= 1 and out["zero3"]["gathers_per_step"] == 0
 
 
 def _selfcheck_worker(rank, ws, port):

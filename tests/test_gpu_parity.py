@@ -84,6 +84,47 @@ def test_rccl_comm_ws1(gpu, pg1):
     comm.close()
 
 
+def test_rccl_table_collectives_ws1(gpu, pg1):
+    """The table forms (zs_all_gather_group / zs_reduce_scatter_group / zs_reduce_group /
+    zs_broadcast_group) are copies at ws=1: every entry lands at its own destination, zero-count
+    entries are skipped, bf16 and fp32; and the GlooStagedComm adapter's raw-pointer views
+    (__cuda_array_interface__) see the same memory."""
+    from _gloo_comm import _dev_view
+    from zero_amd import _lib
+    from zero_amd.comm import RcclComm
+
+    comm = RcclComm()
+    st = torch.cuda.current_stream()
+    for dt, code in ((torch.float32, _lib.ZS_F32), (torch.bfloat16, _lib.ZS_BF16)):
+        counts = np.array([1000, 0, 7, 4096], np.int64)
+        src = [torch.randn(int(n) or 1, device=gpu).to(dt) for n in counts]
+        dst = [torch.zeros(int(n) or 1, device=gpu, dtype=dt) for n in counts]
+        sp = np.array([t.data_ptr() for t in src], np.uint64)
+        for fn in (comm.all_gather_group, comm.reduce_scatter_group):
+            for d in dst:
+                d.zero_()
+            dp = np.array([t.data_ptr() for t in dst], np.uint64)
+            fn(sp, dp, counts, code, st)
+            torch.cuda.synchronize()
+            for n, a, b in zip(counts, src, dst):
+                if n:
+                    assert torch.equal(a, b), (fn.__name__, dt, n)
+                else:
+                    assert not b.any()  # a zero-count entry touches nothing
+        v = _dev_view(src[0].data_ptr(), counts[0], code)
+        assert v.dtype == dt and torch.equal(v, src[0])
+    buf = torch.arange(64, dtype=torch.float32, device=gpu)
+    out = torch.zeros_like(buf)
+    one = lambda *a: np.array(a)  # noqa: E731
+    comm.reduce_group(one(buf.data_ptr()).astype(np.uint64), one(out.data_ptr()).astype(np.uint64),
+                      one(64).astype(np.int64), one(0).astype(np.int32), _lib.ZS_F32, st)
+    comm.broadcast_group(one(out.data_ptr()).astype(np.uint64), one(64).astype(np.int64),
+                         one(0).astype(np.int32), _lib.ZS_F32, st)
+    torch.cuda.synchronize()
+    assert torch.equal(out, buf)
+    comm.close()
+
+
 def _mr_worker(rank, ws, port, variant, name, buckets="ragged", arena=None):
     import sys
     from conftest import PKG, REPO  # noqa: F401  (sets sys.path in the child)
