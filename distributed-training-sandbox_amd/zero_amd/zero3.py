@@ -355,6 +355,7 @@ def register_zero3_hooks(model, param_managers, units=None):
         mod_managers[id(mod)] = ms
     for rt in runtimes:
         rt.key_managers = {}
+        rt._tables = {}  # a key's managers may differ from an earlier registration
         for mod in model.modules():
             ms = mod_managers[id(mod)]
             if ms:
