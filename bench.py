@@ -891,7 +891,7 @@ def bench_train_smollm3(args, world, rank, dev, use_nccl):
         zero3.register_zero3_hooks(model, opt.param_managers, units=list(model.model.layers))
     else:
         opt = zero2.ShardedOptimizer(torch.optim.AdamW(model.parameters(), lr=1e-5), overlap=True,
-                                     sync=False)
+                                     sync=False, arena="buckets" if args.arena == "buckets" else "flat")
     batch = args.batch or 1
     g = torch.Generator(device=dev).manual_seed(42 + rank)  # each rank its own data shard
     ids = torch.randint(0, cfg.vocab_size, (batch, args.seq), device=dev, generator=g)

@@ -97,7 +97,8 @@ class ShardedOptimizerBase:
         self._overlap_hooks = []
         if self._overlap:
             # hooks must exist before the first backward: build the engine (and the communicator,
-            # a collective call every rank makes here) now
+            # a collective call every rank makes here) now.  Flat arena: per-owner reduces of G
+            # stretches from the hooks (flat.py); bucket arena: GradBuckets views (overlap.py)
             self._build_engine()
             gb = self.engine.enable_overlap(int(overlap_bucket_mb * (1 << 20)))
             self._overlap_hooks = gb.register_hooks()
@@ -107,7 +108,7 @@ class ShardedOptimizerBase:
             self._build_engine()
 
     def _flat(self) -> bool:
-        return self._arena == "flat" and not self._overlap and self._layout == "reference"
+        return self._arena == "flat" and self._layout == "reference"
 
     def _shard_optimizer_params(self):
         """zero1.py:71-74: drop non-owned params from the inner optimizer's groups."""
@@ -219,11 +220,11 @@ class ShardedOptimizerBase:
             p.grad = None
 
     def zero_grad(self, set_to_none: bool = True):
-        if self._overlap:  # grads become zeroed views of the overlap buckets (no pack copy)
-            self.engine.gb.install_views()
-            return
         if self._flat():  # zeroed views of the grad arena (backward accumulates in place)
             self.engine.zero_grad()
+            return
+        if self._overlap:  # grads become zeroed views of the overlap buckets (no pack copy)
+            self.engine.gb.install_views()
             return
         for p in self.params:
             if p.grad is not None:

@@ -122,6 +122,9 @@ class FlatEngine(ShardEngine):
         self.ev_c0 = torch.cuda.Event(enable_timing=True)
         self.ev_c1 = torch.cuda.Event(enable_timing=True)
         self.capture_reduced = None  # optional tensor: a copy of R after the reduces (checks)
+        self.overlap = False  # backward-overlapped reduces (enable_overlap)
+        self.ov_K = 0
+        self.launched_in_backward = 0
 
     # ------------------------------------------------------------------------------------------
     def _make_round(self, j: int) -> _Round:
@@ -178,6 +181,8 @@ class FlatEngine(ShardEngine):
         self.dirty[:] = False
         self.install_views()
         self.zero_grad_calls += 1
+        if self.overlap:
+            self._ov_reset()
 
     def rebuild_rows(self):
         """Adam rows again (after the amsgrad buffer appeared)."""
@@ -247,6 +252,145 @@ class FlatEngine(ShardEngine):
                     s0 = int(self.base[r]) + rd.j * self.W
                     comm.broadcast(self.P[s0:s0 + c], r, cs)
 
+    # ------------------------------------------------------------------------------------------
+    # Backward overlap on the flat arena
+    def enable_overlap(self, bucket_bytes: int):
+        """Reduce gradients while backward runs: parameters grouped in reverse index order (the
+        order a sequential model's backward produces them) into buckets of at most
+        ``bucket_bytes`` that never mix owners, so a bucket is one contiguous stretch of its
+        owner's stream in G (and in the owner's R).  A post-accumulate-grad hook counts a bucket's
+        gradients; a complete bucket whose predecessors have been launched is reduced to its owner
+        at once — one RCCL reduce on the comm stream behind an event on the stream that produced
+        the gradient — strictly in bucket order, so every rank issues the same sequence.  step()
+        reduces what backward left, runs Adam as soon as this rank's own buckets have arrived,
+        and broadcasts in rounds as without overlap: no unpack, the parameters are the arena."""
+        from .overlap import plan_grad_buckets
+
+        groups, keys, *_ = plan_grad_buckets(self.numel.tolist(), self.owner.tolist(),
+                                             int(bucket_bytes), self.ces, align=ALIGN_ELEMS)
+        n = len(self.params)
+        self.ov_groups = groups
+        self.ov_K = len(groups)
+        self.ov_owner = np.asarray(keys, np.int64)
+        self.ov_lo = np.array([int(self.slot[g].min()) for g in groups], np.int64)
+        self.ov_hi = np.array([int((self.slot[g] + self.numel[g]).max()) for g in groups], np.int64)
+        self.ov_bucket_of = np.zeros(n, np.int64)
+        for k, g in enumerate(groups):
+            self.ov_bucket_of[g] = k
+        self.ov_size = np.array([len(g) for g in groups], np.int64)
+        self.ov_ev = [torch.cuda.Event() for _ in range(self.ov_K)]
+        own = np.nonzero(self.ov_owner == self.rank)[0]
+        self.ov_last_own = int(own[-1]) if len(own) else -1
+        self.overlap = True
+        self._ov_reset()
+        return self
+
+    def register_hooks(self):
+        return [p.register_post_accumulate_grad_hook(lambda _p, i=i: self._ov_ready(i))
+                for i, p in enumerate(self.params) if p.requires_grad]
+
+    def _ov_reset(self):
+        self.ov_pending = self.ov_size.copy()
+        self.ov_marked = np.zeros(len(self.params), bool)
+        self.ov_next = 0
+        self.ov_launched = 0
+
+    def _ov_ready(self, i: int):
+        if self.ov_marked[i]:
+            raise RuntimeError(
+                "zero_amd: gradient of parameter %d accumulated twice before step(); the "
+                "backward-overlapped mode reduces each gradient once per step" % i)
+        self.ov_marked[i] = True
+        g = self.params[i].grad
+        if g is not None and not self.is_view(i, g):  # a fresh grad (the caller cleared the view)
+            self.grad_view(i).copy_(g.reshape(self.params[i].shape))
+        self.ov_pending[self.ov_bucket_of[i]] -= 1
+        while self.ov_next < self.ov_K and self.ov_pending[self.ov_next] == 0:
+            self._ov_launch(self.ov_next)
+            self.ov_launched += 1
+            self.ov_next += 1
+
+    def _ov_launch(self, k: int, stream=None):
+        cur = torch.cuda.current_stream(self.device) if stream is None else stream
+        lo, hi, r = int(self.ov_lo[k]), int(self.ov_hi[k]), int(self.ov_owner[k])
+        if self.ws == 1:  # nothing to exchange: Adam reads G
+            self.ov_ev[k].record(cur)
+            return
+        if self.grad_comm:  # the bucket's grads as bf16 for the wire (gfx950 RNE kernel)
+            from .kernels import convert
+
+            convert(self.G[lo:hi], self.Gc[lo:hi], cur)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        cs = self.comm_stream
+        cs.wait_event(ev)
+        e0 = self._timed_start(cs)
+        b = int(self.base[r])
+        if hasattr(self.comm, "reduce_group"):
+            ces = self.ces
+            send = np.array([self.Gc.data_ptr() + lo * ces], np.uint64)
+            recv = np.array([self.R.data_ptr() + (lo - b) * ces], np.uint64) if r == self.rank else send
+            self.comm.reduce_group(send, recv, np.array([hi - lo], np.int64),
+                                   np.array([r], np.int32), self.czdtype, cs)
+        else:  # tensor-level communicators (tests)
+            src = self.Gc[lo:hi]
+            self.comm.reduce_out(src, self.R[lo - b:hi - b] if r == self.rank else src, r, cs)
+        self.ov_ev[k].record(cs)
+        if e0 is not None:  # bus bytes of a reduce of S bytes to one root: S per rank
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record(cs)
+            self.comm_events.append(("rs", "flat-overlap", e0, e1, (hi - lo) * self.ces))
+
+    def _step_overlap(self, grads, has, view, cmul, hps, hparams_of, stream):
+        """step() after a backward-overlapped backward: flush, Adam, broadcast rounds."""
+        n = len(self.params)
+        es = self.es
+        marked = self.ov_marked
+        # grads assigned by hand (no hook fired) are copied in; a stale slot without a grad this
+        # step is zero-filled — only in buckets not launched yet (a launched bucket is complete)
+        copy = np.nonzero(has & ~view & ~marked)[0]
+        zero = np.nonzero(~has & self.dirty & ~marked)[0]
+        if len(copy) or len(zero):
+            src = np.concatenate([np.fromiter((_ptr(grads[i]) for i in copy), np.uint64, len(copy)),
+                                  np.zeros(len(zero), np.uint64)])
+            idx = np.concatenate([copy, zero]).astype(np.int64)
+            dst = np.uint64(self.G.data_ptr()) + (self.slot[idx] * es).astype(np.uint64)
+            nb = self.numel[idx] * es
+            cs_ = self._cached(("gcopy",), src.tobytes() + dst.tobytes(), lambda: CopySet(src, dst, nb))
+            self._run_copy("pack", cs_, stream)
+        self.dirty = has.copy()
+        with _lib.phase_range("all_reduce_gradients"):  # what backward did not reduce
+            while self.ov_next < self.ov_K:
+                self._ov_launch(self.ov_next, stream)
+                self.ov_next += 1
+        self.launched_in_backward = self.ov_launched
+        if self.ws > 1:
+            self.ev_c1.record(self.comm_stream)
+        if self.ov_last_own >= 0:  # Adam needs this rank's own buckets only
+            stream.wait_event(self.ov_ev[self.ov_last_own])
+        if self.capture_reduced is not None:
+            self.capture_reduced.copy_(self.R[:self.capture_reduced.numel()])
+        with _lib.phase_range("optimizer_step"):  # zero1.py:88
+            for rd in self.rounds:
+                if len(rd.idx) and not (hps and self._adam_round_fast(rd, hps, stream)):
+                    live = has[rd.idx]
+                    rows, idx = (rd.rows, rd.idx) if live.all() else (rd.rows[live], rd.idx[live])
+                    self._run_adam(("flat", rd.j), rows, idx, hparams_of, stream,
+                                   carry_mul=cmul[idx])
+                self.ev_adam[rd.j].record(stream)
+        if self.ws > 1:
+            cs = self.comm_stream
+            with _lib.phase_range("broadcast_parameters"):  # zero1.py:91-102
+                for rd in self.rounds:
+                    cs.wait_event(self.ev_adam[rd.j])
+                    e0 = self._timed_start(cs)
+                    self._bcast_round(rd, cs)
+                    self.ev_bc[rd.j].record(cs)
+                    self._timed_end(e0, cs, "ag", int(rd.count.sum()))
+            stream.wait_event(self.ev_bc[self.K - 1])
+        self._reinstall(has, view)
+        self._ov_reset()
+
     def step(self, grads, hparams_of, stream=None):
         stream = torch.cuda.current_stream(self.device) if stream is None else stream
         n = len(self.params)
@@ -261,8 +405,9 @@ class FlatEngine(ShardEngine):
         self.ev_c0.record(stream)
         # gradients not accumulated into the arena (assigned tensors, fresh grads after the caller
         # cleared the views) are copied in; a stale slot whose grad is gone is zero-filled
-        copy = np.nonzero(has & ~view)[0]
-        zero = np.nonzero(~has & self.dirty)[0]
+        # (overlap mode: in _step_overlap, for the parameters no hook has handled)
+        copy = np.nonzero(has & ~view)[0] if not self.overlap else ()
+        zero = np.nonzero(~has & self.dirty)[0] if not self.overlap else ()
         if len(copy) or len(zero):
             src = np.concatenate([np.fromiter((_ptr(grads[i]) for i in copy), np.uint64, len(copy)),
                                   np.zeros(len(zero), np.uint64)])
@@ -271,7 +416,8 @@ class FlatEngine(ShardEngine):
             nb = self.numel[idx] * es
             cs_ = self._cached(("gcopy",), src.tobytes() + dst.tobytes(), lambda: CopySet(src, dst, nb))
             self._run_copy("pack", cs_, stream)
-        self.dirty = has.copy()
+        if not self.overlap:
+            self.dirty = has.copy()
         # ZeRO-1: the carry weight per owned param (see the module docstring)
         cmul = np.where(view, self.ws - 1, 0).astype(np.int64)
         self.steps[self.owned & has] += 1
@@ -296,6 +442,9 @@ class FlatEngine(ShardEngine):
                     decoupled=h["decoupled"], amsgrad=h["amsgrad"], maximize=h["maximize"],
                     grad_div=float(self.ws),
                     carry_mul=float(cm[0]) if self.carry is not None else 0.0)
+        if self.overlap:
+            self._step_overlap(grads, has, view, cmul, hps, hparams_of, stream)
+            return
         if self.grad_comm:  # the exchange moves bf16: convert every local grad once (2 launches' worth
             from .kernels import convert  # of bytes: read 4 + write 2 B per element)
 

@@ -86,20 +86,33 @@ def run_injected(z, variant: int, rank: int, ws: int, device, comm=None, window_
 
 
 def run_backward(z, variant: int, rank: int, ws: int, device, comm=None, tol=1e-6, overlap=True,
-                 views=True, bucket_mb=None):
+                 views=True, bucket_mb=None, arena=None):
     """Like run_injected, but the fixture's grads arrive through a real backward pass
     (loss = Σ_i <p_i, G_i>, so p_i.grad == G_i exactly), which fires the post-accumulate-grad
     hooks of the backward-overlapped mode.  ``views``: zero_grad() installs bucket views
-    (autograd accumulates in place); otherwise grads are set to None and copied into the buckets."""
+    (autograd accumulates in place); otherwise grads are set to None and copied into the buckets.
+    ZeRO-1 on the flat arena with ``views=False`` is the loop that clears every grad itself
+    (model.zero_grad()): no carry, so the expectation is the oracle's zero_grad="model" run
+    (the bucket arena keeps the reference harness's carry either way)."""
     mod = module_for(variant)
     steps = int(z["steps"])
-    params = [torch.nn.Parameter(torch.from_numpy(z[f"init_{i}"].copy()).to(device)) for i in range(12)]
+    init = [z[f"init_{i}"] for i in range(12)]
+    params = [torch.nn.Parameter(torch.from_numpy(a.copy()).to(device)) for a in init]
     kw = dict(overlap=overlap)
     if bucket_mb is not None:
         kw["overlap_bucket_mb"] = bucket_mb
     if comm is not None:
         kw["comm"] = comm
+    if arena is not None:
+        kw["arena"] = arena
     opt = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), **kw)
+    flat = getattr(opt.engine, "arena_kind", None) == "flat"
+    want = None
+    if flat and variant == 1 and ws > 1 and not views:
+        from oracle import zero_oracle as zo
+
+        want = zo.simulate(1, ws, init, steps=steps, zero_grad="model",
+                           local_grads=lambda t, r, i: z[f"r{r}_t{t}_lg{i}"])
     for t in range(steps):
         if views:
             opt.zero_grad()
@@ -110,10 +123,16 @@ def run_backward(z, variant: int, rank: int, ws: int, device, comm=None, tol=1e-
         loss = sum((p * g).sum() for p, g in zip(params, gs))
         loss.backward()
         opt.step()
-        if f"r{rank}_t{t}_p0" in z.files:
+        if want is not None:
+            for i, p in enumerate(params):
+                e = rel(p.detach().cpu().numpy(), want["params"][t][rank][i])
+                assert e <= tol, (variant, ws, rank, t, i, e, "model.zero_grad")
+        elif f"r{rank}_t{t}_p0" in z.files:
             for i, p in enumerate(params):
                 e = rel(p.detach().cpu().numpy(), z[f"r{rank}_t{t}_p{i}"])
                 assert e <= tol, (variant, ws, rank, t, i, e)
+    if want is not None:
+        return opt
     for i, p in enumerate(params):
         key = f"r{rank}_state_{i}_exp_avg"
         if key in z.files:

@@ -30,12 +30,22 @@ def pg1():
     dist.destroy_process_group()
 
 
+def _overlap_stats(opt):
+    """(buckets, buckets launched during the last backward) of either overlap implementation."""
+    eng = opt.engine
+    if getattr(eng, "arena_kind", None) == "flat":
+        return eng.ov_K, eng.launched_in_backward
+    return eng.gb.K, eng.gb.launched_in_backward
+
+
+@pytest.mark.parametrize("arena", ["flat", "buckets"])
 @pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("views", [True, False])
-def test_ws1_overlap_backward(gpu, golden, pg1, variant, views):
+def test_ws1_overlap_backward(gpu, golden, pg1, variant, views, arena):
     z = golden(f"traj_z{variant}_ws1_d16_distinct.npz")
-    opt = run_backward(z, variant, 0, 1, gpu, views=views, bucket_mb=2e-3)
-    assert opt.engine.gb.K > 1 and opt.engine.gb.launched_in_backward > 0
+    opt = run_backward(z, variant, 0, 1, gpu, views=views, bucket_mb=2e-3, arena=arena)
+    k, launched = _overlap_stats(opt)
+    assert k > 1 and launched > 0
 
 
 def test_overlap_bf16_matches_bucket_engine(gpu, pg1):
@@ -47,18 +57,19 @@ def test_overlap_bf16_matches_bucket_engine(gpu, pg1):
     init = [(torch.randn(s, generator=g) * 0.02).to(torch.bfloat16) for s in shapes]
     grads = [[(torch.randn(s, generator=g) * 1e-3).to(torch.bfloat16) for s in shapes] for _ in range(3)]
     out = []
-    for overlap in (False, True):
+    for overlap, arena in ((False, "flat"), (True, "flat"), (True, "buckets")):
         ps = [torch.nn.Parameter(t.clone().to(gpu)) for t in init]
         opt = zero2.ShardedOptimizer(torch.optim.Adam(ps, lr=1e-3), overlap=overlap,
-                                     overlap_bucket_mb=0.01)
+                                     overlap_bucket_mb=0.01, arena=arena)
         for gs in grads:
             opt.zero_grad()
             loss = sum((p.float() * gg.to(gpu).float()).sum() for p, gg in zip(ps, gs))
             loss.backward()
             opt.step()
         out.append([p.detach().cpu().view(torch.int16) for p in ps])
-    for a, b in zip(*out):
-        assert torch.equal(a, b)
+    for other in out[1:]:
+        for a, b in zip(out[0], other):
+            assert torch.equal(a, b)
 
 
 def test_overlap_unused_param_keeps_value(gpu, pg1):
@@ -88,7 +99,7 @@ def test_overlap_double_backward_raises(gpu, pg1):
         ps[0].sum().backward()
 
 
-def _mr_worker(rank, ws, port, variant, name, views):
+def _mr_worker(rank, ws, port, variant, name, views, arena):
     import sys
     from conftest import PKG, REPO  # noqa: F401
     from _gloo_comm import GlooStagedComm
@@ -96,18 +107,21 @@ def _mr_worker(rank, ws, port, variant, name, views):
     torch.cuda.set_device(0)
     init_pg(rank, ws, port)
     z = np.load(GOLDEN / name)
-    run_backward(z, variant, rank, ws, torch.device("cuda:0"), comm=GlooStagedComm(), views=views,
-                 bucket_mb=2e-3)
+    opt = run_backward(z, variant, rank, ws, torch.device("cuda:0"), comm=GlooStagedComm(),
+                       views=views, bucket_mb=2e-3, arena=arena)
+    k, launched = _overlap_stats(opt)
+    assert k >= ws and launched > 0  # buckets reduced while backward was still running
     dist.barrier()
     dist.destroy_process_group()
     sys.stdout.flush()
 
 
+@pytest.mark.parametrize("arena", ["flat", "buckets"])
 @pytest.mark.parametrize("variant", [1, 2])
-@pytest.mark.parametrize("ws,views", [(2, True), (3, True), (3, False)])
-def test_multirank_overlap_backward(gpu, variant, ws, views):
+@pytest.mark.parametrize("ws,views", [(2, True), (3, True), (3, False), (4, True)])
+def test_multirank_overlap_backward(gpu, variant, ws, views, arena):
     name = f"traj_z{variant}_ws{ws}_d16_distinct.npz"
-    spawn_ranks(_mr_worker, ws, (ws, _port(), variant, name, views))
+    spawn_ranks(_mr_worker, ws, (ws, _port(), variant, name, views, arena))
 
 
 # ---------------------------------------------------------------------------------------------
