@@ -313,13 +313,13 @@ class FlatEngine(ShardEngine):
     def _ov_launch(self, k: int, stream=None):
         cur = torch.cuda.current_stream(self.device) if stream is None else stream
         lo, hi, r = int(self.ov_lo[k]), int(self.ov_hi[k]), int(self.ov_owner[k])
-        if self.ws == 1:  # nothing to exchange: Adam reads G
-            self.ov_ev[k].record(cur)
-            return
         if self.grad_comm:  # the bucket's grads as bf16 for the wire (gfx950 RNE kernel)
             from .kernels import convert
 
             convert(self.G[lo:hi], self.Gc[lo:hi], cur)
+        if self.ws == 1:  # nothing to exchange: Adam reads Gc (= G unless converted)
+            self.ov_ev[k].record(cur)
+            return
         ev = torch.cuda.Event()
         ev.record(cur)
         cs = self.comm_stream
