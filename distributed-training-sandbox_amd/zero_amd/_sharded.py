@@ -106,6 +106,7 @@ class ShardedOptimizerBase:
             # params become views of the arena now, so zero_grad() can hand out grad views
             # before the first step (every rank builds it: the communicator is a collective)
             self._build_engine()
+            self._overlap_hooks = self.engine.register_marks()
 
     def _flat(self) -> bool:
         return self._arena == "flat" and self._layout == "reference"

@@ -122,6 +122,12 @@ class FlatEngine(ShardEngine):
         self.ev_c0 = torch.cuda.Event(enable_timing=True)
         self.ev_c1 = torch.cuda.Event(enable_timing=True)
         self.capture_reduced = None  # optional tensor: a copy of R after the reduces (checks)
+        # which parameters backward touched since zero_grad() (post-accumulate-grad hooks): a view
+        # nobody accumulated into is NO gradient (the reference's p.grad is None after zero_grad),
+        # unless no backward ran at all (grads written into the views by hand)
+        self.touched = np.zeros(n, bool)
+        self.any_touched = False
+        self._mark_hooks = []
         self.overlap = False  # backward-overlapped reduces (enable_overlap)
         self.ov_K = 0
         self.launched_in_backward = 0
@@ -181,6 +187,8 @@ class FlatEngine(ShardEngine):
         self.dirty[:] = False
         self.install_views()
         self.zero_grad_calls += 1
+        self.touched[:] = False
+        self.any_touched = False
         if self.overlap:
             self._ov_reset()
 
@@ -252,6 +260,15 @@ class FlatEngine(ShardEngine):
                     s0 = int(self.base[r]) + rd.j * self.W
                     comm.broadcast(self.P[s0:s0 + c], r, cs)
 
+    def register_marks(self):
+        """Post-accumulate-grad hooks that only record which parameters backward reached."""
+        def mark(i):
+            self.touched[i] = True
+            self.any_touched = True
+        self._mark_hooks = [p.register_post_accumulate_grad_hook(lambda _p, i=i: mark(i))
+                            for i, p in enumerate(self.params) if p.requires_grad]
+        return self._mark_hooks
+
     # ------------------------------------------------------------------------------------------
     # Backward overlap (SURVEY.md §8(f) 1) on the flat arena
     def enable_overlap(self, bucket_bytes: int):
@@ -277,7 +294,9 @@ class FlatEngine(ShardEngine):
         self.ov_bucket_of = np.zeros(n, np.int64)
         for k, g in enumerate(groups):
             self.ov_bucket_of[g] = k
-        self.ov_size = np.array([len(g) for g in groups], np.int64)
+        # only parameters that can receive a gradient are waited for (a frozen one never fires)
+        req = np.array([p.requires_grad for p in self.params], bool)
+        self.ov_size = np.array([int(req[g].sum()) for g in groups], np.int64)
         self.ov_ev = [torch.cuda.Event() for _ in range(self.ov_K)]
         own = np.nonzero(self.ov_owner == self.rank)[0]
         self.ov_last_own = int(own[-1]) if len(own) else -1
@@ -301,6 +320,8 @@ class FlatEngine(ShardEngine):
                 "zero_amd: gradient of parameter %d accumulated twice before step(); the "
                 "backward-overlapped mode reduces each gradient once per step" % i)
         self.ov_marked[i] = True
+        self.touched[i] = True
+        self.any_touched = True
         g = self.params[i].grad
         if g is not None and not self.is_view(i, g):  # a fresh grad (the caller cleared the view)
             self.grad_view(i).copy_(g.reshape(self.params[i].shape))
@@ -395,10 +416,12 @@ class FlatEngine(ShardEngine):
         stream = torch.cuda.current_stream(self.device) if stream is None else stream
         n = len(self.params)
         es = self.es
-        has = np.fromiter((g is not None for g in grads), bool, n)
         vw = self._views
         view = np.fromiter((g is not None and (g is vw[i] or self.is_view(i, g))
                             for i, g in enumerate(grads)), bool, n)
+        has = np.fromiter((g is not None for g in grads), bool, n)
+        if self.any_touched:  # a backward ran: an arena view it did not reach carries no gradient
+            has &= ~view | self.touched
         if any(hparams_of(g)["amsgrad"] for g in set(self.group_of)) and self.vmax is None:
             self.ensure_vmax()
             self.rebuild_rows()

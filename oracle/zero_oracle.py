@@ -172,6 +172,8 @@ def simulate(variant: int, ws: int, init, xs=None, ys=None, steps: int = 10, lr:
             else:
                 g = [local_grads(t, r, i) for i in range(n)]
             for i in range(n):
+                if g[i] is None:  # no gradient this step (frozen or unused parameter)
+                    continue
                 if variant == 3:
                     held[r][i] = np.array(g[i], F32)
                 else:  # backward accumulates into a surviving grad (ZeRO-1 carry)
@@ -179,6 +181,10 @@ def simulate(variant: int, ws: int, init, xs=None, ys=None, steps: int = 10, lr:
         reduced = [[] for _ in range(ws)]
         if variant == 1:  # zero1.py:80-84: all_reduce(SUM) then /ws on every param, every rank
             for i in range(n):
+                if all(held[r][i] is None for r in range(ws)):  # `if p.grad is not None` everywhere
+                    for r in range(ws):
+                        reduced[r].append(None)
+                    continue
                 a = (_sum_ranks([held[r][i] for r in range(ws)]) / F32(ws)).astype(F32)
                 for r in range(ws):
                     held[r][i] = a.copy()
@@ -187,6 +193,11 @@ def simulate(variant: int, ws: int, init, xs=None, ys=None, steps: int = 10, lr:
         elif variant == 2:  # zero2.py:94-113: reduce_scatter of ws copies == all-reduce; owner /ws
             own_grad = [dict() for _ in range(ws)]
             for i in range(n):
+                if all(held[r][i] is None for r in range(ws)):  # no grad anywhere: no collective
+                    for r in range(ws):
+                        own_grad[r][i] = None
+                        reduced[r].append(None)
+                    continue
                 if grad_comm == "bf16":
                     ssum = bf16_round(_sum_ranks([bf16_round(held[r][i].reshape(-1))
                                                   for r in range(ws)]))
@@ -219,6 +230,8 @@ def simulate(variant: int, ws: int, init, xs=None, ys=None, steps: int = 10, lr:
             for r in range(ws):
                 s, e = owner_range(n, ws, r)
                 for i in range(s, e):
+                    if grads_for(r, i) is None:  # torch Adam skips a parameter without a grad
+                        continue
                     z0 = np.zeros_like(init[i])
                     st, m, v, vm = state[r].get(i, (0, z0, z0, z0))
                     st += 1

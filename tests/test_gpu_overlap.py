@@ -116,6 +116,58 @@ def _mr_worker(rank, ws, port, variant, name, views, arena):
     sys.stdout.flush()
 
 
+def _frozen_worker(rank, ws, port, variant, overlap):
+    """A frozen parameter (requires_grad=False) and one the loss reaches only at step 0: without a
+    gradient Adam skips a parameter (the reference's `p.grad is None`, zero2.py:99-101) — so the
+    second one keeps its step-0 value although its Adam moments are non-zero — every rank ends
+    bit-identical, and the frozen one does not hold back the overlapped reduces of later buckets."""
+    import sys
+    from conftest import PKG, REPO  # noqa: F401
+    from _gloo_comm import GlooStagedComm
+    from _zero_run import module_for, rel
+    from oracle import zero_oracle as zo
+
+    torch.cuda.set_device(0)
+    init_pg(rank, ws, port)
+    dev = torch.device("cuda:0")
+    shapes = [(40, 8), (40,), (24, 8), (24,), (16, 8), (16,)]
+    frozen, unused = 2, 4
+    g = torch.Generator().manual_seed(21)
+    init = [torch.randn(s, generator=g).numpy() for s in shapes]
+    steps = 3
+    lg = {(t, r, i): (torch.randn(s, generator=torch.Generator().manual_seed(100 * t + 10 * r + i))
+                      * 1e-2).numpy() for t in range(steps) for r in range(ws) for i, s in enumerate(shapes)}
+    # ZeRO-1: the reference's owner and non-owners would disagree about a parameter that loses
+    # its gradient after step 0 (the non-owners' surviving averaged grad vs the owner's None, a
+    # mismatched all_reduce, zero1.py:81-84), so there the second parameter is never reached
+    skip = lambda t, i: i == frozen or (i == unused and (t > 0 or variant == 1))  # noqa: E731
+    grad_of = lambda t, r, i: None if skip(t, i) else lg[(t, r, i)]  # noqa: E731
+    want = zo.simulate(variant, ws, init, steps=steps, local_grads=grad_of)
+    params = [torch.nn.Parameter(torch.from_numpy(a.copy()).to(dev), requires_grad=i != frozen)
+              for i, a in enumerate(init)]
+    opt = module_for(variant).ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=GlooStagedComm(),
+                                               overlap=overlap, overlap_bucket_mb=1e-3)
+    for t in range(steps):
+        opt.zero_grad()
+        loss = sum((p * torch.from_numpy(lg[(t, rank, i)].copy()).to(dev)).sum()
+                   for i, p in enumerate(params) if not skip(t, i))
+        loss.backward()
+        opt.step()
+        for i, p in enumerate(params):
+            assert rel(p.detach().cpu().numpy(), want["params"][t][rank][i]) <= 1e-6, (variant, rank, t, i)
+        assert torch.equal(params[frozen].detach().cpu(), torch.from_numpy(init[frozen]))
+    assert not overlap or opt.engine.launched_in_backward > 0
+    dist.barrier()
+    dist.destroy_process_group()
+    sys.stdout.flush()
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+@pytest.mark.parametrize("variant", [1, 2])
+def test_frozen_and_unused_params(gpu, variant, overlap):
+    spawn_ranks(_frozen_worker, 2, (2, _port(), variant, overlap))
+
+
 @pytest.mark.parametrize("arena", ["flat", "buckets"])
 @pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("ws,views", [(2, True), (3, True), (3, False), (4, True)])

@@ -373,20 +373,21 @@ def _bf16comm_worker(rank, ws, port, which):
     init = [z[f"init_{i}"] for i in range(12)]
     want = zo.simulate(2, ws, init, local_grads=lambda t, r, i: z[f"r{r}_t{t}_lg{i}"], grad_comm="bf16")
     params = [torch.nn.Parameter(torch.from_numpy(a.copy()).to(dev)) for a in init]
-    if which == "zero2":
+    if which in ("zero2", "zero2_overlap"):
         opt = zero2.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=GlooStagedComm(),
-                                     bucket_mb=ws * 64 * 4 / (1 << 20), grad_comm="bf16")
+                                     bucket_mb=ws * 64 * 4 / (1 << 20), grad_comm="bf16",
+                                     overlap=which == "zero2_overlap", overlap_bucket_mb=2e-3)
         assert opt.engine.R.dtype == torch.bfloat16
     else:
         opt = zero3.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), update=True,
                                      comm=GlooStagedComm(), grad_comm="bf16")
         assert opt.grad_arena().dtype == torch.bfloat16
-    cs = lambda a: a if which == "zero2" else a[rank * -(-a.shape[0] // ws):(rank + 1) * -(-a.shape[0] // ws)]  # noqa: E731
+    cs = lambda a: a if which != "zero3" else a[rank * -(-a.shape[0] // ws):(rank + 1) * -(-a.shape[0] // ws)]  # noqa: E731
     for t in range(int(z["steps"])):
         opt.zero_grad()
         for i, p in enumerate(params):
             g = torch.from_numpy(z[f"r{rank}_t{t}_lg{i}"].copy()).to(dev)
-            if which == "zero2":
+            if which != "zero3":
                 set_grad(p, g)
             else:  # a full-size grad on a sharded param, as autograd leaves it
                 shard = p.data
@@ -403,7 +404,8 @@ def _bf16comm_worker(rank, ws, port, which):
     sys.stdout.flush()
 
 
-@pytest.mark.parametrize("which,ws", [("zero2", 3), ("zero2", 4), ("zero3", 3), ("zero3", 4)])
+@pytest.mark.parametrize("which,ws", [("zero2", 3), ("zero2", 4), ("zero2_overlap", 3), ("zero3", 3),
+                                     ("zero3", 4)])
 def test_bf16_gradient_exchange_for_fp32_params(gpu, which, ws):
     spawn_ranks(_bf16comm_worker, ws, (ws, _port(), which))
 

@@ -18,8 +18,10 @@ run --config C3 --dtype fp32 --zero 2
 run --config C4 --zero 2
 run --config C4 --zero 2 --master fp32
 run --config C4 --zero 1
-run --config C5 --zero 2
-run --config C5 --zero 3
+run --config C5 --zero 2 --steps 50
+run --config C5 --zero 3 --steps 50
 run --config C3 --dtype fp32 --zero 3
-run --config C4 --simulate-ws 8 --steps 5 --warmup 1
-run --config C5 --simulate-ws 8 --steps 5 --warmup 1
+run --config C4 --simulate-ws 8 --steps 20 --warmup 2
+run --config C4 --zero 1 --simulate-ws 8 --steps 20 --warmup 2
+run --config C5 --simulate-ws 8 --steps 10 --warmup 2
+run --config C5 --zero 3 --simulate-ws 8 --steps 10 --warmup 2
