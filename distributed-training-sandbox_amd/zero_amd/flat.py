@@ -105,8 +105,8 @@ class FlatEngine(ShardEngine):
         self.czdtype = _lib.ZS_BF16 if self.grad_comm else self.zdtype
         # ws == 1: nothing to reduce — Adam reads the gradient arena itself (R aliases Gc) and the
         # step is one round with no collective; the arena still places P and G by probe
-        self.R = (self.Gc if ws == 1 else
-                  torch.zeros(max(int(self.Ls[rank]), ALIGN_ELEMS), dtype=cdt, device=dev))
+        self.R = (self.Gc if ws == 1 else  # Adam streams R every step: placed by probe as well
+                  _zeros_placed(max(int(self.Ls[rank]), ALIGN_ELEMS), cdt, dev, placement_tries)[0])
         self.dirty = np.zeros(n, bool)  # G slot may hold a stale gradient
         self.zero_grad_calls = 0
         W = max(ALIGN_ELEMS, (int(bucket_bytes) // (ws * es)) // ALIGN_ELEMS * ALIGN_ELEMS)
