@@ -888,7 +888,8 @@ def bench_train_smollm3(args, world, rank, dev, use_nccl):
         opt = zero3.ShardedOptimizer(torch.optim.AdamW(model.parameters(), lr=1e-5), update=True,
                                      sync=False, bucket_mb=args.bucket_mb or 128.0, **kw)
         # one gather group per decoder layer (FSDP2 fully_shard per block, train_fsdp.py:90-97)
-        zero3.register_zero3_hooks(model, opt.param_managers, units=list(model.model.layers))
+        zero3.register_zero3_hooks(model, opt.param_managers, units=list(model.model.layers),
+                                   reshard_after_forward=not args.no_reshard)
     else:
         opt = zero2.ShardedOptimizer(torch.optim.AdamW(model.parameters(), lr=1e-5), overlap=True,
                                      sync=False, arena="buckets" if args.arena == "buckets" else "flat")
@@ -928,7 +929,9 @@ def bench_train_smollm3(args, world, rank, dev, use_nccl):
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random tokens, random init)",
             "config": {"workload": ("SmolLM3 causal-LM training step, ZeRO-3 AdamW(lr=1e-5), "
-                                    "per-module gathers, backward reduce-scatters"
+                                    "per-layer gathers" + (" (kept through backward: FSDP2 "
+                                    "reshard_after_forward=False)" if args.no_reshard else "") +
+                                    ", backward reduce-scatters"
                                     if args.zero == 3 else
                                     "SmolLM3 causal-LM training step, ZeRO-2 AdamW(lr=1e-5) "
                                     "backward-overlapped"), "params": int(params),
@@ -967,6 +970,9 @@ def main():
     ap.add_argument("--seq", type=int, default=8192, help="--train sequence length "
                     "(fsdp/train_fsdp.py:44: 8192)")
     ap.add_argument("--train-layers", type=int, default=None, help="--train: fewer decoder layers")
+    ap.add_argument("--no-reshard", action="store_true",
+                    help="--train --zero 3: keep gathered parameters from forward through backward "
+                         "(FSDP2 reshard_after_forward=False, the reference's 'ZeRO-2' run)")
     ap.add_argument("--set-layers", type=int, default=None,
                     help="--zero 3 on C4/C5: a copy of the parameter set with fewer decoder layers "
                          "(tests)")

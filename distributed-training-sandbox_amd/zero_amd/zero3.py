@@ -321,7 +321,7 @@ class Zero3ParamManager:
         self.full_data = None
 
 
-def register_zero3_hooks(model, param_managers, units=None):
+def register_zero3_hooks(model, param_managers, units=None, reshard_after_forward=True):
     """zero3.py:56-77: forward / backward pre-hooks materialise a module's direct parameters (one
     grouped all-gather, prefetched on the side stream), post-hooks release them.
 
@@ -329,7 +329,12 @@ def register_zero3_hooks(model, param_managers, units=None):
     group each — every managed parameter anywhere inside a unit is materialised by the unit's
     pre-hooks and released by its post-hooks, as FSDP2's ``fully_shard`` of each transformer block
     does (fsdp/train_fsdp.py:90-97).  One RCCL group and four hooks per block instead of per
-    Linear / norm.  Modules outside every unit keep per-module gathers of their direct params."""
+    Linear / norm.  Modules outside every unit keep per-module gathers of their direct params.
+
+    ``reshard_after_forward`` (FSDP2's flag, fsdp/train_fsdp.py:84-94): True (the reference's
+    hooks, FSDP2 "ZeRO-3") releases after forward and gathers again for backward; False (FSDP2
+    "ZeRO-2") keeps the gathered parameters from forward through backward — one gather per group
+    per step instead of two, full parameters resident between forward and backward."""
     if all(m.world_size == 1 and not m.fp8 for m in param_managers.values()):
         # one rank: every shard is its whole parameter, so materialize / release are identities —
         # hooks would only cost host time (a forward whose host enqueue falls behind the GPU)
@@ -367,6 +372,9 @@ def register_zero3_hooks(model, param_managers, units=None):
             ms = mod_managers.get(id(module)) or []
             if not ms:
                 return None
+            if phase == "bwd" and not reshard_after_forward and all(
+                    m.full_data is not None for m in ms):
+                return None  # still gathered from forward
             rt = ms[0].runtime
             if rt is None:
                 for m in ms:
@@ -376,10 +384,14 @@ def register_zero3_hooks(model, param_managers, units=None):
             return None
         return pre_hook
 
-    def post_hook(module, *args):
-        for m in mod_managers.get(id(module)) or []:
-            m.release()
-        return None
+    def make_post(phase):
+        def post_hook(module, *args):
+            if phase == "fwd" and not reshard_after_forward:
+                return None  # kept for backward
+            for m in mod_managers.get(id(module)) or []:
+                m.release()
+            return None
+        return post_hook
 
     handles = []
     for m in model.modules():
@@ -389,9 +401,9 @@ def register_zero3_hooks(model, param_managers, units=None):
         if not mod_managers[id(m)]:
             continue
         handles.append(m.register_forward_pre_hook(make_pre("fwd")))
-        handles.append(m.register_forward_hook(post_hook))
+        handles.append(m.register_forward_hook(make_post("fwd")))
         handles.append(m.register_full_backward_pre_hook(make_pre("bwd")))
-        handles.append(m.register_full_backward_hook(post_hook))
+        handles.append(m.register_full_backward_hook(make_post("bwd")))
     return handles
 
 

@@ -54,7 +54,7 @@ def test_smollm3_zero2_adamw_overlap_bit_exact(gpu):
         dist.destroy_process_group()
 
 
-def _zero3_smollm3(rank, ws, port, dev, units=False):
+def _zero3_smollm3(rank, ws, port, dev, units=False, reshard=True):
     """One rank of a SmolLM3 ZeRO-3 run (update mode, AdamW, hooks on every module with
     parameters).  Every rank trains on the SAME batch, so the reduce-scattered sum of a chunk is
     exactly ws times this rank's own gradient and the mean is exact: each rank's chunks then equal
@@ -81,7 +81,8 @@ def _zero3_smollm3(rank, ws, port, dev, units=False):
     opt = zero3.ShardedOptimizer(torch.optim.AdamW(params, lr=lr, weight_decay=wd), update=True,
                                  bucket_mb=0.05, **kw)
     zero3.register_zero3_hooks(model, opt.param_managers,
-                               units=list(model.model.layers) if units else None)
+                               units=list(model.model.layers) if units else None,
+                               reshard_after_forward=reshard)
     ar = opt._arena
     hi, lo, m, v = [], [], [], []
     for i, p in enumerate(params):
@@ -104,6 +105,14 @@ def _zero3_smollm3(rank, ws, port, dev, units=False):
             got = p.detach().reshape(-1).view(torch.int16).cpu().numpy().view(np.uint16)
             assert np.array_equal(got, hi[i]), (rank, t, i)
     assert ws == 1 or opt.runtime.n_prefetch_hits > 0  # (ws=1: no hooks, nothing to gather)
+    if ws > 1:  # gather groups per iteration: forward AND backward, or forward only (FSDP2 ZeRO-2)
+        groups = len(set(k[1] for k in opt.runtime.key_managers))
+        n = opt.runtime.n_gathers  # over 3 iterations, +1: the prefetch for a 4th
+        if reshard:
+            assert n in (6 * groups, 6 * groups + 1), (n, groups)
+        else:  # forward gathers only — except the tied embedding, which lm_head's backward
+            # releases before the embedding's backward needs it again
+            assert 3 * groups <= n <= 3 * (groups + 1) + 1, (n, groups)
 
 
 def test_smollm3_zero3_adamw_bit_exact(gpu):
@@ -115,20 +124,22 @@ def test_smollm3_zero3_adamw_bit_exact(gpu):
         dist.destroy_process_group()
 
 
-def _mr_zero3(rank, ws, port, units):
+def _mr_zero3(rank, ws, port, units, reshard=True):
     torch.cuda.set_device(0)
     init_pg(rank, ws, port)
     try:
-        _zero3_smollm3(rank, ws, port, torch.device("cuda:0"), units)
+        _zero3_smollm3(rank, ws, port, torch.device("cuda:0"), units, reshard)
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("units", [False, True])
-def test_smollm3_zero3_two_ranks_bit_exact(gpu, units):
-    """units=True: one gather group per decoder layer (FSDP2's per-block fully_shard)."""
+@pytest.mark.parametrize("units,reshard", [(False, True), (True, True), (True, False)])
+def test_smollm3_zero3_two_ranks_bit_exact(gpu, units, reshard):
+    """units=True: one gather group per decoder layer (FSDP2's per-block fully_shard);
+    reshard=False: parameters stay gathered from forward through backward (FSDP2's
+    reshard_after_forward=False, the reference's "ZeRO-2" run, fsdp/train_fsdp.py:84-86)."""
     from conftest import free_port
     from _zero_run import spawn_ranks
 
-    spawn_ranks(_mr_zero3, 2, (2, free_port(), units))
+    spawn_ranks(_mr_zero3, 2, (2, free_port(), units, reshard))
