@@ -54,7 +54,7 @@ PROBE_MIN_BYTES = 1 << 30
 PROBE_ACCEPT_GBS = 5950.0
 
 
-def probed_zeros(n: int, dtype, device, tries: int = 5, accept_gbs: float = PROBE_ACCEPT_GBS):
+def probed_zeros(n: int, dtype, device, tries: int = 8, accept_gbs: float = PROBE_ACCEPT_GBS):
     """A zero-filled buffer for a long-lived, bandwidth-bound stream, placed by measurement.
 
     Streaming bandwidth depends on WHERE in VRAM an allocation lands, stably per allocation:
@@ -109,7 +109,7 @@ def probed_zeros(n: int, dtype, device, tries: int = 5, accept_gbs: float = PROB
 class ShardEngine:
     def __init__(self, params, group_of, ws: int, rank: int, *, layout="reference", carry=False,
                  comm=None, bucket_bytes: int = 256 << 20, align: int = ALIGN_ELEMS,
-                 buckets: str = "ragged", placement_tries: int = 5, master: str = "split"):
+                 buckets: str = "ragged", placement_tries: int = 8, master: str = "split"):
         if not params:
             raise ValueError("ShardEngine: no parameters")
         dev = params[0].device

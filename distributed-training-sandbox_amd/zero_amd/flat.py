@@ -62,7 +62,7 @@ class _Round:
 
 class FlatEngine(ShardEngine):
     def __init__(self, params, group_of, ws: int, rank: int, *, carry=False, comm=None,
-                 bucket_bytes: int = 256 << 20, master: str = "split", placement_tries: int = 5,
+                 bucket_bytes: int = 256 << 20, master: str = "split", placement_tries: int = 8,
                  grad_comm: str | None = None):
         # the base class gives the reference layout's streams, the optimizer state and the Adam
         # launch machinery; its bucket plan (one bucket) is unused
