@@ -62,7 +62,7 @@ def test_fp8_rows_kernels_bit_exact(gpu, rows, row_len, dtype):
     assert torch.equal(y.cpu(), want)
 
 
-def _check_materialize(rank, ws, dtype, comm=None):
+def _check_materialize(rank, ws, dtype, comm=None, reshard=True):
     from zero_amd import zero3
 
     dev = torch.device("cuda:0")
@@ -83,13 +83,18 @@ def _check_materialize(rank, ws, dtype, comm=None):
             want = f
         assert torch.equal(got, want), (rank, tuple(f.shape))
         man.release()
-    # a hooked training iteration runs on fp8-gathered weights
-    zero3.register_zero3_hooks(model, opt.param_managers)
+    # a hooked training iteration runs on fp8-gathered weights (reshard=False: gathered once,
+    # kept from forward through backward)
+    zero3.register_zero3_hooks(model, opt.param_managers, reshard_after_forward=reshard)
     x = torch.randn(8, 40, device=dev).to(dtype)
+    n0 = opt.runtime.n_gathers
     loss = model(x).float().pow(2).mean()
     loss.backward()
     opt.step()
     assert torch.isfinite(loss)
+    if ws > 1:  # two Linear modules: gathered in forward, and again in backward unless kept
+        assert opt.runtime.n_gathers - n0 in ((4, 5) if reshard else (2, 3))
+    assert all(m.full_data is None for m in opt.param_managers.values())  # released after backward
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
@@ -101,17 +106,17 @@ def test_zero3_fp8_gather_ws1(gpu, dtype):
         dist.destroy_process_group()
 
 
-def _mr(rank, ws, port):
+def _mr(rank, ws, port, reshard=True):
     from conftest import PKG, REPO  # noqa: F401
     from _gloo_comm import GlooStagedComm
 
     torch.cuda.set_device(0)
     init_pg(rank, ws, port)
-    _check_materialize(rank, ws, torch.bfloat16, comm=GlooStagedComm())
+    _check_materialize(rank, ws, torch.bfloat16, comm=GlooStagedComm(), reshard=reshard)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws", [2, 3])
-def test_zero3_fp8_gather_multirank(gpu, ws):
-    spawn_ranks(_mr, ws, (ws, _port()))
+@pytest.mark.parametrize("ws,reshard", [(2, True), (3, True), (2, False)])
+def test_zero3_fp8_gather_multirank(gpu, ws, reshard):
+    spawn_ranks(_mr, ws, (ws, _port(), reshard))

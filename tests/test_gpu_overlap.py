@@ -176,6 +176,13 @@ def test_multirank_overlap_backward(gpu, variant, ws, views, arena):
     spawn_ranks(_mr_worker, ws, (ws, _port(), variant, name, views, arena))
 
 
+@pytest.mark.parametrize("variant", [1, 2])
+def test_multirank_overlap_backward_ws8_flat(gpu, variant):
+    """ws=8 (12 parameters: ranks 4-7 own one each) through a real backward on the flat arena."""
+    name = f"traj_z{variant}_ws8_d16_distinct.npz"
+    spawn_ranks(_mr_worker, 8, (8, _port(), variant, name, True, "flat"))
+
+
 # ---------------------------------------------------------------------------------------------
 # DDP
 def _ddp_grads(ws, shapes, step):
