@@ -1293,7 +1293,9 @@ def main():
         }
         out["step_roofline"] = step_roofline
         out["placement"] = {"state": eng.placement,
-                            "arena": getattr(eng, "arena_placement", None)}
+                            "arena": getattr(eng, "arena_placement", None),
+                            "grads": getattr(eng, "grad_placement", None),
+                            "reduced": getattr(eng, "reduced_placement", None)}
         if selfcheck is not None:
             out["rccl_selfcheck"] = selfcheck
         if exchange_check:

@@ -90,7 +90,7 @@ class FlatEngine(ShardEngine):
                 s = int(self.slot[i])
                 self.P[s:s + int(self.numel[i])].copy_(p.detach().reshape(-1))
                 p.data = self.P[s:s + int(self.numel[i])].view(p.shape)
-        self.G, _ = _zeros_placed(total, dt, dev, placement_tries)
+        self.G, self.grad_placement = _zeros_placed(total, dt, dev, placement_tries)
         # bf16 gradient exchange for fp32 parameters: G is converted into Gc
         # (bf16, same layout) before the reduces, which then move and sum 2 B per element; Adam
         # reads the bf16 sum (its fp32 master is the fp32 parameter itself)
@@ -105,8 +105,12 @@ class FlatEngine(ShardEngine):
         self.czdtype = _lib.ZS_BF16 if self.grad_comm else self.zdtype
         # ws == 1: nothing to reduce — Adam reads the gradient arena itself (R aliases Gc) and the
         # step is one round with no collective; the arena still places P and G by probe
-        self.R = (self.Gc if ws == 1 else  # Adam streams R every step: placed by probe as well
-                  _zeros_placed(max(int(self.Ls[rank]), ALIGN_ELEMS), cdt, dev, placement_tries)[0])
+        self.reduced_placement = None
+        if ws == 1:
+            self.R = self.Gc
+        else:  # Adam streams R every step: placed by probe as well
+            self.R, self.reduced_placement = _zeros_placed(max(int(self.Ls[rank]), ALIGN_ELEMS), cdt,
+                                                           dev, placement_tries)
         self.dirty = np.zeros(n, bool)  # G slot may hold a stale gradient
         self.zero_grad_calls = 0
         W = max(ALIGN_ELEMS, (int(bucket_bytes) // (ws * es)) // ALIGN_ELEMS * ALIGN_ELEMS)
