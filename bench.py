@@ -64,25 +64,25 @@ def cpu_baseline(shapes, sample_elems: int, variant: int = 2, min_seconds: float
     grads = [torch.randn(s, generator=g) * 1e-3 for s in sel]
     opt = ReferenceStepCPU(ps, variant=variant if variant in (1, 2) else 2)
 
-    def one():
+    def feed():  # what backward leaves (outside the timing: only step() is the reference's step)
         opt.zero_grad()
         for p, gr in zip(ps, grads):
             p.grad = gr.clone() if p.grad is None else p.grad.add_(gr)
-        opt.step()
 
-    one()  # Adam state allocation outside the timing
-    steps, t0 = 0, time.perf_counter()
-    while True:
-        one()
+    feed()
+    opt.step()  # Adam state allocation outside the timing
+    steps, el = 0, 0.0
+    while el < min_seconds and steps < 100:
+        feed()
+        t0 = time.perf_counter()
+        opt.step()
+        el += time.perf_counter() - t0
         steps += 1
-        el = time.perf_counter() - t0
-        if el >= min_seconds or steps >= 100:
-            break
     return dict(value=n * steps / el, unit="params/s", cores=torch.get_num_threads(), kind="port",
                 sample=f"first {n:,} params ({len(sel)} leading tensors of the set, fp32), "
                        f"{steps} steps of the reference's ZeRO-{variant if variant in (1, 2) else 2} "
                        f"step restated on CPU (per-tensor gloo collectives + torch.optim.Adam, "
-                       f"oracle/zero_cpu_step.py), {el:.1f} s; torch {torch.__version__}")
+                       f"oracle/zero_cpu_step.py), {el:.1f} s of step(); torch {torch.__version__}")
 
 
 def cpu_oracle_adam(shapes, sample_elems: int, min_seconds: float = 6.0, split: bool = True):
