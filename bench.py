@@ -228,6 +228,22 @@ def comm_selfcheck(comm, world, rank, dev):
 
 
 _PHASE = ["start"]
+_REHEARSAL = [None]  # --share-gpu: set to a note that goes into the JSON line
+
+
+class _stdout_to_stderr:
+    """Point fd 1 at stderr for the block (native libraries write there, not to sys.stdout)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self._saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self._saved, 1)
+        os.close(self._saved)
+        return False
 
 
 def _phase(name: str) -> None:
@@ -455,6 +471,8 @@ def _zero3_report(args, opt, world, rank, red_dev, el, total, workload, extra):
         if comm is not None:
             out["collectives"] = comm
         out.update(extra)
+        if _REHEARSAL[0]:
+            out["rehearsal"] = _REHEARSAL[0]
         print(json.dumps(out), flush=True)
 
 
@@ -1003,6 +1021,10 @@ def main():
                     help="DIAGNOSTIC (N=1 only): run the ws>1 bucket path of rank 0 of a ws-rank job "
                          "with the collectives replaced by no-ops, to time pack / Adam / unpack "
                          "at that layout; prints a diagnostic line, not the metric")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="REHEARSAL on a one-GPU box: all ranks on one device, real RCCL between "
+                         "them over its socket transport (per-rank NCCL_HOSTID); the exchange "
+                         "checks and calibration run for real, the timings mean nothing")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "c10d", "gloo-staged"],
                     help="rccl: the library's own RCCL communicator; c10d: the same RCCL through "
                          "torch.distributed (A/B); gloo-staged = TEST ONLY (tests/_gloo_comm.py): "
@@ -1034,13 +1056,24 @@ def main():
         log(f"note: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE")
     if args.comm == "gloo-staged":  # test-only: every rank shares the box's GPUs round-robin
         local = local % torch.cuda.device_count()
+    if args.share_gpu and world > 1:
+        # rehearsal on a one-GPU box: every rank on the same device, each one a separate "node"
+        # to RCCL (its own NCCL_HOSTID), so the real RCCL collectives run between the ranks
+        # through RCCL's socket transport over loopback; read before RCCL's first init
+        local = local % torch.cuda.device_count()
+        os.environ["NCCL_HOSTID"] = f"zs-share-gpu-rank{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
+        _REHEARSAL[0] = ("share-gpu: every rank on ONE device, RCCL between them over its socket "
+                         "transport (checks are real, timings are not xGMI's)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29531")
     use_nccl = world > 1 and args.comm in ("rccl", "c10d")
-    dist.init_process_group("nccl" if use_nccl else "gloo", rank=rank, world_size=world,
-                            device_id=dev if use_nccl else None)
+    with _stdout_to_stderr():  # gloo prints a connection banner on stdout: keep ONE JSON line there
+        dist.init_process_group("nccl" if use_nccl else "gloo", rank=rank, world_size=world,
+                                device_id=dev if use_nccl else None)
 
     if args.train == "smollm3":
         return bench_train_smollm3(args, world, rank, dev, use_nccl)
@@ -1313,6 +1346,8 @@ def main():
             out["cpu_baseline"] = cpu_baseline(shapes, args.cpu_sample, variant=args.zero)
             out["cpu_oracle_adam"] = cpu_oracle_adam(
                 shapes, args.cpu_sample, split=args.dtype == "bf16" and args.master == "split")
+        if _REHEARSAL[0]:
+            out["rehearsal"] = _REHEARSAL[0]
         print(json.dumps(out), flush=True)
     _teardown(opt)
     dist.destroy_process_group()

@@ -12,6 +12,7 @@ that reads a collective's output, or frees one of its buffers, inside the group 
 it would be on the device.
 """
 import contextlib
+import os
 
 import torch
 import torch.distributed as dist
@@ -188,6 +189,23 @@ def _add_table_methods(cls):
 
 
 _add_table_methods(GlooStagedComm)
+
+
+def test_comm(group=None):
+    """The multi-rank GPU workers' communicator.  Default: GlooStagedComm.  With
+    ``ZS_TEST_COMM=rccl`` (tests/test_gpu_rccl.py): the PRODUCT communicator, RcclComm — every rank
+    of the one-GPU box is made a separate node to RCCL by its own NCCL_HOSTID, so RCCL accepts the
+    shared device and runs its real collectives (its kernels, ring order and bf16 rounding) between
+    the ranks through the socket transport over loopback.  NCCL_HOSTID is read at communicator
+    init, so it is set here, per rank, just before."""
+    if os.environ.get("ZS_TEST_COMM", "") != "rccl":
+        return GlooStagedComm(group)
+    from zero_amd.comm import RcclComm
+
+    os.environ["NCCL_HOSTID"] = f"zs-test-rank{dist.get_rank()}"
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    os.environ.setdefault("NCCL_IB_DISABLE", "1")
+    return RcclComm(group)
 
 
 class SimRankComm:

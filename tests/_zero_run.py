@@ -146,6 +146,38 @@ def _shifted(i, fn, args):
     fn(i + 1, *args)
 
 
+def _child(i, fn, args, deadline_s):
+    import faulthandler
+    import sys
+
+    # a rank stuck in a device-side wait (a peer died inside a collective) dumps its stack and
+    # exits on its own instead of holding the GPU
+    faulthandler.dump_traceback_later(deadline_s, exit=True, file=sys.stderr)
+    fn(i, *args)
+
+
+def spawn_all_ranks(fn, ws: int, args=(), deadline_s: float = 150.0):
+    """Run ``fn(rank, *args)`` for every rank in a SPAWNED process (the caller touches no device
+    and only watches): when any rank fails, the others are terminated at once — needed with RCCL,
+    whose collectives never time out, so a rank whose peer died would otherwise wait on the GPU
+    forever.  Every rank also exits by itself after ``deadline_s``."""
+    import time
+
+    import torch.multiprocessing as mp
+
+    ctx = mp.start_processes(_child, args=(fn, args, deadline_s), nprocs=ws, join=False,
+                             start_method="spawn")
+    t_end = time.time() + deadline_s + 30
+    try:
+        while not ctx.join(timeout=1.0):  # raises (and kills the rest) when a rank fails
+            if time.time() > t_end:
+                raise TimeoutError(f"ranks still running after {deadline_s + 30:.0f} s")
+    finally:
+        for p in ctx.processes:
+            if p.is_alive():
+                p.kill()
+
+
 def spawn_ranks(fn, ws: int, args=()):
     """Run ``fn(rank, *args)`` for every rank of a ws-rank job: rank 0 in THIS process, ranks
     1..ws-1 spawned.  So a ws-rank GPU test puts exactly ws processes on the box's GPU (the

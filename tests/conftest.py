@@ -39,6 +39,15 @@ def free_port() -> int:
     raise RuntimeError("no free port in 20000-32000")
 
 
+def pytest_runtest_logreport(report):
+    """ZS_FAIL_LOG=<file>: append each failure's report as it happens (a GPU run that is killed
+    later still leaves the reasons of the failures before it)."""
+    path = os.environ.get("ZS_FAIL_LOG")
+    if path and report.failed:
+        with open(path, "a") as f:
+            f.write(f"==== {report.nodeid} ({report.when})\n{report.longreprtext[-6000:]}\n")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
 

@@ -101,7 +101,7 @@ def _selfcheck_worker(rank, ws, port):
     import torch.distributed as dist
 
     from conftest import PKG, REPO  # noqa: F401
-    from _gloo_comm import GlooStagedComm
+    from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
     from _zero_run import init_pg
     import bench
 

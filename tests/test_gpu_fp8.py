@@ -108,11 +108,11 @@ def test_zero3_fp8_gather_ws1(gpu, dtype):
 
 def _mr(rank, ws, port, reshard=True):
     from conftest import PKG, REPO  # noqa: F401
-    from _gloo_comm import GlooStagedComm
+    from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
 
     torch.cuda.set_device(0)
     init_pg(rank, ws, port)
-    _check_materialize(rank, ws, torch.bfloat16, comm=GlooStagedComm(), reshard=reshard)
+    _check_materialize(rank, ws, torch.bfloat16, comm=test_comm(), reshard=reshard)
     dist.barrier()
     dist.destroy_process_group()
 

@@ -23,7 +23,7 @@ pytestmark = pytest.mark.gpu
 def _worker(rank, ws, port, layout, name, buckets, window):
     import sys
     from conftest import PKG, REPO  # noqa: F401  (sets sys.path in the child)
-    from _gloo_comm import GlooStagedComm
+    from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
     from zero_amd import zero2
 
     torch.cuda.set_device(0)
@@ -31,7 +31,7 @@ def _worker(rank, ws, port, layout, name, buckets, window):
     dev = torch.device("cuda:0")
     z = np.load(GOLDEN / name)
     params = [torch.nn.Parameter(torch.from_numpy(z[f"init_{i}"].copy()).to(dev)) for i in range(12)]
-    opt = zero2.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=GlooStagedComm(),
+    opt = zero2.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=test_comm(),
                                  layout=layout, buckets=buckets,
                                  bucket_mb=ws * window * 4 / (1 << 20))
     assert opt.local_param_indices == z[f"r{rank}_local"].tolist()  # the reference's bookkeeping

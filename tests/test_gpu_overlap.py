@@ -102,12 +102,12 @@ def test_overlap_double_backward_raises(gpu, pg1):
 def _mr_worker(rank, ws, port, variant, name, views, arena):
     import sys
     from conftest import PKG, REPO  # noqa: F401
-    from _gloo_comm import GlooStagedComm
+    from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
 
     torch.cuda.set_device(0)
     init_pg(rank, ws, port)
     z = np.load(GOLDEN / name)
-    opt = run_backward(z, variant, rank, ws, torch.device("cuda:0"), comm=GlooStagedComm(),
+    opt = run_backward(z, variant, rank, ws, torch.device("cuda:0"), comm=test_comm(),
                        views=views, bucket_mb=2e-3, arena=arena)
     k, launched = _overlap_stats(opt)
     assert k >= ws and launched > 0  # buckets reduced while backward was still running
@@ -123,7 +123,7 @@ def _frozen_worker(rank, ws, port, variant, overlap):
     bit-identical, and the frozen one does not hold back the overlapped reduces of later buckets."""
     import sys
     from conftest import PKG, REPO  # noqa: F401
-    from _gloo_comm import GlooStagedComm
+    from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
     from _zero_run import module_for, rel
     from oracle import zero_oracle as zo
 
@@ -145,7 +145,7 @@ def _frozen_worker(rank, ws, port, variant, overlap):
     want = zo.simulate(variant, ws, init, steps=steps, local_grads=grad_of)
     params = [torch.nn.Parameter(torch.from_numpy(a.copy()).to(dev), requires_grad=i != frozen)
               for i, a in enumerate(init)]
-    opt = module_for(variant).ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=GlooStagedComm(),
+    opt = module_for(variant).ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=test_comm(),
                                                overlap=overlap, overlap_bucket_mb=1e-3)
     for t in range(steps):
         opt.zero_grad()
@@ -193,7 +193,7 @@ def _ddp_grads(ws, shapes, step):
 def _ddp_worker(rank, ws, port, dtype_name):
     import sys
     from conftest import PKG, REPO  # noqa: F401
-    from _gloo_comm import GlooStagedComm
+    from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
     from zero_amd.ddp import SimpleDistributedDataParallelism
 
     torch.cuda.set_device(0)
@@ -204,7 +204,7 @@ def _ddp_worker(rank, ws, port, dtype_name):
     model = torch.nn.Sequential(torch.nn.Linear(40, 24), torch.nn.ReLU(), torch.nn.Linear(24, 8),
                                 torch.nn.Linear(8, 8)).to(dev).to(dt)
     ddp = SimpleDistributedDataParallelism(model, bucket_mb=1e-3,
-                                           comm=GlooStagedComm() if ws > 1 else None)
+                                           comm=test_comm() if ws > 1 else None)
     shapes = [tuple(p.shape) for p in model.parameters()]
     for step in range(3):
         allg = _ddp_grads(ws, shapes, step)

@@ -6,6 +6,8 @@ real HIP kernels, the exchange goes through tests/_gloo_comm.py (RCCL cannot put
 communicator on one device).  Tolerance: 1e-6 normwise relative (north star), every step.
 """
 
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -128,12 +130,12 @@ def test_rccl_table_collectives_ws1(gpu, pg1):
 def _mr_worker(rank, ws, port, variant, name, buckets="ragged", arena=None):
     import sys
     from conftest import PKG, REPO  # noqa: F401  (sets sys.path in the child)
-    from _gloo_comm import GlooStagedComm
+    from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
 
     torch.cuda.set_device(0)
     init_pg(rank, ws, port)
     z = np.load(GOLDEN / name)
-    run_injected(z, variant, rank, ws, torch.device("cuda:0"), comm=GlooStagedComm(), buckets=buckets,
+    run_injected(z, variant, rank, ws, torch.device("cuda:0"), comm=test_comm(), buckets=buckets,
                  arena=arena)
     dist.barrier()
     dist.destroy_process_group()
@@ -170,7 +172,7 @@ def test_multirank_padded_buckets(gpu, variant):
 def _edge_worker(rank, ws, port, variant, buckets, arena="flat"):
     import sys
     from conftest import PKG, REPO  # noqa: F401
-    from _gloo_comm import GlooStagedComm
+    from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
     from _zero_run import module_for
     from oracle import zero_oracle as zo
 
@@ -185,7 +187,7 @@ def _edge_worker(rank, ws, port, variant, buckets, arena="flat"):
                       * 1e-2).numpy() for t in range(steps) for r in range(ws) for i, s in enumerate(shapes)}
     want = zo.simulate(variant, ws, init, steps=steps, local_grads=lambda t, r, i: lg[(t, r, i)])
     params = [torch.nn.Parameter(torch.from_numpy(a.copy()).to(dev)) for a in init]
-    opt = module_for(variant).ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=GlooStagedComm(),
+    opt = module_for(variant).ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=test_comm(),
                                                bucket_mb=ws * 64 * 4 / (1 << 20), buckets=buckets,
                                                arena=arena)
     if rank == 3:
@@ -225,7 +227,7 @@ HP_CASES = {
 def _hp_worker(rank, ws, port, variant, case):
     import sys
     from conftest import PKG, REPO  # noqa: F401
-    from _gloo_comm import GlooStagedComm
+    from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
     from _zero_run import module_for
     from oracle import zero_oracle as zo
 
@@ -250,7 +252,7 @@ def _hp_worker(rank, ws, port, variant, case):
                        adam_kw=kw_of)
     params = [torch.nn.Parameter(torch.from_numpy(a.copy()).to(dev)) for a in init]
     pg = [dict(params=[p for p, gi in zip(params, group_of) if gi == k], **h) for k, h in enumerate(groups)]
-    opt = module_for(variant).ShardedOptimizer(cls(pg), comm=GlooStagedComm(),
+    opt = module_for(variant).ShardedOptimizer(cls(pg), comm=test_comm(),
                                                bucket_mb=ws * 128 * 4 / (1 << 20))
     for t in range(steps):
         opt.zero_grad()
@@ -316,7 +318,7 @@ def _carry_worker(rank, ws, port, clear):
     model.zero_grad() clears every grad, so nothing carries.  Both against the oracle."""
     import sys
     from conftest import PKG, REPO  # noqa: F401
-    from _gloo_comm import GlooStagedComm
+    from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
     from zero_amd import zero1
     from oracle import zero_oracle as zo
 
@@ -333,7 +335,7 @@ def _carry_worker(rank, ws, port, clear):
                        zero_grad=clear)
     model = torch.nn.ParameterList([torch.nn.Parameter(torch.from_numpy(a.copy()).to(dev)) for a in init])
     params = list(model)
-    opt = zero1.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=GlooStagedComm(),
+    opt = zero1.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=test_comm(),
                                  bucket_mb=ws * 64 * 4 / (1 << 20))
     for t in range(steps):
         if clear == "model":
@@ -362,7 +364,7 @@ def _bf16comm_worker(rank, ws, port, which):
     within 2e-2 of the reference's fp32 trajectory (the price of bf16 gradients; opt-in)."""
     import sys
     from conftest import PKG, REPO  # noqa: F401
-    from _gloo_comm import GlooStagedComm
+    from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
     from oracle import zero_oracle as zo
     from zero_amd import zero2, zero3
 
@@ -374,14 +376,18 @@ def _bf16comm_worker(rank, ws, port, which):
     want = zo.simulate(2, ws, init, local_grads=lambda t, r, i: z[f"r{r}_t{t}_lg{i}"], grad_comm="bf16")
     params = [torch.nn.Parameter(torch.from_numpy(a.copy()).to(dev)) for a in init]
     if which in ("zero2", "zero2_overlap"):
-        opt = zero2.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=GlooStagedComm(),
+        opt = zero2.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=test_comm(),
                                      bucket_mb=ws * 64 * 4 / (1 << 20), grad_comm="bf16",
                                      overlap=which == "zero2_overlap", overlap_bucket_mb=2e-3)
         assert opt.engine.R.dtype == torch.bfloat16
     else:
         opt = zero3.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), update=True,
-                                     comm=GlooStagedComm(), grad_comm="bf16")
+                                     comm=test_comm(), grad_comm="bf16")
         assert opt.grad_arena().dtype == torch.bfloat16
+    # the emulation rounds the fp32 sum to bf16 once; RCCL (tests/test_gpu_rccl.py) rounds each of
+    # its ws-1 ring partial sums: at ws > 2 a sum near zero can come out with the other sign and
+    # move Adam's update of that element by up to ~2 lr, hence the wider bound there
+    tol = 5e-3 if os.environ.get("ZS_TEST_COMM") == "rccl" and ws > 2 else 1e-4
     cs = lambda a: a if which != "zero3" else a[rank * -(-a.shape[0] // ws):(rank + 1) * -(-a.shape[0] // ws)]  # noqa: E731
     for t in range(int(z["steps"])):
         opt.zero_grad()
@@ -397,7 +403,8 @@ def _bf16comm_worker(rank, ws, port, which):
         opt.step()
         for i, p in enumerate(params):
             got = p.detach().cpu().numpy()
-            assert rel(got, cs(want["params"][t][rank][i])) <= 1e-4, (which, rank, t, i)
+            e = rel(got, cs(want["params"][t][rank][i]))
+            assert e <= tol, (which, rank, t, i, e)
             assert rel(got, cs(z[f"r{rank}_t{t}_p{i}"])) <= 2e-2, (which, rank, t, i)
     dist.barrier()
     dist.destroy_process_group()
@@ -417,7 +424,7 @@ def _comm_time_worker(rank, ws, port):
     shard all-reduce (zero3.py:125,158)."""
     import sys
     from conftest import PKG, REPO  # noqa: F401
-    from _gloo_comm import GlooStagedComm
+    from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
     from zero_amd import zero1, zero2, zero3
 
     torch.cuda.set_device(0)
@@ -444,13 +451,13 @@ def _comm_time_worker(rank, ws, port):
         torch.cuda.synchronize()
         return opt
 
-    o1 = run(lambda ps: zero1.ShardedOptimizer(torch.optim.Adam(ps), comm=GlooStagedComm()))
+    o1 = run(lambda ps: zero1.ShardedOptimizer(torch.optim.Adam(ps), comm=test_comm()))
     assert o1.communication_time == 0.0 and o1.step_time > 0
     for arena in ("flat", "buckets"):
-        o2 = run(lambda ps: zero2.ShardedOptimizer(torch.optim.Adam(ps), comm=GlooStagedComm(),
+        o2 = run(lambda ps: zero2.ShardedOptimizer(torch.optim.Adam(ps), comm=test_comm(),
                                                    arena=arena))
         assert 0.0 < o2.communication_time <= o2.step_time, (arena, o2.communication_time, o2.step_time)
-    o3 = run(lambda ps: zero3.ShardedOptimizer(torch.optim.Adam(ps), comm=GlooStagedComm()),
+    o3 = run(lambda ps: zero3.ShardedOptimizer(torch.optim.Adam(ps), comm=test_comm()),
              full_grads=True)
     assert 0.0 < o3.communication_time <= o3.step_time
     dist.barrier()

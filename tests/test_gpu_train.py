@@ -75,9 +75,9 @@ def _zero3_smollm3(rank, ws, port, dev, units=False, reshard=True):
     lr, wd = 1e-3, 0.01
     kw = {}
     if ws > 1:
-        from _gloo_comm import GlooStagedComm
+        from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
 
-        kw["comm"] = GlooStagedComm()
+        kw["comm"] = test_comm()
     opt = zero3.ShardedOptimizer(torch.optim.AdamW(params, lr=lr, weight_decay=wd), update=True,
                                  bucket_mb=0.05, **kw)
     zero3.register_zero3_hooks(model, opt.param_managers,

@@ -192,13 +192,13 @@ def _mr(rank, ws, port, fn, name):
     import faulthandler
     import sys
 
-    from _gloo_comm import GlooStagedComm
+    from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
 
     if rank:  # spawned ranks: a hang names its line (rank 0 is the pytest process itself)
         faulthandler.dump_traceback_later(120, exit=True, file=sys.stderr)
     torch.cuda.set_device(0)
     init_pg(rank, ws, port)
-    globals()[fn](rank, ws, name, torch.device("cuda:0"), comm=GlooStagedComm())
+    globals()[fn](rank, ws, name, torch.device("cuda:0"), comm=test_comm())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -228,7 +228,7 @@ def test_multirank_update_mode_hooks(gpu, ws, mode):
 def _mem_worker(rank, ws, port):
     """update mode frees each full gradient once its reduce-scatter is enqueued: peak gradient
     memory during backward is one bucket, not the model; the full parameters are released."""
-    from _gloo_comm import GlooStagedComm
+    from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
     from zero_amd import zero3
 
     torch.cuda.set_device(0)
@@ -241,7 +241,7 @@ def _mem_worker(rank, ws, port):
     torch.cuda.synchronize()
     before = torch.cuda.memory_allocated(dev)
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
-                                 comm=GlooStagedComm(), bucket_mb=D * D * 4 / (1 << 20))
+                                 comm=test_comm(), bucket_mb=D * D * 4 / (1 << 20))
     zero3.register_zero3_hooks(model, opt.param_managers)
     torch.cuda.synchronize()
     after = torch.cuda.memory_allocated(dev)
