@@ -1064,6 +1064,8 @@ def main():
         os.environ["NCCL_HOSTID"] = f"zs-share-gpu-rank{rank}"
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         os.environ.setdefault("NCCL_IB_DISABLE", "1")
+        # ranks probing placements on one device at once would race for its memory
+        os.environ.setdefault("ZERO_AMD_PROBE_TRIES", "1")
         _REHEARSAL[0] = ("share-gpu: every rank on ONE device, RCCL between them over its socket "
                          "transport (checks are real, timings are not xGMI's)")
     torch.cuda.set_device(local)
