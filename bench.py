@@ -694,10 +694,10 @@ def zero12_exchange_check(opt, step, params, shapes, dev, world, rank, red_dev, 
             r = float((p - want).abs().max() / want.abs().max().clamp_min(1e-30))
             if r > 1e-6:
                 bad.append(("adam update (rel)", i, r))
+    del cap, before, exact, absum
     sums = []
     for p in params:
-        b = _bits(p.detach()).long()
-        sums += [int(b.sum()), int((b * torch.arange(1, b.numel() + 1, device=dev) % 65521).sum())]
+        sums += _bit_checksums(p.detach(), dev)
     t = torch.tensor(sums, dtype=torch.int64, device=red_dev)
     lo, hi = t.clone(), t.clone()
     dist.all_reduce(lo, op=dist.ReduceOp.MIN)
@@ -722,6 +722,20 @@ def zero12_exchange_check(opt, step, params, shapes, dev, world, rank, red_dev, 
             f"{fail[1]} — excluded from the calibration")
         res["failure"] = f"rank {rank}: {fail[0]}: {fail[1]}"[:400]
     return res
+
+
+def _bit_checksums(t, dev, chunk: int = 1 << 24):
+    """Two checksums of a tensor's bits (plain sum, position-weighted sum mod 65521), taken over
+    16M-element chunks so the int64 temporaries stay small beside a large arena."""
+    import torch
+
+    b = _bits(t).reshape(-1)
+    s0 = s1 = 0
+    for o in range(0, b.numel(), chunk):
+        c = b[o:o + chunk].long()
+        s0 += int(c.sum())
+        s1 += int((c * torch.arange(o + 1, o + c.numel() + 1, device=dev) % 65521).sum())
+    return [s0, s1]
 
 
 def bench_zero3(args, world, rank, dev, use_nccl):
