@@ -738,6 +738,59 @@ def _bit_checksums(t, dev, chunk: int = 1 << 24):
     return [s0, s1]
 
 
+def zero3_mlp_check(opt, model, ref, x, y, step, world, rank, red_dev):
+    """N>1 check of the hooked ZeRO-3 iteration before anything is timed: ONE real iteration
+    (hooked all-gathers, backward reduce-scatters, update-mode step) must leave every rank's chunk
+    equal to the same iteration done unsharded in plain PyTorch (the initial full weights, one
+    forward / MSE / backward, torch.optim.Adam) — within 1e-5 relative (fp32; bf16: 2 ulp, i.e.
+    2^-7): every rank trains on the same batch (zero3.py:186), so the mean of the reduced
+    gradients is this rank's own gradient.  A failure ends the run (exit 4)."""
+    import torch
+    import torch.distributed as dist
+
+    step()
+    torch.cuda.synchronize()
+    lin = [m for m in model if isinstance(m, torch.nn.Linear)]
+    rp = [torch.nn.Parameter(t) for t in ref]
+    h = x
+    for k in range(len(lin)):
+        h = torch.nn.functional.linear(h, rp[2 * k], rp[2 * k + 1])
+        if k < len(lin) - 1:
+            h = torch.relu(h)
+    torch.nn.functional.mse_loss(h, y).backward()
+    if ref[0].dtype != torch.float32:  # bf16 params: the update runs on fp32 masters (as ours does)
+        mp = [torch.nn.Parameter(q.detach().float()) for q in rp]
+        for a, q in zip(mp, rp):
+            a.grad = q.grad.float()
+        torch.optim.Adam(mp, lr=1e-3).step()
+        for a, q in zip(mp, rp):
+            q.data.copy_(a.detach())
+    else:
+        torch.optim.Adam(rp, lr=1e-3).step()
+    torch.cuda.synchronize()
+    fp32 = ref[0].dtype == torch.float32
+    tol = 1e-5 if fp32 else 2.0 ** -7
+    worst, bad = 0.0, []
+    for i, p in enumerate(model.parameters()):
+        m = opt.param_managers[p]
+        want = rp[i].detach()[m.r0:m.r1].float()
+        got = p.detach().reshape(want.shape).float()
+        e = float((got - want).abs().max() / want.abs().max().clamp_min(1e-30)) if want.numel() else 0.0
+        worst = max(worst, e)
+        if e > tol:
+            bad.append((i, e))
+    ok = torch.tensor([0.0 if bad else 1.0], device=red_dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    res = {"what": "one hooked ZeRO-3 iteration vs the same iteration unsharded in plain PyTorch "
+                   "(torch.optim.Adam), this rank's chunks", "max_rel_err": worst, "tol": tol,
+           "all_ranks_ok": bool(ok.item() == 1.0)}
+    if bad:
+        _fail_check("ZeRO-3 iteration", rank, f"chunks of params {bad[:8]} off by more than {tol}")
+    if not res["all_ranks_ok"]:
+        _fail_check("ZeRO-3 iteration", rank, "another rank failed")
+    return res
+
+
 def bench_zero3(args, world, rank, dev, use_nccl):
     """ZeRO-3 (BASELINE.json configs[2]): one step = one training iteration of the reference
     harness loop (zero3.py:171-258: zero_grad → forward → MSE → backward → step) on the
@@ -765,6 +818,7 @@ def bench_zero3(args, world, rank, dev, use_nccl):
     y = torch.randn(batch, D, device=dev, generator=g).to(dt)
     comm, chk = _zero3_comm(args, world, rank, dev)
     kw = {} if comm is None else {"comm": comm}
+    ref = [p.detach().clone() for p in model.parameters()] if world > 1 and not args.gather else None
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
                                  sync=False, gather_dtype=args.gather, bucket_mb=args.bucket_mb or 128.0, **kw)
     zero3.register_zero3_hooks(model, opt.param_managers)
@@ -775,10 +829,14 @@ def bench_zero3(args, world, rank, dev, use_nccl):
         loss.backward()
         opt.step()
 
-    _phase("warmup")
-    el = _zero3_timed(args, opt, step, dev, world)
     red_dev = dev if use_nccl else "cpu"
     extra = {"rccl_selfcheck": chk} if chk is not None else {}
+    if ref is not None:
+        _phase("exchange check (ZeRO-3 training iteration)")
+        extra["exchange_check"] = zero3_mlp_check(opt, model, ref, x, y, step, world, rank, red_dev)
+        del ref
+    _phase("warmup")
+    el = _zero3_timed(args, opt, step, dev, world)
     _zero3_report(args, opt, world, rank, red_dev, el, total,
                   f"{args.config} ZeRO-3 training iteration of the reference MLP 6xLinear({D},{D})+ReLU "
                   f"(hooked all-gathers, backward reduce-scatters, update-mode step), batch {batch}",
