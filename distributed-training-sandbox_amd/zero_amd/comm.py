@@ -31,11 +31,23 @@ def zs_dtype(dt: torch.dtype) -> int:
         raise TypeError(f"zero_amd: unsupported dtype {dt} (float32, bfloat16, uint8)") from None
 
 
+_COMM_STREAMS = {}
+
+
 def comm_stream(device) -> torch.cuda.Stream:
-    """Side stream for collectives, at the highest priority: the compute stream's streaming kernels
-    launch 128 workgroups per CU, and an RCCL kernel queued behind them would wait for CU slots
-    while its peers spin; a high-priority queue gets its workgroups dispatched first."""
-    return torch.cuda.Stream(device=device, priority=-1)  # < 0: torch's high-priority pool
+    """THE side stream for collectives on ``device`` (one per device and process), at the highest
+    priority: the compute stream's streaming kernels launch 128 workgroups per CU, and an RCCL
+    kernel queued behind them would wait for CU slots while its peers spin; a high-priority queue
+    gets its workgroups dispatched first.  One stream for every engine of the process — not a new
+    one from torch's rotating pool per engine — so collectives of different communicators are
+    never in flight at once (the ordering NCCL requires of several communicators), and a process
+    that builds engine after engine keeps the same stream-to-hardware-queue mapping."""
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    s = _COMM_STREAMS.get(idx)
+    if s is None:
+        s = _COMM_STREAMS[idx] = torch.cuda.Stream(device=idx, priority=-1)  # < 0: high priority
+    return s
 
 
 def rccl_version() -> int:

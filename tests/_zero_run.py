@@ -178,6 +178,31 @@ def spawn_all_ranks(fn, ws: int, args=(), deadline_s: float = 150.0):
                 p.kill()
 
 
+def _run_seq(rank, calls):
+    for fn, args in calls:
+        fn(rank, *args)
+
+
+def spawn_batch(ws: int, cases, all_spawned: bool = False, deadline_s: float = 150.0):
+    """Several multi-rank cases in ONE set of ws processes, run one after another: case
+    ``(fn, extra)`` runs ``fn(rank, ws, port, *extra)`` on every rank with a port of its own (each
+    worker makes and destroys its own process group).  Spawning the ranks and importing torch in
+    them cost more than most cases' work, so a test batches the cases of one world size."""
+    from conftest import free_port
+
+    calls, used = [], set()
+    for fn, extra in cases:
+        port = free_port()
+        while port in used:
+            port = free_port()
+        used.add(port)
+        calls.append((fn, (ws, port) + tuple(extra)))
+    if all_spawned:
+        spawn_all_ranks(_run_seq, ws, (calls,), deadline_s=deadline_s)
+    else:
+        spawn_ranks(_run_seq, ws, (calls,))
+
+
 def spawn_ranks(fn, ws: int, args=()):
     """Run ``fn(rank, *args)`` for every rank of a ws-rank job: rank 0 in THIS process, ranks
     1..ws-1 spawned.  So a ws-rank GPU test puts exactly ws processes on the box's GPU (the

@@ -13,7 +13,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import free_port
-from _zero_run import spawn_ranks, init_pg
+from _zero_run import spawn_batch, spawn_ranks, init_pg
 
 pytestmark = pytest.mark.gpu
 
@@ -117,6 +117,6 @@ def _mr(rank, ws, port, reshard=True):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws,reshard", [(2, True), (3, True), (2, False)])
-def test_zero3_fp8_gather_multirank(gpu, ws, reshard):
-    spawn_ranks(_mr, ws, (ws, _port(), reshard))
+@pytest.mark.parametrize("ws,reshards", [(2, (True, False)), (3, (True,))])
+def test_zero3_fp8_gather_multirank(gpu, ws, reshards):
+    spawn_batch(ws, [(_mr, (r,)) for r in reshards])

@@ -15,7 +15,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import GOLDEN, free_port
-from _zero_run import spawn_ranks, init_pg, rel
+from _zero_run import spawn_batch, spawn_ranks, init_pg, rel
 
 pytestmark = pytest.mark.gpu
 
@@ -65,14 +65,14 @@ CASES = [("chunk", 2, "ref", "ragged"), ("chunk", 3, "distinct", "ragged"),
          ("flat", 3, "ref", "ragged"), ("flat", 4, "distinct", "padded")]
 
 
-@pytest.mark.parametrize("layout,ws,mode,buckets", CASES)
-def test_layout_matches_reference_zero2(gpu, layout, ws, mode, buckets):
-    name = f"traj_z2_ws{ws}_d16_{mode}.npz"
-    if not (GOLDEN / name).exists():
-        pytest.skip(f"no fixture {name}")
-    spawn_ranks(_worker, ws, (ws, free_port(), layout, name, buckets, 64))
-
-
-def test_chunk_layout_small_windows_many_buckets(gpu):
-    """Windows smaller than most chunks: every parameter's chunk is split across buckets."""
-    spawn_ranks(_worker, 4, (4, free_port(), "chunk", "traj_z2_ws4_d64_distinct.npz", "ragged", 64))
+@pytest.mark.parametrize("ws", [2, 3, 4, 8])
+def test_layout_matches_reference_zero2(gpu, ws):
+    """Every layout / bucket-mode case of this ws (ws = 4 adds windows smaller than most chunks:
+    every parameter's chunk split across buckets), one after another in one set of processes."""
+    cases = [(_worker, (layout, f"traj_z2_ws{w}_d16_{mode}.npz", buckets, 64))
+             for layout, w, mode, buckets in CASES if w == ws]
+    if ws == 4:
+        cases.append((_worker, ("chunk", "traj_z2_ws4_d64_distinct.npz", "ragged", 64)))
+    for _, (_, name, _, _) in cases:
+        assert (GOLDEN / name).exists(), name
+    spawn_batch(ws, cases)

@@ -14,7 +14,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import GOLDEN, free_port
-from _zero_run import spawn_ranks, init_pg, run_backward
+from _zero_run import spawn_batch, spawn_ranks, init_pg, run_backward
 
 pytestmark = pytest.mark.gpu
 
@@ -162,25 +162,24 @@ def _frozen_worker(rank, ws, port, variant, overlap):
     sys.stdout.flush()
 
 
-@pytest.mark.parametrize("overlap", [True, False])
-@pytest.mark.parametrize("variant", [1, 2])
-def test_frozen_and_unused_params(gpu, variant, overlap):
-    spawn_ranks(_frozen_worker, 2, (2, _port(), variant, overlap))
+def test_frozen_and_unused_params(gpu):
+    spawn_batch(2, [(_frozen_worker, (v, o)) for v in (1, 2) for o in (True, False)])
 
 
-@pytest.mark.parametrize("arena", ["flat", "buckets"])
-@pytest.mark.parametrize("variant", [1, 2])
-@pytest.mark.parametrize("ws,views", [(2, True), (3, True), (3, False), (4, True)])
-def test_multirank_overlap_backward(gpu, variant, ws, views, arena):
-    name = f"traj_z{variant}_ws{ws}_d16_distinct.npz"
-    spawn_ranks(_mr_worker, ws, (ws, _port(), variant, name, views, arena))
+OV_CASES = [(2, True), (3, True), (3, False), (4, True)]
 
 
-@pytest.mark.parametrize("variant", [1, 2])
-def test_multirank_overlap_backward_ws8_flat(gpu, variant):
+@pytest.mark.parametrize("ws", [2, 3, 4])
+def test_multirank_overlap_backward(gpu, ws):
+    """Backward-overlapped reduces against the reference's trajectories: ZeRO-1 and 2, flat and
+    bucket arena, grads as bucket views or handed over (every combination of this ws)."""
+    spawn_batch(ws, [(_mr_worker, (v, f"traj_z{v}_ws{ws}_d16_distinct.npz", views, arena))
+                     for w, views in OV_CASES if w == ws for v in (1, 2) for arena in ("flat", "buckets")])
+
+
+def test_multirank_overlap_backward_ws8_flat(gpu):
     """ws=8 (12 parameters: ranks 4-7 own one each) through a real backward on the flat arena."""
-    name = f"traj_z{variant}_ws8_d16_distinct.npz"
-    spawn_ranks(_mr_worker, 8, (8, _port(), variant, name, True, "flat"))
+    spawn_batch(8, [(_mr_worker, (v, f"traj_z{v}_ws8_d16_distinct.npz", True, "flat")) for v in (1, 2)])
 
 
 # ---------------------------------------------------------------------------------------------
@@ -241,9 +240,8 @@ def _ddp_worker(rank, ws, port, dtype_name):
 
 
 @pytest.mark.parametrize("ws", [1, 2, 3])
-@pytest.mark.parametrize("dtype_name", ["float32", "bfloat16"])
-def test_ddp_sync_gradients(gpu, ws, dtype_name):
-    spawn_ranks(_ddp_worker, ws, (ws, _port(), dtype_name))
+def test_ddp_sync_gradients(gpu, ws):
+    spawn_batch(ws, [(_ddp_worker, (d,)) for d in ("float32", "bfloat16")])
 
 
 @pytest.mark.parametrize("n", [1, 7, 1000, 4099, 1 << 20])

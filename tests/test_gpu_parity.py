@@ -15,7 +15,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import GOLDEN, free_port
-from _zero_run import spawn_ranks, init_pg, rel, run_injected, set_grad
+from _zero_run import spawn_batch, spawn_ranks, init_pg, rel, run_injected, set_grad
 
 pytestmark = pytest.mark.gpu
 
@@ -147,26 +147,28 @@ MR_CASES = [(v, f"traj_z{v}_ws{ws}_d16_{m}.npz") for v in (1, 2) for ws in (2, 3
                                              (2, "traj_z2_ws4_d64_distinct.npz")]
 
 
-@pytest.mark.parametrize("variant,name", MR_CASES)
-def test_multirank_injected(gpu, variant, name):
+def _ws_of(name):
+    return int(name.split("_ws")[1].split("_")[0])
+
+
+@pytest.mark.parametrize("ws", [2, 3, 4, 8])
+def test_multirank_injected(gpu, ws):
     """The default ws > 1 exchange (flat parameter arena: grouped reduce / broadcast rounds, no
-    pack / unpack) against the reference's trajectories, ws 2-8 incl. ZeRO-1's carry."""
-    ws = int(name.split("_ws")[1].split("_")[0])
-    spawn_ranks(_mr_worker, ws, (ws, _port(), variant, name))
+    pack / unpack) against the reference's trajectories, ws 2-8 incl. ZeRO-1's carry (every
+    fixture of this ws, ref and distinct data, ZeRO-1 and ZeRO-2, in one set of processes)."""
+    spawn_batch(ws, [(_mr_worker, (v, name)) for v, name in MR_CASES if _ws_of(name) == ws])
 
 
-@pytest.mark.parametrize("variant,ws", [(1, 3), (2, 4), (1, 8), (2, 8)])
-def test_multirank_injected_bucket_arena(gpu, variant, ws):
-    """The rank-major bucket arena (pack / reduce-scatter / all-gather / unpack, ablation)."""
-    name = f"traj_z{variant}_ws{ws}_d16_distinct.npz"
-    spawn_ranks(_mr_worker, ws, (ws, _port(), variant, name, "ragged", "buckets"))
+BUCKET_CASES = [(1, 3, "ragged"), (1, 3, "padded"), (2, 3, "padded"), (2, 4, "ragged"),
+                (1, 8, "ragged"), (2, 8, "ragged")]
 
 
-@pytest.mark.parametrize("variant", [1, 2])
-def test_multirank_padded_buckets(gpu, variant):
-    """The zero-padded bucket schedule (ablation) gives the same trajectory."""
-    spawn_ranks(_mr_worker, 3, (3, _port(), variant, f"traj_z{variant}_ws3_d16_distinct.npz", "padded",
-                                "buckets"))
+@pytest.mark.parametrize("ws", [3, 4, 8])
+def test_multirank_injected_bucket_arena(gpu, ws):
+    """The rank-major bucket arena (pack / reduce-scatter / all-gather / unpack, ablation), with
+    the ragged tail or the zero-padded bucket schedule."""
+    spawn_batch(ws, [(_mr_worker, (v, f"traj_z{v}_ws{ws}_d16_distinct.npz", b, "buckets"))
+                     for v, w, b in BUCKET_CASES if w == ws])
 
 
 def _edge_worker(rank, ws, port, variant, buckets, arena="flat"):
@@ -208,13 +210,12 @@ def _edge_worker(rank, ws, port, variant, buckets, arena="flat"):
     sys.stdout.flush()
 
 
-@pytest.mark.parametrize("variant", [1, 2])
-@pytest.mark.parametrize("buckets,arena", [("ragged", "flat"), ("ragged", "buckets"),
-                                           ("padded", "buckets")])
-def test_multirank_fewer_params_than_ranks(gpu, variant, buckets, arena):
+def test_multirank_fewer_params_than_ranks(gpu):
     """Edge cases of the reference's ownership rule on the device path: n < ws (empty ranks) and a
-    zero-element parameter, against the oracle's restatement of the reference."""
-    spawn_ranks(_edge_worker, 4, (4, _port(), variant, buckets, arena))
+    zero-element parameter, against the oracle's restatement of the reference (ZeRO-1 and 2; flat
+    arena, ragged and padded bucket arena)."""
+    spawn_batch(4, [(_edge_worker, (v, b, a)) for v in (1, 2)
+                    for b, a in (("ragged", "flat"), ("ragged", "buckets"), ("padded", "buckets"))])
 
 
 HP_CASES = {
@@ -272,12 +273,10 @@ def _hp_worker(rank, ws, port, variant, case):
     sys.stdout.flush()
 
 
-@pytest.mark.parametrize("variant", [1, 2])
-@pytest.mark.parametrize("case", sorted(HP_CASES))
-def test_multirank_hyperparameters(gpu, variant, case):
-    """AdamW / L2 weight decay / amsgrad / maximize and per-group lr through the bucketed ws=3
-    path (ragged buckets included) against the oracle's restatement of the reference."""
-    spawn_ranks(_hp_worker, 3, (3, _port(), variant, case))
+def test_multirank_hyperparameters(gpu):
+    """AdamW / L2 weight decay / amsgrad / maximize and per-group lr through the ws=3 exchange
+    against the oracle's restatement of the reference (ZeRO-1 and ZeRO-2, every case)."""
+    spawn_batch(3, [(_hp_worker, (v, c)) for v in (1, 2) for c in sorted(HP_CASES)])
 
 
 def test_profiler_ranges_match_reference_names(gpu, pg1):
@@ -352,9 +351,8 @@ def _carry_worker(rank, ws, port, clear):
     sys.stdout.flush()
 
 
-@pytest.mark.parametrize("clear", ["optimizer", "model"])
-def test_zero1_carry_follows_zero_grad(gpu, clear):
-    spawn_ranks(_carry_worker, 3, (3, _port(), clear))
+def test_zero1_carry_follows_zero_grad(gpu):
+    spawn_batch(3, [(_carry_worker, (c,)) for c in ("optimizer", "model")])
 
 
 def _bf16comm_worker(rank, ws, port, which):
@@ -411,10 +409,9 @@ def _bf16comm_worker(rank, ws, port, which):
     sys.stdout.flush()
 
 
-@pytest.mark.parametrize("which,ws", [("zero2", 3), ("zero2", 4), ("zero2_overlap", 3), ("zero3", 3),
-                                     ("zero3", 4)])
-def test_bf16_gradient_exchange_for_fp32_params(gpu, which, ws):
-    spawn_ranks(_bf16comm_worker, ws, (ws, _port(), which))
+@pytest.mark.parametrize("ws,whiches", [(3, ("zero2", "zero2_overlap", "zero3")), (4, ("zero2", "zero3"))])
+def test_bf16_gradient_exchange_for_fp32_params(gpu, ws, whiches):
+    spawn_batch(ws, [(_bf16comm_worker, (w,)) for w in whiches])
 
 
 def _comm_time_worker(rank, ws, port):

@@ -25,7 +25,7 @@ import sys
 import pytest
 
 from conftest import REPO, free_port
-from _zero_run import spawn_all_ranks, spawn_ranks
+from _zero_run import spawn_batch
 
 pytestmark = pytest.mark.gpu
 
@@ -39,117 +39,76 @@ def rccl_env(monkeypatch):
     yield
 
 
-def _run(fn, ws, *args):
-    """Every rank spawned (a failing rank takes the others down) up to ws = 4; at ws = 8 rank 0
-    runs here, as in the gloo-staged tests (9 processes on the device stalled those)."""
-    if ws <= 4:
-        spawn_all_ranks(fn, ws, (ws, free_port()) + args)
-    else:
-        spawn_ranks(fn, ws, (ws, free_port()) + args)
+def _batch(ws, cases):
+    """The cases of one ws in one set of processes: every rank spawned (a failing rank takes the
+    others down) up to ws = 4; at ws = 8 rank 0 runs here, as in the gloo-staged tests (9
+    processes on the device stalled those)."""
+    spawn_batch(ws, cases, all_spawned=ws <= 4)
 
 
-# --- ZeRO-1/2 against the reference's trajectories ------------------------------------------
-@pytest.mark.parametrize("variant,ws,mode,arena", [
-    (1, 2, "distinct", None), (2, 2, "distinct", None), (1, 4, "ref", None), (2, 4, "distinct", None),
-    (1, 3, "distinct", "buckets"), (2, 4, "distinct", "buckets"), (2, 8, "distinct", None)])
-def test_rccl_injected_trajectories(gpu, rccl_env, variant, ws, mode, arena):
-    """Flat arena (grouped reduce / broadcast rounds) and bucket arena (in-place RS / AG)."""
-    from test_gpu_parity import _mr_worker
+def _zero12_cases(ws):
+    from test_gpu_layouts import _worker as layout_worker
+    from test_gpu_overlap import _ddp_worker, _frozen_worker, _mr_worker as ov_worker
+    from test_gpu_parity import (_bf16comm_worker, _carry_worker, _comm_time_worker, _edge_worker,
+                                 _hp_worker, _mr_worker)
 
-    _run(_mr_worker, ws, variant, f"traj_z{variant}_ws{ws}_d16_{mode}.npz", "ragged", arena)
-
-
-@pytest.mark.parametrize("variant", [1, 2])
-def test_rccl_fewer_params_than_ranks(gpu, rccl_env, variant):
-    from test_gpu_parity import _edge_worker
-
-    _run(_edge_worker, 4, variant, "ragged", "flat")
-
-
-def test_rccl_hyperparameters(gpu, rccl_env):
-    from test_gpu_parity import _hp_worker
-
-    _run(_hp_worker, 3, 2, "adamw_amsgrad_2groups")
-
-
-def test_rccl_zero1_carry(gpu, rccl_env):
-    from test_gpu_parity import _carry_worker
-
-    _run(_carry_worker, 3, "optimizer")
+    inj = {2: [(1, "distinct", None), (2, "distinct", None)],
+           3: [(1, "distinct", "buckets")],
+           4: [(1, "ref", None), (2, "distinct", None), (2, "distinct", "buckets")],
+           8: [(2, "distinct", None)]}[ws]
+    cases = [(_mr_worker, (v, f"traj_z{v}_ws{ws}_d16_{m}.npz", "ragged", a)) for v, m, a in inj]
+    if ws == 2:
+        cases += [(_bf16comm_worker, ("zero2",)), (_comm_time_worker, ()),
+                  (ov_worker, (1, "traj_z1_ws2_d16_distinct.npz", True, "flat")),
+                  (_frozen_worker, (2, True)), (_ddp_worker, ("float32",)), (_ddp_worker, ("bfloat16",))]
+    if ws == 3:
+        cases += [(_hp_worker, (2, "adamw_amsgrad_2groups")), (_carry_worker, ("optimizer",)),
+                  (_bf16comm_worker, ("zero2_overlap",)),
+                  (ov_worker, (2, "traj_z2_ws3_d16_distinct.npz", True, "buckets")),
+                  (_ddp_worker, ("float32",))]
+    if ws == 4:
+        cases += [(_edge_worker, (1, "ragged", "flat")), (_edge_worker, (2, "ragged", "flat")),
+                  (_bf16comm_worker, ("zero2",)),
+                  (ov_worker, (2, "traj_z2_ws4_d16_distinct.npz", True, "flat")),
+                  (layout_worker, ("chunk", "traj_z2_ws4_d64_distinct.npz", "ragged", 64))]
+    return cases
 
 
-@pytest.mark.parametrize("which,ws", [("zero2", 2), ("zero2", 4), ("zero2_overlap", 3), ("zero3", 4)])
-def test_rccl_bf16_gradient_exchange(gpu, rccl_env, which, ws):
-    """bf16 sums inside RCCL (ring order, per-hop rounding) vs the oracle's emulation (1e-4)."""
+@pytest.mark.parametrize("ws", [2, 3, 4, 8])
+def test_rccl_zero12(gpu, rccl_env, ws):
+    """ZeRO-1/2 through real RCCL: the reference's trajectories on the flat arena (grouped reduce /
+    broadcast rounds) and the bucket arena (in-place RS / AG); ws 2-4 add the overlapped backward,
+    bf16 gradient exchange, hyper-parameters, the ZeRO-1 carry, empty ranks, the timing counters,
+    DDP and the chunk layout."""
+    _batch(ws, _zero12_cases(ws))
+
+
+def _zero3_cases(ws):
+    from test_gpu_fp8 import _mr as fp8_worker
     from test_gpu_parity import _bf16comm_worker
-
-    _run(_bf16comm_worker, ws, which)
-
-
-def test_rccl_timing_counters(gpu, rccl_env):
-    from test_gpu_parity import _comm_time_worker
-
-    _run(_comm_time_worker, 2)
-
-
-# --- backward-overlapped reduces, DDP ------------------------------------------------------
-@pytest.mark.parametrize("variant,ws,arena", [(1, 2, "flat"), (2, 4, "flat"), (2, 3, "buckets")])
-def test_rccl_overlap_backward(gpu, rccl_env, variant, ws, arena):
-    from test_gpu_overlap import _mr_worker
-
-    _run(_mr_worker, ws, variant, f"traj_z{variant}_ws{ws}_d16_distinct.npz", True, arena)
-
-
-def test_rccl_frozen_and_unused(gpu, rccl_env):
-    from test_gpu_overlap import _frozen_worker
-
-    _run(_frozen_worker, 2, 2, True)
-
-
-@pytest.mark.parametrize("ws,dtype_name", [(2, "float32"), (2, "bfloat16"), (3, "float32")])
-def test_rccl_ddp_sync_gradients(gpu, rccl_env, ws, dtype_name):
-    from test_gpu_overlap import _ddp_worker
-
-    _run(_ddp_worker, ws, dtype_name)
-
-
-# --- ZeRO-3 -------------------------------------------------------------------------------
-@pytest.mark.parametrize("fn,ws,name", [
-    ("_ref_mode", 2, "traj_z3_ws2_d16_distinct.npz"), ("_ref_mode", 4, "traj_z3_ws4_d16_distinct.npz"),
-    ("_ref_injected", 4, "traj_z3_ws4_d16_ref.npz"),
-    ("_update_injected", 3, "traj_z2_ws3_d16_distinct.npz"),
-    ("_update_hooks", 2, "traj_z2_ws2_d16_distinct.npz"), ("_update_hooks", 4, "traj_z2_ws4_d16_distinct.npz")])
-def test_rccl_zero3(gpu, rccl_env, fn, ws, name):
-    from test_gpu_zero3 import _mr
-
-    _run(_mr, ws, fn, name)
-
-
-def test_rccl_zero3_gradient_memory(gpu, rccl_env):
-    from test_gpu_zero3 import _mem_worker
-
-    _run(_mem_worker, 4)
-
-
-@pytest.mark.parametrize("reshard", [True, False])
-def test_rccl_zero3_fp8_gather(gpu, rccl_env, reshard):
-    from test_gpu_fp8 import _mr
-
-    _run(_mr, 2, reshard)
-
-
-@pytest.mark.parametrize("units,reshard", [(False, True), (True, False)])
-def test_rccl_smollm3_zero3_bit_exact(gpu, rccl_env, units, reshard):
-    """SmolLM3 ZeRO-3 AdamW at ws=2, bit-exact against the C oracle every step."""
     from test_gpu_train import _mr_zero3
+    from test_gpu_zero3 import _mem_worker, _mr
 
-    _run(_mr_zero3, 2, units, reshard)
+    cases = {2: [("_ref_mode", "traj_z3_ws2_d16_distinct.npz"),
+                 ("_update_hooks", "traj_z2_ws2_d16_distinct.npz")],
+             3: [("_update_injected", "traj_z2_ws3_d16_distinct.npz")],
+             4: [("_ref_mode", "traj_z3_ws4_d16_distinct.npz"), ("_ref_injected", "traj_z3_ws4_d16_ref.npz"),
+                 ("_update_hooks", "traj_z2_ws4_d16_distinct.npz")]}[ws]
+    cases = [(_mr, c) for c in cases]
+    if ws == 2:  # SmolLM3 ZeRO-3 AdamW bit-exact against the C oracle; fp8 gathers
+        cases += [(_mr_zero3, (False, True)), (_mr_zero3, (True, False)),
+                  (fp8_worker, (True,)), (fp8_worker, (False,))]
+    if ws == 4:
+        cases += [(_bf16comm_worker, ("zero3",)), (_mem_worker, ())]
+    return cases
 
 
-def test_rccl_chunk_layout(gpu, rccl_env):
-    from test_gpu_layouts import _worker
-
-    _run(_worker, 4, "chunk", "traj_z2_ws4_d64_distinct.npz", "ragged", 64)
+@pytest.mark.parametrize("ws", [2, 3, 4])
+def test_rccl_zero3(gpu, rccl_env, ws):
+    """ZeRO-3 through real RCCL: table gathers from the module hooks (reference and update mode),
+    backward reduce-scatters, uneven chunks (ws = 3), bf16 gradient exchange, sharded gradient
+    memory, fp8 gathers, SmolLM3 ZeRO-3 AdamW bit for bit against the C oracle."""
+    _batch(ws, _zero3_cases(ws))
 
 
 # --- bench.py at N = 2 on the shared GPU ------------------------------------------------

@@ -134,12 +134,10 @@ def _mr_zero3(rank, ws, port, units, reshard=True):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("units,reshard", [(False, True), (True, True), (True, False)])
-def test_smollm3_zero3_two_ranks_bit_exact(gpu, units, reshard):
-    """units=True: one gather group per decoder layer (FSDP2's per-block fully_shard);
-    reshard=False: parameters stay gathered from forward through backward (FSDP2's
+def test_smollm3_zero3_two_ranks_bit_exact(gpu):
+    """Per-module groups; units=True: one gather group per decoder layer (FSDP2's per-block
+    fully_shard); reshard=False: parameters stay gathered from forward through backward (FSDP2's
     reshard_after_forward=False, the reference's "ZeRO-2" run, fsdp/train_fsdp.py:84-86)."""
-    from conftest import free_port
-    from _zero_run import spawn_ranks
+    from _zero_run import spawn_batch
 
-    spawn_ranks(_mr_zero3, 2, (2, free_port(), units, reshard))
+    spawn_batch(2, [(_mr_zero3, (u, r)) for u, r in ((False, True), (True, True), (True, False))])

@@ -13,7 +13,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import GOLDEN, free_port
-from _zero_run import spawn_ranks, init_pg, rel
+from _zero_run import spawn_batch, spawn_ranks, init_pg, rel
 
 pytestmark = pytest.mark.gpu
 
@@ -203,26 +203,20 @@ def _mr(rank, ws, port, fn, name):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws", [2, 4, 8])
-def test_multirank_reference_mode_hooks(gpu, ws):
-    spawn_ranks(_mr, ws, (ws, _port(), "_ref_mode", f"traj_z3_ws{ws}_d16_distinct.npz"))
-
-
-@pytest.mark.parametrize("ws", [2, 4, 8])
-def test_multirank_reference_mode_injected(gpu, ws):
-    spawn_ranks(_mr, ws, (ws, _port(), "_ref_injected", f"traj_z3_ws{ws}_d16_ref.npz"))
+Z3_CASES = [("_ref_mode", w, f"traj_z3_ws{w}_d16_distinct.npz") for w in (2, 4, 8)] + \
+    [("_ref_injected", w, f"traj_z3_ws{w}_d16_ref.npz") for w in (2, 4, 8)] + \
+    [("_update_injected", w, f"traj_z2_ws{w}_d16_distinct.npz") for w in (2, 3, 4, 8)] + \
+    [("_update_hooks", w, f"traj_z2_ws{w}_d16_{m}.npz")
+     for w, m in ((2, "distinct"), (3, "distinct"), (4, "distinct"), (8, "ref"), (8, "distinct"))]
 
 
 @pytest.mark.parametrize("ws", [2, 3, 4, 8])
-def test_multirank_update_mode(gpu, ws):
-    """ws=3 exercises uneven torch.chunk (16 rows → 6,6,4), which deadlocks the reference."""
-    spawn_ranks(_mr, ws, (ws, _port(), "_update_injected", f"traj_z2_ws{ws}_d16_distinct.npz"))
-
-
-@pytest.mark.parametrize("ws,mode", [(2, "distinct"), (3, "distinct"), (4, "distinct"), (8, "ref"),
-                                     (8, "distinct")])
-def test_multirank_update_mode_hooks(gpu, ws, mode):
-    spawn_ranks(_mr, ws, (ws, _port(), "_update_hooks", f"traj_z2_ws{ws}_d16_{mode}.npz"))
+def test_multirank_zero3(gpu, ws):
+    """Every ZeRO-3 mode at this ws, one after another in one set of processes: reference mode
+    through the real hooks (params never change, reduced shards vs the fixture) and with the
+    reference's step() inputs injected (1e-6); update mode (real ZeRO-3) injected — uneven dim-0
+    chunks at ws = 3 — and through the hooks, against DP-Adam sliced to each rank's chunk."""
+    spawn_batch(ws, [(_mr, (fn, name)) for fn, w, name in Z3_CASES if w == ws])
 
 
 def _mem_worker(rank, ws, port):
