@@ -73,6 +73,9 @@ def probed_zeros(n: int, dtype, device, tries: int = 8, accept_gbs: float = PROB
     env = os.environ.get("ZERO_AMD_PROBE_TRIES")  # diagnostics: 1 = plain allocation
     if env:
         tries = int(env)
+    env = os.environ.get("ZERO_AMD_PROBE_ACCEPT_GBS")  # diagnostics: the acceptance threshold
+    if env:
+        accept_gbs = float(env)
     if tries <= 1 or nbytes < PROBE_MIN_BYTES:
         return torch.zeros(n, dtype=dtype, device=device), info
     free, total = torch.cuda.mem_get_info(device)
