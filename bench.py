@@ -1041,7 +1041,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     # default: ~4 s of timed GPU work at N=1 (C4), long enough for an outside utilisation sampler
-    ap.add_argument("--steps", type=int, default=None, help="default 300 (--train: 4)")
+    ap.add_argument("--steps", type=int, default=None,
+                    help="default 1500 at N=1 (~20 s of GPU time at C4, so an outside utilisation "
+                         "sampler sees the timed region), 300 at N>1 (exchange-bound steps are "
+                         "longer); --train: 4")
     ap.add_argument("--warmup", type=int, default=None, help="default 5 (--train: 2)")
     ap.add_argument("--config", default="C4", choices=["C2", "C3", "C4", "C5"])
     ap.add_argument("--zero", type=int, default=2, choices=[1, 2, 3],
@@ -1109,7 +1112,7 @@ def main():
                          "after this many seconds (a collective that never completes)")
     args = ap.parse_args()
     if args.steps is None:
-        args.steps = 4 if args.train else 300
+        args.steps = 4 if args.train else (1500 if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 300)
     if args.warmup is None:
         args.warmup = 2 if args.train else 5
     _start_watchdog(args.watchdog_s)
