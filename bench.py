@@ -1006,6 +1006,18 @@ def bench_train_smollm3(args, world, rank, dev, use_nccl):
     ms = el / args.steps * 1e3
     tok_s = world * batch * args.seq / (ms / 1e3)
     fpt = sm.model_flops_per_token(cfg, args.seq)
+    identical = None
+    if world > 1 and args.zero != 3:  # ZeRO-2 broadcasts every update: replicas must agree bit for bit
+        sums = []
+        for p in model.parameters():
+            sums += _bit_checksums(p.detach(), dev)
+        lo = torch.tensor(sums, dtype=torch.int64, device=red_dev)
+        hi = lo.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        identical = bool(torch.equal(lo, hi))
+        if not identical:
+            _fail_check("SmolLM3 ZeRO-2 replicas", rank, "parameters differ across ranks after training")
     if os.environ.get("ZERO_AMD_DIAG_BW"):  # diagnostics: streaming GB/s of fresh 64 MB buffers
         print(json.dumps({"diag_fresh_64mb_copy_gbs": _fresh_buffer_gbs(dev),
                           "segments": torch.cuda.memory_stats(dev).get("segment.all.current"),
@@ -1027,6 +1039,7 @@ def bench_train_smollm3(args, world, rank, dev, use_nccl):
                                     "backward-overlapped"), "params": int(params),
                        "layers": cfg.num_hidden_layers, "seq_len": args.seq,
                        "global_batch": world * batch, "parallelism": f"dp{world}"},
+            "params_identical_across_ranks": identical, "rehearsal": _REHEARSAL[0],
             "mfu_flops_per_token": fpt,
             "tflops_per_gpu": fpt * tok_s / world / 1e12,
             "loss": float(loss.item()),

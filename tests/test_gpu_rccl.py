@@ -159,3 +159,16 @@ def test_bench_share_gpu_zero3_mlp(gpu):
     assert out["n_gpus"] == 2 and out["rehearsal"].startswith("share-gpu")
     chk = out["exchange_check"]
     assert chk["all_ranks_ok"] and chk["max_rel_err"] <= chk["tol"] == 2.0 ** -7
+
+
+@pytest.mark.parametrize("zero", [2, 3])
+def test_bench_share_gpu_smollm3(gpu, zero):
+    """§8(f) 3 at N = 2 through real RCCL: SmolLM3 (2 decoder layers, full vocabulary) trains
+    with ZeRO-2 (backward-overlapped reduces; replicas bit-identical afterwards) or ZeRO-3
+    (per-layer gathers, backward reduce-scatters)."""
+    out = _bench2(["--train", "smollm3", "--zero", str(zero), "--train-layers", "2", "--seq", "256",
+                   "--steps", "2", "--warmup", "1"])
+    assert out["n_gpus"] == 2 and out["rehearsal"].startswith("share-gpu")
+    assert out["loss"] == out["loss"] and out["value"] > 0  # finite loss
+    if zero == 2:
+        assert out["params_identical_across_ranks"] is True
