@@ -130,6 +130,19 @@ def _sum_ranks(arrs):
     return acc
 
 
+def ddp_sync(local_by_rank, bf16: bool = False):
+    """DDP/ddp.py:43-47 ``sync_gradients``: every rank's gradient all-reduced (SUM) then divided
+    in place by the world size.  fp32: the sum in rank order, then ``/ ws`` in fp32.  bf16: the
+    sum rounded to bf16 once (a ring rounds per hop — within tolerance of this), then ``/ ws``
+    rounded to bf16.  Returns fp32 values."""
+    ws = len(local_by_rank)
+    acc = _sum_ranks([np.asarray(a, F32) for a in local_by_rank])
+    if bf16:
+        acc = bf16_round(acc)
+        return bf16_round((acc / F32(ws)).astype(F32))
+    return (acc / F32(ws)).astype(F32)
+
+
 def bf16_round(x):
     """fp32 → bf16 (round to nearest even) → fp32."""
     return bf16_bits_to_f32(f32_to_bf16_bits(np.asarray(x, F32))).reshape(np.shape(x))

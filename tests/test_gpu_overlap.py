@@ -239,9 +239,63 @@ def _ddp_worker(rank, ws, port, dtype_name):
     sys.stdout.flush()
 
 
+def _ddp_fixture_worker(rank, ws, port, dtype_name):
+    """The drop-in against the reference's own SimpleDistributedDataParallelism outputs
+    (tests/golden/ddp_sync_ws*_*.npz, made by running its class on gloo): the same seeded model,
+    each step's local gradients set by hand, sync_gradients().  ws = 2: bit-exact (fp32 and bf16:
+    a two-term sum rounds once in any order, / 2 is exact); ws = 3: within the ring's order noise
+    (fp32 1e-6, bf16 2^-7 normwise).  The last Linear gets no gradient and keeps None."""
+    import sys
+    from conftest import PKG, REPO  # noqa: F401
+    from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
+    from zero_amd.ddp import SimpleDistributedDataParallelism
+
+    torch.cuda.set_device(0)
+    init_pg(rank, ws, port)
+    dev = torch.device("cuda:0")
+    dt = getattr(torch, dtype_name)
+    bf16 = dt == torch.bfloat16
+    z = np.load(GOLDEN / f"ddp_sync_ws{ws}_{dtype_name}.npz")
+
+    def tens(a):
+        t = torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16) if bf16 else torch.from_numpy(a.copy())
+        return t.to(dev)
+
+    torch.manual_seed(0)  # the generator's model init (make_ddp_golden.py), on the CPU, then moved
+    model = torch.nn.Sequential(torch.nn.Linear(40, 24), torch.nn.ReLU(), torch.nn.Linear(24, 8),
+                                torch.nn.Linear(8, 8)).to(dt).to(dev)
+    ddp = SimpleDistributedDataParallelism(model, bucket_mb=1e-3, comm=test_comm())
+    params = list(model.parameters())
+    for t in range(3):
+        for i, p in enumerate(params):
+            p.grad = tens(z[f"r{rank}_t{t}_in{i}"]) if bool(z[f"has{i}"]) else None
+        ddp.sync_gradients()
+        torch.cuda.synchronize()
+        for i, p in enumerate(params):
+            if not bool(z[f"has{i}"]):
+                assert p.grad is None
+                continue
+            got = p.grad.detach().cpu()
+            want = tens(z[f"r{rank}_t{t}_out{i}"]).cpu()
+            if ws == 2:
+                assert torch.equal(got, want), (dtype_name, rank, t, i)
+            else:
+                tol = 2.0 ** -7 if bf16 else 1e-6
+                d = float((got.float() - want.float()).abs().max() / want.float().abs().max())
+                assert d <= tol, (dtype_name, rank, t, i, d)
+    dist.barrier()
+    dist.destroy_process_group()
+    sys.stdout.flush()
+
+
 @pytest.mark.parametrize("ws", [1, 2, 3])
 def test_ddp_sync_gradients(gpu, ws):
-    spawn_batch(ws, [(_ddp_worker, (d,)) for d in ("float32", "bfloat16")])
+    """DDP drop-in: the numpy restatement through a real backward (every ws), and the reference's
+    own sync_gradients outputs (ws 2-3)."""
+    cases = [(_ddp_worker, (d,)) for d in ("float32", "bfloat16")]
+    if ws > 1:
+        cases += [(_ddp_fixture_worker, (d,)) for d in ("float32", "bfloat16")]
+    spawn_batch(ws, cases)
 
 
 @pytest.mark.parametrize("n", [1, 7, 1000, 4099, 1 << 20])

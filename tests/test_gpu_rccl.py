@@ -48,7 +48,7 @@ def _batch(ws, cases):
 
 def _zero12_cases(ws):
     from test_gpu_layouts import _worker as layout_worker
-    from test_gpu_overlap import _ddp_worker, _frozen_worker, _mr_worker as ov_worker
+    from test_gpu_overlap import _ddp_fixture_worker, _ddp_worker, _frozen_worker, _mr_worker as ov_worker
     from test_gpu_parity import (_bf16comm_worker, _carry_worker, _comm_time_worker, _edge_worker,
                                  _hp_worker, _mr_worker)
 
@@ -60,7 +60,8 @@ def _zero12_cases(ws):
     if ws == 2:
         cases += [(_bf16comm_worker, ("zero2",)), (_comm_time_worker, ()),
                   (ov_worker, (1, "traj_z1_ws2_d16_distinct.npz", True, "flat")),
-                  (_frozen_worker, (2, True)), (_ddp_worker, ("float32",)), (_ddp_worker, ("bfloat16",))]
+                  (_frozen_worker, (2, True)), (_ddp_worker, ("float32",)), (_ddp_worker, ("bfloat16",)),
+                  (_ddp_fixture_worker, ("float32",)), (_ddp_fixture_worker, ("bfloat16",))]
     if ws == 3:
         cases += [(_hp_worker, (2, "adamw_amsgrad_2groups")), (_carry_worker, ("optimizer",)),
                   (_bf16comm_worker, ("zero2_overlap",)),

@@ -232,3 +232,31 @@ def test_cpu_reference_step_restatement(variant, ws):
 
     mp.spawn(_cpu_step_worker, args=(ws, free_port(), variant, f"traj_z{variant}_ws{ws}_d16_distinct.npz"),
              nprocs=ws, join=True)
+
+
+@pytest.mark.parametrize("ws", [2, 3])
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_ddp_sync_restatement_vs_reference(golden, ws, dtype):
+    """zero_oracle.ddp_sync against the reference's own SimpleDistributedDataParallelism
+    (tests/golden/make_ddp_golden.py: its class, run on gloo): bit-exact for fp32 at ws=2 and
+    for bf16 at ws=2 (a two-term sum rounds once in any order); at ws=3 within the ring's
+    summation-order noise (fp32 1e-6, bf16 2^-7 normwise)."""
+    z = golden(f"ddp_sync_ws{ws}_{dtype}.npz")
+    bf16 = dtype == "bfloat16"
+
+    def val(a):
+        return zo.bf16_bits_to_f32(a).reshape(a.shape) if bf16 else a
+
+    for t in range(3):
+        for i in range(6):
+            if not bool(z[f"has{i}"]):
+                assert f"r0_t{t}_out{i}" not in z.files  # no gradient: skipped, stays None
+                continue
+            want = zo.ddp_sync([val(z[f"r{r}_t{t}_in{i}"]) for r in range(ws)], bf16=bf16)
+            for r in range(ws):
+                got = val(z[f"r{r}_t{t}_out{i}"])
+                if ws == 2:
+                    assert np.array_equal(got, want), (ws, dtype, t, i, r)
+                else:
+                    tol = 2.0 ** -7 if bf16 else 1e-6
+                    assert np.max(np.abs(got - want)) <= tol * np.max(np.abs(want)), (ws, dtype, t, i, r)
