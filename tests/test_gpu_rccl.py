@@ -55,7 +55,7 @@ def _zero12_cases(ws):
     inj = {2: [(1, "distinct", None), (2, "distinct", None)],
            3: [(1, "distinct", "buckets")],
            4: [(1, "ref", None), (2, "distinct", None), (2, "distinct", "buckets")],
-           8: [(2, "distinct", None)]}[ws]
+           8: [(2, "distinct", None), (1, "distinct", None), (2, "distinct", "buckets")]}[ws]
     cases = [(_mr_worker, (v, f"traj_z{v}_ws{ws}_d16_{m}.npz", "ragged", a)) for v, m, a in inj]
     if ws == 2:
         cases += [(_bf16comm_worker, ("zero2",)), (_comm_time_worker, ()),
