@@ -1,5 +1,6 @@
 """Full-scale (BASELINE.json configs[3], SmolLM3-3B set, 3.08e9 bf16 params) properties of the
-bucketed ZeRO-2 step, size-independent so no full-size oracle run is needed.
+bucketed ZeRO-2 step, size-independent so no full-size oracle run is needed.  ws = 1 is the
+headline's own step (one 3.08e9-element stream: offsets past 2^31).
 
 Rank 0 of a ws-rank job runs on the one GPU with an identity communicator (nothing arrives from
 the other ranks, nothing leaves): after one step every parameter rank 0 owns must equal the C
@@ -40,7 +41,8 @@ class IdentityComm:
 
 
 @pytest.mark.parametrize("ws,buckets,arena", [(8, "ragged", "buckets"), (4, "padded", "buckets"),
-                                              (8, "ragged", "flat"), (3, "ragged", "flat")])
+                                              (8, "ragged", "flat"), (3, "ragged", "flat"),
+                                              (1, "ragged", "flat")])
 def test_c4_rank0_bucket_path_full_scale(gpu, monkeypatch, ws, buckets, arena):
     import torch.distributed as dist
 
@@ -77,7 +79,10 @@ def test_c4_rank0_bucket_path_full_scale(gpu, monkeypatch, ws, buckets, arena):
         opt.step()
         torch.cuda.synchronize()
         eng = opt.engine
-        if arena == "flat":
+        if arena == "flat" and ws == 1:  # the headline's layout: ONE stream of 3.08e9 elements,
+            # so arena offsets, Adam chunk indices and segment offsets run past 2^31 (int64 paths)
+            assert getattr(eng, "arena_kind", None) == "flat" and eng.P.numel() > 2 ** 31
+        elif arena == "flat":
             assert getattr(eng, "arena_kind", None) == "flat" and eng.K > 1
             for p in params:  # every parameter is a view of the arena
                 assert p.data.untyped_storage().data_ptr() == eng.P.untyped_storage().data_ptr()
