@@ -337,18 +337,20 @@ def test_c3_hooked_iteration_rank0_of_ws8(gpu, monkeypatch):
         dist.destroy_process_group()
 
 
-def test_c5_paramset_step_rank0_of_ws8(gpu, monkeypatch):
+@pytest.mark.parametrize("ws", [8, 1])
+def test_c5_paramset_step_rank0_of_ws8(gpu, monkeypatch, ws):
     """BASELINE.json configs[4] at full size: the Llama-3.1-8B-shaped set (291 bf16 tensors, 8.03e9
     params) as 34 hooked layer modules, rank 0 of ws=8: per-layer gathers in forward and backward,
     synthetic full gradients reduce-scattered from the hooks, split-master Adam on the chunks.
-    Sampled chunk elements equal the C oracle's split-master Adam of (chunk gradient / 8)."""
+    Sampled chunk elements equal the C oracle's split-master Adam of (chunk gradient / 8).
+    ws = 1 is the bench's N=1 configs[4] step: one 8.03e9-element chunk arena, so element offsets
+    run past 2^32 (no hooks: every shard is its whole parameter)."""
     import zero_amd.zero3 as z3
     from _gloo_comm import SimRankComm
     from oracle import c_oracle
     from zero_amd.paramset import ParamSetModel, decoder_layer_groups
     from zero_amd.shapes import llama31_8b_shapes
 
-    ws = 8
     init_pg(0, 1, _port())
     real_get = z3.get
     monkeypatch.setattr(z3, "get", lambda what, dm=None: {"ws": ws, "rank": 0}[what]
@@ -373,8 +375,11 @@ def test_c5_paramset_step_rank0_of_ws8(gpu, monkeypatch):
         opt.step()
         torch.cuda.synchronize()
         # forward + backward per layer, plus the prefetch of the next iteration's first gather
-        assert opt.runtime.n_gathers == 2 * len(model.layers) + 1
+        # (ws = 1: no hooks at all)
+        assert opt.runtime.n_gathers == (2 * len(model.layers) + 1 if ws > 1 else 0)
         ar = opt._arena
+        if ws == 1:
+            assert ar.P.numel() > 2 ** 32
         hp = c_oracle.hparams(step=1, grad_div=float(ws))
         rng = np.random.default_rng(1)
         for i, p in enumerate(params):
