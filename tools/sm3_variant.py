@@ -4,7 +4,8 @@ to find which one makes the ws=1 step's kernels slower than ZeRO-2's (DESIGN.md 
     python tools/sm3_variant.py <variant> [bench args...]
 
 variants: none (as is) | nohooks (no module hooks) | nobwdhooks (forward hooks only) |
-          nogradhooks (no post-accumulate-grad hooks: grads collected at step())."""
+          nogradhooks (no post-accumulate-grad hooks: grads collected at step()) |
+          nooverlap (ZeRO-2: no backward-overlapped reduce hooks).""""
 from __future__ import annotations
 
 import os
@@ -39,6 +40,15 @@ def main():
         zero3.register_zero3_hooks = fwd_only
     elif variant == "nogradhooks":
         zero3._GradReducer.register_hooks = lambda self: []
+    elif variant == "nooverlap":  # ZeRO-2 without the backward-overlapped reduce hooks
+        from zero_amd import zero2
+
+        real_init = zero2.ShardedOptimizer.__init__
+
+        def init(self, *a, **k):
+            k["overlap"] = False
+            real_init(self, *a, **k)
+        zero2.ShardedOptimizer.__init__ = init
     elif variant != "none":
         raise SystemExit(f"unknown variant {variant}")
     import json
