@@ -5,7 +5,7 @@ to find which one makes the ws=1 step's kernels slower than ZeRO-2's (DESIGN.md 
 
 variants: none (as is) | nohooks (no module hooks) | nobwdhooks (forward hooks only) |
           nogradhooks (no post-accumulate-grad hooks: grads collected at step()) |
-          nooverlap (ZeRO-2: no backward-overlapped reduce hooks).""""
+          nooverlap (ZeRO-2: no backward-overlapped reduce hooks)."""
 from __future__ import annotations
 
 import os
