@@ -446,6 +446,15 @@ def _zero3_report(args, opt, world, rank, red_dev, el, total, workload, extra):
         _phase("bucket-size sweep")
         comm["sweep"] = comm_sweep(opt.comm, opt.grad_arena(), world, red_dev,
                                    sizes_mb=(4, 8, 16, 32, 64, 128, 256))
+    traffic, traffic_src = None, None
+    if world == 1 and args.gather is None and getattr(args, "set_layers", None) is None:
+        # PMC passes of this same configuration (profiles/README.md), matched like the ZeRO-1/2 line
+        want = {"workload": args.config, "zero": 3, "param_dtype": args.dtype, "n_gpus": world,
+                "master": "split"}
+        for tj in sorted((REPO / "profiles").glob("*_pmc.json")):
+            d = json.loads(tj.read_text())
+            if d.get("config") == want:
+                traffic, traffic_src = d.get("hbm_bytes_per_launch"), str(tj.relative_to(REPO))
     if rank == 0:
         out = {
             "metric": METRIC, "value": total / (ms / 1e3), "unit": "params/s", "n_gpus": world,
@@ -458,11 +467,11 @@ def _zero3_report(args, opt, world, rank, red_dev, el, total, workload, extra):
                            update="real ZeRO-3 (update=True)", bucket_mb=args.bucket_mb or 128.0,
                            gather_dtype=args.gather or args.dtype, parallelism=f"dp{world}"),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "adam_segments_kernel",
                          "avg_launch_ms": adam_ms / max(len(ev), 1),
                          "alg_bytes_per_launch": adam_bytes / max(len(ev), 1),
-                         "launches_per_step": len(ev) / args.steps},
+                         "launches_per_step": len(ev) / args.steps, "traffic_source": traffic_src},
             "zero3": {"gathers_per_step": opt.runtime.n_gathers / (args.steps + args.warmup),
                       "prefetch_hits": opt.runtime.n_prefetch_hits,
                       "reduce_buckets_per_step": opt._reducer.K,
