@@ -525,8 +525,17 @@ def _zero3_comm(args, world, rank, dev):
     return None, None
 
 
+class ExchangeCheckFailed(RuntimeError):
+    pass
+
+
+_IN_PROCESS = [False]  # main() called from a test process: raise instead of exiting it
+
+
 def _fail_check(what: str, rank: int, detail) -> None:
     log(f"[bench] EXCHANGE CHECK FAILED on rank {rank}: {what}: {detail}")
+    if _IN_PROCESS[0]:
+        raise ExchangeCheckFailed(f"rank {rank}: {what}: {detail}")
     sys.stdout.flush()
     sys.stderr.flush()
     os._exit(4)
@@ -1059,7 +1068,8 @@ def bench_train_smollm3(args, world, rank, dev, use_nccl):
     dist.destroy_process_group()
 
 
-def main():
+def main(argv=None):
+    """The benchmark; returns rank 0's JSON object (None on other ranks) after printing it."""
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     # default: ~4 s of timed GPU work at N=1 (C4), long enough for an outside utilisation sampler
@@ -1089,8 +1099,8 @@ def main():
                     help="--train --zero 3: keep gathered parameters from forward through backward "
                          "(FSDP2 reshard_after_forward=False, the reference's 'ZeRO-2' run)")
     ap.add_argument("--set-layers", type=int, default=None,
-                    help="--zero 3 on C4/C5: a copy of the parameter set with fewer decoder layers "
-                         "(tests)")
+                    help="C4/C5: a copy of the parameter set with fewer decoder layers (tests and "
+                         "N=8 rehearsals on one GPU; not the metric)")
     ap.add_argument("--layout", default="reference", choices=["reference", "flat", "chunk"],
                     help="optimizer-shard layout: reference = whole params by index (zero1.py:55-62, "
                          "ZeRO-1/2); chunk = dim-0 chunks of every param (zero3.py:107-108, forced "
@@ -1132,7 +1142,7 @@ def main():
     ap.add_argument("--watchdog-s", type=float, default=1200.0,
                     help="end the process (exit 3) with a diagnostic if the run has not finished "
                          "after this many seconds (a collective that never completes)")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     if args.steps is None:
         args.steps = 4 if args.train else (1500 if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 300)
     if args.warmup is None:
@@ -1182,6 +1192,11 @@ def main():
         return bench_zero3_paramset(args, world, rank, dev, use_nccl)
     name, shape_fn = CONFIGS[args.config]
     shapes = shape_fn()
+    if args.set_layers is not None:  # test-size copy of the set: fewer decoder layers
+        from zero_amd.shapes import decoder_shapes
+
+        shapes = decoder_shapes(args.config, args.set_layers)
+        name += f" ({args.set_layers} layers)"
     total = int(sum(int(np.prod(s)) for s in shapes))
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     gen = torch.Generator(device=dev)
@@ -1450,6 +1465,7 @@ def main():
         print(json.dumps(out), flush=True)
     _teardown(opt)
     dist.destroy_process_group()
+    return out if rank == 0 else None
 
 
 if __name__ == "__main__":

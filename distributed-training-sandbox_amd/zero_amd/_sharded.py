@@ -11,11 +11,13 @@ engine (engine.py → libzero_amd.so); the inner torch optimizer's own ``step`` 
 from __future__ import annotations
 
 import time
+import weakref
 
 import torch
 import torch.distributed as dist
 from torch.optim import Optimizer
 
+from . import checkpoint as ckpt
 from .engine import ShardEngine
 from .training_utils.utils import get
 
@@ -63,6 +65,7 @@ class ShardedOptimizerBase:
         self.local_param_indices = list(range(start_idx, end_idx))
         self.local_params = set(self.params[i] for i in self.local_param_indices)
         self._shard_optimizer_params()
+        ckpt.bind_inner_load(self)  # opt.optimizer.load_state_dict fills the flat state
 
         self.broadcast_count = 0
         self.communication_time = 0.0
@@ -185,12 +188,14 @@ class ShardedOptimizerBase:
         grads = [p.grad for p in self.params]
         seen = self._validated
         for i, (g, p) in enumerate(zip(grads, self.params)):
-            if g is None or g is seen[i]:  # the same grad tensor as last step: already checked
+            # the same grad tensor as last step: already checked (a weak reference, so a grad the
+            # step releases is not kept alive by the check)
+            if g is None or (seen[i] is not None and seen[i]() is g):
                 continue
             if g.dtype != p.dtype or g.shape != p.shape or not g.is_contiguous():
                 raise ValueError("zero_amd: grads must be contiguous and match their param's "
                                  "dtype and shape")
-            seen[i] = g
+            seen[i] = weakref.ref(g)
         with torch.no_grad():
             self.engine.step(grads, self._hparams_of)
         if not had_vmax and self.engine.vmax is not None:
@@ -239,8 +244,84 @@ class ShardedOptimizerBase:
     def param_groups(self):
         return self.optimizer.param_groups
 
+    # checkpointing (zero_amd/checkpoint.py) -------------------------------------------------------
+    def _ckpt_header(self):
+        return ckpt.header(self._variant, self.world_size, self.rank, self.local_param_indices)
+
+    def _ckpt_views(self, i: int) -> dict:
+        """name -> live view of param i's flat state (the owned params of Layout R)."""
+        eng = self.engine
+        views = eng.state_views(i)
+        if views is None:
+            raise NotImplementedError("zero_amd: state_dict() needs the reference (whole-param) layout")
+        if eng.vmax is not None:
+            so = int(eng.pieces.stream_off[eng.pieces.param == i][0])
+            views["max_exp_avg_sq"] = eng.vmax[so:so + self.params[i].numel()].view(self.params[i].shape)
+        if eng.carry is not None:
+            so = int(eng.pieces.stream_off[eng.pieces.param == i][0])
+            views["zero1_carry"] = eng.carry[so:so + self.params[i].numel()].view(self.params[i].shape)
+        return views
+
     def state_dict(self):
-        return self.optimizer.state_dict()
+        """The inner optimizer's state dict in torch's format (indices over the owned parameters,
+        as the reference's ``opt.optimizer.state_dict()``), every tensor a copy of the engine's
+        flat state, plus the split master's residual / fp32 master and ZeRO-1's carry
+        (zero_amd/checkpoint.py)."""
+        torch.cuda.synchronize(self.params[0].device)  # the state of every enqueued step
+        sd = Optimizer.state_dict(self.optimizer)
+        index = {id(p): k for k, p in enumerate(ckpt.inner_params(self.optimizer))}
+        state = {}
+        if self.engine is not None:
+            for i in self.engine.owned_param_indices():
+                p = self.params[i]
+                if id(p) not in index:
+                    continue
+                entry = {k: v.detach().clone() for k, v in self._ckpt_views(i).items()}
+                entry["step"] = torch.tensor(float(self.engine.steps[i]), dtype=torch.float32)
+                state[index[id(p)]] = entry
+        sd["state"] = state
+        sd["zero_amd"] = self._ckpt_header()
+        return sd
+
+    def load_state_dict(self, state_dict):
+        """Restore a ``state_dict()`` of this rank (or a plain torch Adam state dict over the same
+        owned parameters): hyper-parameters through torch's loader, state copied into the flat
+        buffers.  Parameters are the model's (load them with the model's own state dict)."""
+        ckpt.check_header(state_dict, self._ckpt_header())
+        if self.engine is None:
+            self._build_engine()
+        eng = self.engine
+        torch.cuda.synchronize(eng.device)
+        ckpt.load_param_groups(self.optimizer, state_dict)
+        self.original_param_groups = self.optimizer.param_groups
+        self._groups = list(self.optimizer.param_groups)
+        saved = state_dict.get("state", {})
+        params = ckpt.inner_params(self.optimizer)
+        if any("max_exp_avg_sq" in saved.get(k, {}) for k in range(len(params))) and eng.vmax is None:
+            eng.ensure_vmax()
+            if hasattr(eng, "rebuild_rows"):
+                eng.rebuild_rows()
+        index = {id(p): k for k, p in enumerate(params)}
+        with torch.no_grad():
+            for i in eng.owned_param_indices():
+                p = self.params[i]
+                entry = saved.get(index.get(id(p), -1), {})
+                views = self._ckpt_views(i)
+                for name, view in views.items():
+                    src = entry.get(name)
+                    if src is not None:
+                        view.copy_(src.reshape(view.shape))
+                    elif name == "master_residual":  # master = the bf16 param exactly
+                        view.zero_()
+                    elif name == "master_param":
+                        view.copy_(p.detach().reshape(view.shape))
+                    else:  # no state: torch's fresh Adam (moments 0), no carry
+                        view.zero_()
+                eng.steps[i] = ckpt.step_of(entry)
+        self.optimizer.state.clear()
+        self._expose_state()
+        self._update_step_state()
+        ckpt.bind_inner_load(self)
 
     def __repr__(self):
         return (f"{type(self).__name__}(zero={self._variant}, ws={self.world_size}, rank={self.rank}, "

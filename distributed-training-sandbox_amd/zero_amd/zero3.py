@@ -45,6 +45,7 @@ from torch.optim import Optimizer
 
 from . import _lib
 from ._lib import ZS_BF16, ZS_BF16_SPLIT, ZS_F32
+from . import checkpoint as ckpt
 from ._sharded import adam_group_hparams
 from .comm import RcclComm, comm_stream, zs_dtype
 from .engine import ALIGN_ELEMS, probed_zeros
@@ -685,6 +686,7 @@ class ShardedOptimizer:
         if not self.update:
             for group in self.optimizer.param_groups:  # zero3.py:114-115
                 group["params"] = [p for p in group["params"] if p in self.local_params]
+        ckpt.bind_inner_load(self)  # opt.optimizer.load_state_dict fills the flat state
         self.grad_hooks = {}
         self.communication_time = 0.0
         self.step_time = 0.0
@@ -718,11 +720,36 @@ class ShardedOptimizer:
         self._steps = np.zeros(len(self.params), np.int64)
         self._adam_cache = {}
         self._retired = []
+        self._expose_state()
+
+    def _state_views(self, i: int) -> dict:
+        """name -> live view of param i's chunk of the flat update state."""
+        ar = self._arena
+        s, n, shp = int(ar.slot[i]), int(ar.ln[i]), ar.shard_shapes[i]
+        views = {"exp_avg": self._m[s:s + n].view(shp), "exp_avg_sq": self._v[s:s + n].view(shp)}
+        if self._lo is not None:  # fp32 master = the bf16 chunk's bits << 16 + this residual
+            views["master_residual"] = self._lo[s:s + n].view(shp)
+        if self._vmax is not None:
+            views["max_exp_avg_sq"] = self._vmax[s:s + n].view(shp)
+        return views
+
+    def _expose_state(self):
+        """optimizer.state[p]: views of the flat state (chunk-shaped) and torch's ``step``."""
+        step_t = {}
         for i, p in enumerate(self.params):
-            s, n = int(ar.slot[i]), int(ar.ln[i])
             st = self.optimizer.state[p]
-            st["exp_avg"] = self._m[s:s + n].view(ar.shard_shapes[i])
-            st["exp_avg_sq"] = self._v[s:s + n].view(ar.shard_shapes[i])
+            st.update(self._state_views(i))
+            s = int(self._steps[i])
+            if s:
+                t = step_t.get(s)
+                if t is None:
+                    t = step_t[s] = torch.tensor(float(s))
+                st["step"] = t
+
+    def _ensure_vmax(self):
+        ar = self._arena
+        self._vmax = torch.zeros(ar.total, dtype=torch.float32, device=ar.device)
+        self._expose_state()  # (cached Adam rows gain the vmax pointer: rebuilt on their next use)
 
     def grad_arena(self):
         """The flat gradient chunk arena (update mode, ws > 1): slot i holds param i's summed chunk."""
@@ -802,10 +829,7 @@ class ShardedOptimizer:
         self._steps[idx] += 1
         hps = {gi: adam_group_hparams(self._groups[gi], self.optimizer) for gi in set(self._group_of)}
         if any(h["amsgrad"] for h in hps.values()) and self._vmax is None:
-            self._vmax = torch.zeros(ar.total, dtype=torch.float32, device=ar.device)
-            for i, p in enumerate(self.params):
-                s, n = int(ar.slot[i]), int(ar.ln[i])
-                self.optimizer.state[p]["max_exp_avg_sq"] = self._vmax[s:s + n].view(ar.shard_shapes[i])
+            self._ensure_vmax()
         if len(idx):
             rows = self._adam_rows(idx)
             keys = np.stack([np.asarray(self._group_of)[idx], self._steps[idx]], axis=1)
@@ -879,3 +903,54 @@ class ShardedOptimizer:
 
     def zero_grad(self, set_to_none: bool = True):
         self.optimizer.zero_grad(set_to_none=set_to_none)
+
+    # checkpointing (zero_amd/checkpoint.py) -------------------------------------------------------
+    def _ckpt_header(self):
+        return ckpt.header(3, self.world_size, self.rank, self.local_param_indices, update=self.update)
+
+    def state_dict(self):
+        """The inner optimizer's state dict in torch's format; update mode: every parameter's
+        entry is this rank's dim-0 chunk of its state (copies of the flat state, incl. the split
+        master's residual), so each rank saves its own shard.  Reference mode keeps no state
+        (zero3.py:150-153), like the reference."""
+        torch.cuda.synchronize(self._arena.device)
+        sd = Optimizer.state_dict(self.optimizer)
+        state = {}
+        if self.update:
+            index = {id(p): k for k, p in enumerate(ckpt.inner_params(self.optimizer))}
+            for i, p in enumerate(self.params):
+                entry = {k: v.detach().clone() for k, v in self._state_views(i).items()}
+                entry["step"] = torch.tensor(float(self._steps[i]), dtype=torch.float32)
+                state[index[id(p)]] = entry
+        sd["state"] = state
+        sd["zero_amd"] = self._ckpt_header()
+        return sd
+
+    def load_state_dict(self, state_dict):
+        """Restore this rank's ``state_dict()``: hyper-parameters through torch's loader, the
+        chunk state copied into the flat buffers.  The parameters themselves (this rank's chunks)
+        are restored by the caller, e.g. ``p.data.copy_(saved_chunk)``."""
+        ckpt.check_header(state_dict, self._ckpt_header())
+        torch.cuda.synchronize(self._arena.device)
+        ckpt.load_param_groups(self.optimizer, state_dict)
+        self.original_param_groups = self.optimizer.param_groups
+        self._groups = list(self.optimizer.param_groups)
+        self.optimizer.state.clear()
+        if not self.update:
+            return
+        saved = state_dict.get("state", {})
+        params = ckpt.inner_params(self.optimizer)
+        index = {id(p): k for k, p in enumerate(params)}
+        if any("max_exp_avg_sq" in e for e in saved.values()) and self._vmax is None:
+            self._ensure_vmax()
+        with torch.no_grad():
+            for i, p in enumerate(self.params):
+                entry = saved.get(index.get(id(p), -1), {})
+                for name, view in self._state_views(i).items():
+                    src = entry.get(name)
+                    if src is not None:
+                        view.copy_(src.reshape(view.shape))
+                    else:  # moments 0 (fresh Adam); residual 0 (master = the bf16 chunk)
+                        view.zero_()
+                self._steps[i] = ckpt.step_of(entry)
+        self._expose_state()

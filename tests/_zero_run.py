@@ -146,6 +146,35 @@ def _shifted(i, fn, args):
     fn(i + 1, *args)
 
 
+# Environment of the ranks a multi-rank GPU test spawns beside this process.  Up to 8 processes
+# share the box's one GPU; at HIP's default of 4 hardware queues each, an over-subscribed 8-rank
+# run stalled with half the ranks inside a backward pass while the others waited in a collective.
+# Two queues per spawned rank keep them within what the device schedules at once.  This process
+# (rank 0 of spawn_ranks, and every single-process test) keeps the box default.
+CHILD_ENV = {"GPU_MAX_HW_QUEUES": "2"}
+
+
+class child_env:
+    """os.environ += CHILD_ENV while child processes are started (spawned children copy the
+    parent's environment at start), restored afterwards."""
+
+    def __init__(self, extra=None):
+        self.extra = dict(CHILD_ENV, **(extra or {}))
+
+    def __enter__(self):
+        self.saved = {k: os.environ.get(k) for k in self.extra}
+        os.environ.update(self.extra)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        return False
+
+
 def _child(i, fn, args, deadline_s):
     import faulthandler
     import sys
@@ -165,8 +194,9 @@ def spawn_all_ranks(fn, ws: int, args=(), deadline_s: float = 150.0):
 
     import torch.multiprocessing as mp
 
-    ctx = mp.start_processes(_child, args=(fn, args, deadline_s), nprocs=ws, join=False,
-                             start_method="spawn")
+    with child_env():
+        ctx = mp.start_processes(_child, args=(fn, args, deadline_s), nprocs=ws, join=False,
+                                 start_method="spawn")
     t_end = time.time() + deadline_s + 30
     try:
         while not ctx.join(timeout=1.0):  # raises (and kills the rest) when a rank fails
@@ -214,8 +244,9 @@ def spawn_ranks(fn, ws: int, args=()):
     if ws == 1:
         fn(0, *args)
         return
-    ctx = mp.start_processes(_shifted, args=(fn, args), nprocs=ws - 1, join=False,
-                             start_method="spawn")
+    with child_env():
+        ctx = mp.start_processes(_shifted, args=(fn, args), nprocs=ws - 1, join=False,
+                                 start_method="spawn")
     try:
         fn(0, *args)
     except BaseException:

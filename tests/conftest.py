@@ -11,12 +11,10 @@ for p in (str(REPO), str(PKG), str(REPO / "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-# The multi-rank GPU tests put up to 8 ranks (+ this process) on the box's one GPU.  At HIP's
-# default of 4 hardware queues per process that is more queues than the device schedules at once;
-# an over-subscribed 8-rank run stalled with half the ranks inside a backward pass while the
-# others waited in a collective.  Two queues per process keep 9 processes within the limit (in a
-# queue shared by two streams, a wait is always behind the record it waits for, in host order).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "2")
+# This process (single-process kernel tests, rank 0 of the multi-rank ones) runs at the box's
+# default number of HIP hardware queues; only the ranks spawned beside it are given two
+# (tests/_zero_run.py CHILD_ENV), so up to 8 processes on the one GPU stay within the queues the
+# device schedules at once.
 
 
 def free_port() -> int:

@@ -25,7 +25,7 @@ import sys
 import pytest
 
 from conftest import REPO, free_port
-from _zero_run import spawn_batch
+from _zero_run import CHILD_ENV, spawn_batch
 
 pytestmark = pytest.mark.gpu
 
@@ -55,9 +55,13 @@ def _zero12_cases(ws):
     inj = {2: [(1, "distinct", None), (2, "distinct", None)],
            3: [(1, "distinct", "buckets")],
            4: [(1, "ref", None), (2, "distinct", None), (2, "distinct", "buckets")],
-           8: [(2, "distinct", None), (1, "distinct", None), (2, "distinct", "buckets")]}[ws]
+           8: [(2, "distinct", None), (1, "distinct", None), (2, "distinct", "buckets"),
+               (1, "distinct", "buckets")]}[ws]
     cases = [(_mr_worker, (v, f"traj_z{v}_ws{ws}_d16_{m}.npz", "ragged", a)) for v, m, a in inj]
     if ws == 2:
+        from test_gpu_checkpoint import _ckpt_worker
+
+        cases += [(_ckpt_worker, ("z1_fp32",)), (_ckpt_worker, ("z2_bf16_split",))]
         cases += [(_bf16comm_worker, ("zero2",)), (_comm_time_worker, ()),
                   (ov_worker, (1, "traj_z1_ws2_d16_distinct.npz", True, "flat")),
                   (_frozen_worker, (2, True)), (_ddp_worker, ("float32",)), (_ddp_worker, ("bfloat16",)),
@@ -72,6 +76,8 @@ def _zero12_cases(ws):
                   (_bf16comm_worker, ("zero2",)),
                   (ov_worker, (2, "traj_z2_ws4_d16_distinct.npz", True, "flat")),
                   (layout_worker, ("chunk", "traj_z2_ws4_d64_distinct.npz", "ragged", 64))]
+    if ws == 8:
+        cases += [(_bf16comm_worker, ("zero2",))]
     return cases
 
 
@@ -94,17 +100,27 @@ def _zero3_cases(ws):
                  ("_update_hooks", "traj_z2_ws2_d16_distinct.npz")],
              3: [("_update_injected", "traj_z2_ws3_d16_distinct.npz")],
              4: [("_ref_mode", "traj_z3_ws4_d16_distinct.npz"), ("_ref_injected", "traj_z3_ws4_d16_ref.npz"),
-                 ("_update_hooks", "traj_z2_ws4_d16_distinct.npz")]}[ws]
+                 ("_update_hooks", "traj_z2_ws4_d16_distinct.npz")],
+             # ws = 8: the exchanges the first 8-GPU run executes — table gathers from the module
+             # hooks in forward and backward, backward reduce-scatters, the shard all-reduce
+             8: [("_ref_mode", "traj_z3_ws8_d16_distinct.npz"), ("_ref_injected", "traj_z3_ws8_d16_ref.npz"),
+                 ("_update_hooks", "traj_z2_ws8_d16_ref.npz"),
+                 ("_update_injected", "traj_z2_ws8_d16_distinct.npz")]}[ws]
     cases = [(_mr, c) for c in cases]
-    if ws == 2:  # SmolLM3 ZeRO-3 AdamW bit-exact against the C oracle; fp8 gathers
+    if ws == 2:  # SmolLM3 ZeRO-3 AdamW bit-exact against the C oracle; fp8 gathers; checkpoint
+        from test_gpu_checkpoint import _ckpt_worker
+
+        cases += [(_ckpt_worker, ("z3_bf16",))]
         cases += [(_mr_zero3, (False, True)), (_mr_zero3, (True, False)),
                   (fp8_worker, (True,)), (fp8_worker, (False,))]
     if ws == 4:
         cases += [(_bf16comm_worker, ("zero3",)), (_mem_worker, ())]
+    if ws == 8:
+        cases += [(_bf16comm_worker, ("zero3",))]
     return cases
 
 
-@pytest.mark.parametrize("ws", [2, 3, 4])
+@pytest.mark.parametrize("ws", [2, 3, 4, 8])
 def test_rccl_zero3(gpu, rccl_env, ws):
     """ZeRO-3 through real RCCL: table gathers from the module hooks (reference and update mode),
     backward reduce-scatters, uneven chunks (ws = 3), bf16 gradient exchange, sharded gradient
@@ -114,7 +130,7 @@ def test_rccl_zero3(gpu, rccl_env, ws):
 
 # --- bench.py at N = 2 on the shared GPU ------------------------------------------------
 def _bench2(args, timeout=300):
-    env = dict(os.environ)
+    env = dict(os.environ, **CHILD_ENV)
     env.pop("ZS_TEST_COMM", None)
     env.pop("NCCL_HOSTID", None)  # bench --share-gpu sets it per rank
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
@@ -173,3 +189,60 @@ def test_bench_share_gpu_smollm3(gpu, zero):
     assert out["loss"] == out["loss"] and out["value"] > 0  # finite loss
     if zero == 2:
         assert out["params_identical_across_ranks"] is True
+
+
+# --- bench.py at N = 8 on the shared GPU: every exchange the 8-GPU run can pick ---------------
+def _bench_rank(rank, ws, port, argv):
+    """One rank of ``bench.main(argv)`` with the environment torch.distributed.run gives it (rank 0
+    runs in this process, as every ws = 8 test here: 8 processes on the one GPU, not 9)."""
+    import sys
+
+    from conftest import REPO
+
+    if str(REPO) not in sys.path:
+        sys.path.insert(0, str(REPO))
+    import bench
+
+    env = {"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(ws),
+           "LOCAL_WORLD_SIZE": str(ws), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+           "NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1"}
+    keys = list(env) + ["NCCL_HOSTID", "ZERO_AMD_PROBE_TRIES", "ZS_TEST_COMM"]
+    saved = {k: os.environ.get(k) for k in keys}
+    os.environ.update(env)
+    os.environ.pop("ZS_TEST_COMM", None)
+    bench._IN_PROCESS[0] = True
+    try:
+        out = bench.main(argv)
+    finally:
+        bench._IN_PROCESS[0] = False
+        bench._REHEARSAL[0] = None
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    if rank == 0:
+        checks = out["exchange_check_all_arenas"]
+        assert set(checks) == {"flat", "buckets"}, checks
+        for kind, c in checks.items():
+            assert c["all_ranks_ok"] and "failure" not in c, (kind, c)
+            assert c["reduce_max_err_over_bound"] <= 1.0 and c["adam_max_bf16_ulp"] <= 1, (kind, c)
+            assert c["params_identical_across_ranks"], (kind, c)
+        assert set(out["arena_calibration_ms_per_step"]) == {"flat", "buckets"}
+        assert out["rccl_selfcheck"]["all_ranks_ok"] and out["config"]["comm"] == "rccl"
+
+
+@pytest.mark.timeout(600)
+def test_bench_share_gpu_n8_both_arenas(gpu):
+    """The driver's default N=8 run (C4 ZeRO-2, ``--arena auto``) rehearsed through real RCCL on a
+    4-layer copy of the SmolLM3-3B set (8 ranks x full C4 exceed one device): communicator
+    self-check, then BOTH arenas the calibration can pick — the flat arena's grouped reduce /
+    broadcast rounds and the bucket arena's pack / RS / AG / unpack — each exchange-checked (reduced
+    grads within the ring bound, Adam within 1 bf16 ulp of the restatement, ranks bit-identical),
+    calibrated and timed."""
+    from _zero_run import spawn_ranks
+
+    argv = ["--gpus", "8", "--share-gpu", "--no-cpu-baseline", "--watchdog-s", "0", "--config", "C4",
+            "--set-layers", "4", "--zero", "2", "--arena", "auto", "--steps", "2", "--warmup", "1",
+            "--no-comm-sweep"]
+    spawn_ranks(_bench_rank, 8, (8, free_port(), argv))
