@@ -446,15 +446,14 @@ def _zero3_report(args, opt, world, rank, red_dev, el, total, workload, extra):
         _phase("bucket-size sweep")
         comm["sweep"] = comm_sweep(opt.comm, opt.grad_arena(), world, red_dev,
                                    sizes_mb=(4, 8, 16, 32, 64, 128, 256))
-    traffic, traffic_src = None, None
-    if world == 1 and args.gather is None and getattr(args, "set_layers", None) is None:
+    traffic, traffic_src, traffic_note = None, None, None
+    if (args.traffic_json or world == 1) and args.gather is None \
+            and getattr(args, "set_layers", None) is None:
         # PMC passes of this same configuration (profiles/README.md), matched like the ZeRO-1/2 line
         want = {"workload": args.config, "zero": 3, "param_dtype": args.dtype, "n_gpus": world,
                 "master": "split"}
-        for tj in sorted((REPO / "profiles").glob("*_pmc.json")):
-            d = json.loads(tj.read_text())
-            if d.get("config") == want:
-                traffic, traffic_src = d.get("hbm_bytes_per_launch"), str(tj.relative_to(REPO))
+        traffic, traffic_src, traffic_note = match_traffic(
+            want, adam_bytes / max(len(ev), 1), args.traffic_json)
     if rank == 0:
         out = {
             "metric": METRIC, "value": total / (ms / 1e3), "unit": "params/s", "n_gpus": world,
@@ -465,13 +464,18 @@ def _zero3_report(args, opt, world, rank, red_dev, el, total, workload, extra):
             "data": "synthetic",
             "config": dict(workload=workload, params=int(total), param_dtype=args.dtype, zero=3,
                            update="real ZeRO-3 (update=True)", bucket_mb=args.bucket_mb or 128.0,
-                           gather_dtype=args.gather or args.dtype, parallelism=f"dp{world}"),
+                           gather_dtype=args.gather or args.dtype, parallelism=f"dp{world}",
+                           gathers=("none at N=1: every shard is its whole parameter, no hooks "
+                                    "are registered (zero3.register_zero3_hooks), so this is an "
+                                    "unsharded step" if world == 1 and not args.gather
+                                    else "per-layer all-gathers in forward and backward")),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "adam_segments_kernel",
                          "avg_launch_ms": adam_ms / max(len(ev), 1),
                          "alg_bytes_per_launch": adam_bytes / max(len(ev), 1),
-                         "launches_per_step": len(ev) / args.steps, "traffic_source": traffic_src},
+                         "launches_per_step": len(ev) / args.steps, "traffic_source": traffic_src,
+                         "traffic_note": traffic_note},
             "zero3": {"gathers_per_step": opt.runtime.n_gathers / (args.steps + args.warmup),
                       "prefetch_hits": opt.runtime.n_prefetch_hits,
                       "reduce_buckets_per_step": opt._reducer.K,
@@ -530,6 +534,32 @@ class ExchangeCheckFailed(RuntimeError):
 
 
 _IN_PROCESS = [False]  # main() called from a test process: raise instead of exiting it
+
+
+def match_traffic(want: dict, alg_bytes_per_launch: float, traffic_json=None):
+    """roofline.traffic: HBM bytes per Adam launch from a PMC summary of THIS configuration —
+    ``--traffic-json`` if given, else the profiles/*_pmc.json whose ``config`` equals ``want`` — used
+    only when the summary's algorithmic bytes per launch equal this run's (within 1e-6): after a
+    kernel, arena or bucket change an old measurement is not reported as this run's.  Returns
+    (bytes or None, source or None, note or None)."""
+    # newest round's summary first (profiles are named by round: r01_, r02_, r02s2_, r03_ ...)
+    cands = [Path(traffic_json)] if traffic_json else sorted((REPO / "profiles").glob("*_pmc.json"),
+                                                              reverse=True)
+    note = None
+    for tj in cands:
+        if not tj.exists():
+            continue
+        d = json.loads(tj.read_text())
+        if not traffic_json and d.get("config") != want:
+            continue
+        src = str(tj.relative_to(REPO) if tj.is_absolute() and REPO in tj.parents else tj)
+        alg = float(d.get("algorithmic_bytes_per_launch") or 0.0)
+        if alg <= 0 or abs(alg - alg_bytes_per_launch) > 1e-6 * max(alg, alg_bytes_per_launch):
+            note = (f"{src}: algorithmic bytes per launch {alg:.6g} != this run's "
+                    f"{alg_bytes_per_launch:.6g}; not used")
+            continue
+        return d.get("hbm_bytes_per_launch"), src, None
+    return None, None, note
 
 
 def _fail_check(what: str, rank: int, detail) -> None:
@@ -1118,11 +1148,16 @@ def main(argv=None):
                          "reduce/broadcast per owner for the rest; padded: every window padded")
     ap.add_argument("--no-comm-sweep", action="store_true",
                     help="skip the RS/AG bus-bandwidth sweep (N>1, after the timed region)")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"],
+                    help="parameter dtype; default fp32 for --zero 3 on the C2/C3 MLP (the "
+                         "reference MLP is fp32, zero1.py:237-249), bf16 otherwise (C4/C5 sets)")
     ap.add_argument("--master", default="split", choices=["split", "fp32"],
                     help="bf16 params: the fp32 master as the bf16 param + an int16 residual "
                          "(split, 26 B/element per update) or a separate fp32 array (28 B)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fp32-master-line", action="store_true",
+                    help="N=1 bf16: skip timing the same step with the exact fp32 master beside "
+                         "the split-master headline")
     ap.add_argument("--cpu-sample", type=int, default=256 << 20)
     ap.add_argument("--simulate-ws", type=int, default=0,
                     help="DIAGNOSTIC (N=1 only): run the ws>1 bucket path of rank 0 of a ws-rank job "
@@ -1147,6 +1182,8 @@ def main(argv=None):
         args.steps = 4 if args.train else (1500 if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 300)
     if args.warmup is None:
         args.warmup = 2 if args.train else 5
+    if args.dtype is None:
+        args.dtype = "fp32" if (args.zero == 3 and args.config in ("C2", "C3")) else "bf16"
     _start_watchdog(args.watchdog_s)
 
     import numpy as np
@@ -1247,10 +1284,10 @@ def main(argv=None):
     arenas = ["flat", "buckets"] if (args.arena == "auto" and multi) else \
         [args.arena if args.arena != "auto" else "flat"]
 
-    def build(arena):
+    def build(arena, master=None):
         o = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), layout=args.layout,
                                  bucket_mb=args.bucket_mb, sync=False, buckets=args.buckets,
-                                 master=args.master, arena=arena, **kw)
+                                 master=master or args.master, arena=arena, **kw)
         if o.engine is None:
             o._build_engine()  # (the bucket engine is otherwise built by the first step)
         if getattr(o.engine, "arena_kind", None) == "flat":
@@ -1349,22 +1386,42 @@ def main(argv=None):
     if world > 1:  # report the slowest rank's Adam
         dist.all_reduce(stats, op=dist.ReduceOp.MIN)
     achieved = float(stats[0])
-    traffic = None
-    traffic_src = None
     want = {"workload": args.config, "zero": args.zero, "param_dtype": args.dtype,
             "layout": args.layout, "n_gpus": world}
     if args.dtype == "bf16":
         want["master"] = args.master
-    cands = [Path(args.traffic_json)] if args.traffic_json else sorted(
-        (REPO / "profiles").glob("*_pmc.json"))
-    for tj in cands:
-        if not tj.exists():
-            continue
-        d = json.loads(tj.read_text())
-        if d.get("config") == want:  # PMC passes of this same configuration (profiles/README.md)
-            traffic = d.get("hbm_bytes_per_launch")
-            traffic_src = str(tj.relative_to(REPO) if tj.is_absolute() else tj)
+    if world > 1 or args.simulate_ws > 1:
+        want["arena"] = arena_used
+    traffic, traffic_src, traffic_note = match_traffic(want, float(stats[2]), args.traffic_json)
 
+    placement = {"state": eng.placement, "arena": getattr(eng, "arena_placement", None),
+                 "grads": getattr(eng, "grad_placement", None),
+                 "reduced": getattr(eng, "reduced_placement", None)}
+    bucket_mb, n_buckets = opt._bucket_bytes / (1 << 20), eng.K
+    fp32_master = None
+    if (world == 1 and args.simulate_ws <= 1 and args.dtype == "bf16" and args.master == "split"
+            and not args.no_fp32_master_line):
+        # the same step with the exact fp32 master (28 B/elem) beside the split-master headline
+        # (26 B/elem, an exact tie stored 1 ulp toward zero: DESIGN §2)
+        _phase("fp32-master comparison")
+        eng = None  # (its placement is kept above) so the split state can be freed
+        _teardown_engine(opt)
+        opt, step = build(arena_used if multi else "flat", master="fp32")
+        for _ in range(args.warmup):
+            step()
+        opt.engine.timing_events = []
+        n_fp = min(args.steps, 300)
+        ms_fp = timed(step, n_fp)
+        ev_fp, opt.engine.timing_events = opt.engine.timing_events, None
+        a_ms = sum(a.elapsed_time(b) for a, b, _ in ev_fp)
+        a_b = sum(nb for *_, nb in ev_fp)
+        gbs = a_b / (a_ms / 1e3) / 1e9 if a_ms > 0 else 0.0
+        fp32_master = {"ms_per_step": ms_fp, "value": total / (ms_fp / 1e3), "steps": n_fp,
+                       "adam_achieved_gbs": gbs, "adam_frac": gbs / HBM_PEAK_GBS,
+                       "alg_bytes_per_launch": a_b / max(len(ev_fp), 1),
+                       "state_placement": opt.engine.placement,
+                       "what": "the same step with master='fp32' (exact fp32 master array, "
+                               "28 B/elem) instead of the split master"}
     copy_kernels = copy_summary(copy_events, args.steps, world, red_dev) if copy_events else None
     # step roofline: this rank's HBM bytes (Adam + pack + unpack) at 8 TB/s plus its bus bytes at
     # the 7-link xGMI aggregate, no overlap credit; the slowest rank's sum vs the measured step
@@ -1424,9 +1481,9 @@ def main(argv=None):
                 else "fp32 (master, exp_avg, exp_avg_sq)",
                 "master": args.master if args.dtype == "bf16" else "param",
                 "zero": args.zero, "layout": args.layout,
-                "bucket_mb": opt._bucket_bytes / (1 << 20),
+                "bucket_mb": bucket_mb,
                 "bucket_mode": args.buckets,
-                "buckets": eng.K, "parallelism": f"dp{world}", "comm": comm_used,
+                "buckets": n_buckets, "parallelism": f"dp{world}", "comm": comm_used,
                 "arena": arena_used,
             },
             "roofline": {
@@ -1435,14 +1492,14 @@ def main(argv=None):
                 "kernel": "adam_segments_kernel",
                 "avg_launch_ms": float(stats[1]), "alg_bytes_per_launch": float(stats[2]),
                 "launches_per_step": launches / args.steps,
-                "traffic_source": traffic_src,
+                "traffic_source": traffic_src, "traffic_note": traffic_note,
             },
         }
         out["step_roofline"] = step_roofline
-        out["placement"] = {"state": eng.placement,
-                            "arena": getattr(eng, "arena_placement", None),
-                            "grads": getattr(eng, "grad_placement", None),
-                            "reduced": getattr(eng, "reduced_placement", None)}
+        out["placement"] = placement
+        if fp32_master is not None:
+            out["fp32_master_ms_per_step"] = fp32_master["ms_per_step"]
+            out["fp32_master"] = fp32_master
         if selfcheck is not None:
             out["rccl_selfcheck"] = selfcheck
         if exchange_check:

@@ -47,11 +47,46 @@ def _ptr(t: torch.Tensor | None) -> int:
     return 0 if t is None else int(t.data_ptr())
 
 
+def launch_groups(K: int, small_last: bool = False):
+    """Buckets 0..K-1 cut into runs of doubling length — 1, 1, 2, 4, 8, ... — each moved by ONE
+    copy launch: a launch's ramp and tail are paid log2(K) times instead of K times, and the first
+    bucket still reaches its collective after one bucket's copy.  ``small_last``: the mirror image
+    (…, 4, 2, 1, 1), for the unpack after the all-gathers, so only the last bucket's copy is exposed
+    after the last gather."""
+    sizes, left, size = [], K, 1
+    while left > 0:
+        sizes.append(min(size, left))
+        left -= sizes[-1]
+        if len(sizes) > 1:
+            size *= 2
+    if small_last:
+        sizes = sizes[::-1]
+    out, k = [], 0
+    for n in sizes:
+        out.append(list(range(k, k + n)))
+        k += n
+    return out
+
+
 PROBE_MIN_BYTES = 1 << 30
 # An in-place stream over an allocation in MI355X's fast VRAM region runs at ~6.2-6.3 TB/s (the
 # guide's float4 copy: 6.29); in the slow regions at ~5.2 (profiles/r02_alloc/).  A candidate at or
 # above this is kept at once, without allocating the remaining ones.
 PROBE_ACCEPT_GBS = 5950.0
+
+
+def _stream_gbs(buf: torch.Tensor, stream) -> float:
+    """In-place streaming GB/s of ``buf`` (read + write of every byte, gfx950 copy kernel; one warm
+    pass first, which also touches every page)."""
+    nbytes = buf.numel() * buf.element_size()
+    probe = CopySet([buf.data_ptr()], [buf.data_ptr()], [nbytes])  # unchanged contents
+    probe.run(stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    probe.run(stream)
+    e1.record(stream)
+    e1.synchronize()
+    return 2 * nbytes / (e0.elapsed_time(e1) / 1e3) / 1e9
 
 
 def probed_zeros(n: int, dtype, device, tries: int = 8, accept_gbs: float = PROBE_ACCEPT_GBS):
@@ -63,11 +98,14 @@ def probed_zeros(n: int, dtype, device, tries: int = 8, accept_gbs: float = PROB
     alloc_pos8.jsonl); the same launch re-measured later, or after 3 s of warm streaming, keeps its
     speed (alloc_tlb2.jsonl: not a clock effect), and the fast buffers do not translate better
     (they see MORE UTCL1 misses; identical DRAM request counts — pmc_pass*.json).  So for buffers
-    of 1 GiB or more, candidates are allocated (each while the previous ones are still held, so
-    each is new memory) and streamed once in place by the gfx950 copy kernel; the first at
-    ``accept_gbs`` or above is kept at once, otherwise the fastest of ``tries``; the rejected
-    ones are handed back to the device.  Skipped when free memory is short.
-    Returns (buffer, info dict)."""
+    of 1 GiB or more, candidates are allocated and streamed once in place by the gfx950 copy
+    kernel; the first at ``accept_gbs`` or above is kept at once, otherwise the fastest of
+    ``tries``.  At most THREE candidates are held at once (the best so far, the newest, and the
+    last rejected one, so the next allocation cannot be handed the memory just rejected): peak
+    transient memory is 3x the buffer.  Rejected candidates go back to the device.  Skipped when
+    free memory is short — then the single plain allocation is still measured.
+    Returns (buffer, info dict): ``gbs`` every candidate's GB/s in allocation order,
+    ``unprobed_gbs`` the first (what a plain allocation would have given), ``chosen``."""
     nbytes = n * torch.empty((), dtype=dtype).element_size()
     info = {"tries": 1, "gbs": []}
     env = os.environ.get("ZERO_AMD_PROBE_TRIES")  # diagnostics: 1 = plain allocation
@@ -76,37 +114,45 @@ def probed_zeros(n: int, dtype, device, tries: int = 8, accept_gbs: float = PROB
     env = os.environ.get("ZERO_AMD_PROBE_ACCEPT_GBS")  # diagnostics: the acceptance threshold
     if env:
         accept_gbs = float(env)
-    if tries <= 1 or nbytes < PROBE_MIN_BYTES:
-        return torch.zeros(n, dtype=dtype, device=device), info
-    free, total = torch.cuda.mem_get_info(device)
-    # candidates are held together: keep a quarter of the device (and 2 GiB) out of it
-    tries = int(min(tries, max(1, (free - max(total // 4, 2 << 30)) // nbytes)))
-    if tries <= 1:
+    if nbytes < PROBE_MIN_BYTES:
         return torch.zeros(n, dtype=dtype, device=device), info
     stream = torch.cuda.current_stream(device)
-    cands = []
-    for _ in range(tries):
+    free, total = torch.cuda.mem_get_info(device)
+    # three candidates are held at once: keep a quarter of the device (and 2 GiB) out of it
+    room = (free - max(total // 4, 2 << 30)) // nbytes
+    if tries <= 1 or room < 3:
         buf = torch.zeros(n, dtype=dtype, device=device)
-        probe = CopySet([buf.data_ptr()], [buf.data_ptr()], [nbytes])  # read + write, unchanged
-        probe.run(stream)  # warm (first touch)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        probe.run(stream)
-        e1.record(stream)
-        e1.synchronize()
-        gbs = 2 * nbytes / (e0.elapsed_time(e1) / 1e3) / 1e9
-        cands.append((gbs, buf))
-        info["gbs"].append(round(gbs, 1))
-        if gbs >= accept_gbs:
+        g = round(_stream_gbs(buf, stream), 1)
+        info.update(gbs=[g], unprobed_gbs=g, chosen=0,
+                    probe="off" if tries <= 1 else "skipped: free memory short")
+        return buf, info
+    best = newest_rejected = None
+    for k in range(tries):
+        buf = torch.zeros(n, dtype=dtype, device=device)
+        g = _stream_gbs(buf, stream)
+        info["gbs"].append(round(g, 1))
+        if best is None or g > best[0]:
+            rejected, best = best, (g, k, buf)
+        else:
+            rejected = (g, k, buf)
+        del buf
+        if newest_rejected is not None and rejected is not None:
+            # release the older blocker to the device, not to torch's cache (which would hand the
+            # same block straight back as the next candidate)
+            newest_rejected = None
+            torch.cuda.empty_cache()
+        newest_rejected = rejected if rejected is not None else newest_rejected
+        rejected = None
+        if best[0] >= accept_gbs:
             break
-    best = max(range(len(cands)), key=lambda i: cands[i][0])
-    buf = cands[best][1]
-    del cands, probe
+    out, chosen = best[2], best[1]
+    del best, newest_rejected
     # hand the rejected candidates back to the device (not just to torch's cache), so later
     # allocations outside torch (RCCL buffers, segment tables) and mem_get_info see them
     torch.cuda.empty_cache()
-    info.update(tries=len(info["gbs"]), chosen=best, accept_gbs=accept_gbs)
-    return buf, info
+    info.update(tries=len(info["gbs"]), chosen=chosen, accept_gbs=accept_gbs,
+                unprobed_gbs=info["gbs"][0], held_max=3)
+    return out, info
 
 
 class ShardEngine:
@@ -407,15 +453,19 @@ class ShardEngine:
         cs = self.comm_stream
         self.ev_c0.record(stream)  # communication_time: step entry → last gradient reduction
         with _lib.phase_range("all_reduce_gradients"):  # zero1.py:80-84: pack + reduce-scatter
-            for k in range(self.K):  # pack every bucket on the compute stream
-                s, b = self.segs[k], self.buckets[k]
-                src = np.where(has[s.param], gptr[s.param] + s.param_off.astype(np.uint64) * es, 0)
-                dst = base + np.uint64(b.arena_off) * es + s.buf_off.astype(np.uint64) * es
-                nb = s.length * self.es
+            for gi, grp in enumerate(launch_groups(self.K)):  # pack on the compute stream
+                src, dst, nb = [], [], []
+                for k in grp:
+                    s, b = self.segs[k], self.buckets[k]
+                    src.append(np.where(has[s.param], gptr[s.param] + s.param_off.astype(np.uint64) * es, 0))
+                    dst.append(base + np.uint64(b.arena_off) * es + s.buf_off.astype(np.uint64) * es)
+                    nb.append(s.length * self.es)
+                src, dst, nb = np.concatenate(src), np.concatenate(dst), np.concatenate(nb)
                 sig = src.tobytes() + dst.tobytes()
-                pack = self._cached(("pack", k), sig, lambda: CopySet(src, dst, nb))
+                pack = self._cached(("pack", gi), sig, lambda: CopySet(src, dst, nb))
                 self._run_copy("pack", pack, stream)
-                self.ev_pack[k].record(stream)
+                for k in grp:
+                    self.ev_pack[k].record(stream)
             for k in range(self.K):  # in-place reduce-scatter (-v) of each bucket
                 cs.wait_event(self.ev_pack[k])
                 self._collective(k, "rs")
@@ -450,13 +500,19 @@ class ShardEngine:
                 cs.wait_event(self.ev_adam[k])
                 self._collective(k, "ag")
                 self.ev_ag[k].record(cs)
-            for k in range(self.K):  # scatter every bucket back into module storage
-                stream.wait_event(self.ev_ag[k])
-                s, b = self.segs[k], self.buckets[k]
-                src = base + np.uint64(b.arena_off) * es + s.buf_off.astype(np.uint64) * es
-                dst = pptr[s.param] + s.param_off.astype(np.uint64) * es
-                unpack = self._cached(("unpack", k), dst.tobytes(),
-                                      lambda: CopySet(src, dst, s.length * self.es))
+            # scatter the buckets back into module storage, a group per launch as their gathers
+            # complete (gathers run in order on the comm stream: the group's last one suffices)
+            for gi, grp in enumerate(launch_groups(self.K, small_last=True)):
+                stream.wait_event(self.ev_ag[grp[-1]])
+                src, dst, nb = [], [], []
+                for k in grp:
+                    s, b = self.segs[k], self.buckets[k]
+                    src.append(base + np.uint64(b.arena_off) * es + s.buf_off.astype(np.uint64) * es)
+                    dst.append(pptr[s.param] + s.param_off.astype(np.uint64) * es)
+                    nb.append(s.length * self.es)
+                src, dst, nb = np.concatenate(src), np.concatenate(dst), np.concatenate(nb)
+                unpack = self._cached(("unpack", gi), src.tobytes() + dst.tobytes(),
+                                      lambda: CopySet(src, dst, nb))
                 self._run_copy("unpack", unpack, stream)
 
     # ------------------------------------------------------------------------------------------

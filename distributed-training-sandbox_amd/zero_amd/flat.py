@@ -132,6 +132,9 @@ class FlatEngine(ShardEngine):
         self.touched = np.zeros(n, bool)
         self.any_touched = False
         self._mark_hooks = []
+        # parameters carrying this engine's post-accumulate-grad hook; requires_grad can change
+        # after construction (gradual unfreezing), so the set is refreshed (_refresh_requires_grad)
+        self.hooked = np.zeros(n, bool)
         self.overlap = False  # backward-overlapped reduces (enable_overlap)
         self.ov_K = 0
         self.launched_in_backward = 0
@@ -266,12 +269,25 @@ class FlatEngine(ShardEngine):
 
     def register_marks(self):
         """Post-accumulate-grad hooks that only record which parameters backward reached."""
-        def mark(i):
-            self.touched[i] = True
-            self.any_touched = True
-        self._mark_hooks = [p.register_post_accumulate_grad_hook(lambda _p, i=i: mark(i))
-                            for i, p in enumerate(self.params) if p.requires_grad]
+        self._mark_hooks = []
+        self._hook_new(self._requires_grad())
         return self._mark_hooks
+
+    def _mark(self, i: int):
+        self.touched[i] = True
+        self.any_touched = True
+
+    def _requires_grad(self) -> np.ndarray:
+        return np.fromiter((p.requires_grad for p in self.params), bool, len(self.params))
+
+    def _hook_new(self, req: np.ndarray):
+        """Hook every parameter that requires grad and has no hook of this engine yet."""
+        fn = self._ov_ready if self.overlap else self._mark
+        for i in np.nonzero(req & ~self.hooked)[0]:
+            i = int(i)
+            self._mark_hooks.append(self.params[i].register_post_accumulate_grad_hook(
+                lambda _p, i=i: fn(i)))
+            self.hooked[i] = True
 
     # ------------------------------------------------------------------------------------------
     # Backward overlap (SURVEY.md §8(f) 1) on the flat arena
@@ -298,9 +314,10 @@ class FlatEngine(ShardEngine):
         self.ov_bucket_of = np.zeros(n, np.int64)
         for k, g in enumerate(groups):
             self.ov_bucket_of[g] = k
-        # only parameters that can receive a gradient are waited for (a frozen one never fires)
-        req = np.array([p.requires_grad for p in self.params], bool)
-        self.ov_size = np.array([int(req[g].sum()) for g in groups], np.int64)
+        # only parameters that can receive a gradient are waited for (a frozen one never fires);
+        # re-counted at the first hook of a backward if requires_grad changed since
+        self.ov_req = self._requires_grad()
+        self.ov_size = np.array([int(self.ov_req[g].sum()) for g in groups], np.int64)
         self.ov_ev = [torch.cuda.Event() for _ in range(self.ov_K)]
         own = np.nonzero(self.ov_owner == self.rank)[0]
         self.ov_last_own = int(own[-1]) if len(own) else -1
@@ -309,16 +326,40 @@ class FlatEngine(ShardEngine):
         return self
 
     def register_hooks(self):
-        return [p.register_post_accumulate_grad_hook(lambda _p, i=i: self._ov_ready(i))
-                for i, p in enumerate(self.params) if p.requires_grad]
+        self._mark_hooks = []
+        self._hook_new(self.ov_req)
+        return self._mark_hooks
 
     def _ov_reset(self):
         self.ov_pending = self.ov_size.copy()
         self.ov_marked = np.zeros(len(self.params), bool)
         self.ov_next = 0
         self.ov_launched = 0
+        self.ov_first = True
+
+    def _ov_refresh(self):
+        """First hook of a backward: if requires_grad changed since the buckets were counted, hook
+        the newly trainable parameters and re-count what each bucket waits for — before any
+        bucket of this backward is launched.  A newly frozen parameter's bucket no longer waits
+        for it; a newly trainable one whose gradient was accumulated before this first hook is
+        counted but never fires, so its bucket is reduced at step() (correct, not overlapped)."""
+        req = self._requires_grad()
+        if (req == self.ov_req).all():
+            return
+        new = req & ~self.hooked
+        self._hook_new(req)
+        # a newly trainable parameter may have been accumulated before its hook existed: it
+        # counts as reached this backward (its view holds whatever backward put there)
+        self.touched |= new
+        self.any_touched = True
+        self.ov_req = req
+        self.ov_size = np.array([int(req[g].sum()) for g in self.ov_groups], np.int64)
+        self.ov_pending = self.ov_size.copy()
 
     def _ov_ready(self, i: int):
+        if self.ov_first:
+            self.ov_first = False
+            self._ov_refresh()
         if self.ov_marked[i]:
             raise RuntimeError(
                 "zero_amd: gradient of parameter %d accumulated twice before step(); the "
@@ -424,8 +465,13 @@ class FlatEngine(ShardEngine):
         view = np.fromiter((g is not None and (g is vw[i] or self.is_view(i, g))
                             for i, g in enumerate(grads)), bool, n)
         has = np.fromiter((g is not None for g in grads), bool, n)
+        req = self._requires_grad()
         if self.any_touched:  # a backward ran: an arena view it did not reach carries no gradient
-            has &= ~view | self.touched
+            # (parameters without this engine's hook — trainable only since the last step — count
+            # when they require grad; they are hooked below for the next backward)
+            has &= ~view | self.touched | (~self.hooked & req)
+        if (req & ~self.hooked).any() and not self.overlap:
+            self._hook_new(req)
         if any(hparams_of(g)["amsgrad"] for g in set(self.group_of)) and self.vmax is None:
             self.ensure_vmax()
             self.rebuild_rows()

@@ -457,6 +457,12 @@ class _ChunkArena:
 class _GradReducer:
     """update mode: full-size gradients → summed chunks in the grad chunk arena, from backward.
 
+    Contract (as DDP's): every rank's backward reaches the same set of parameters.  A bucket is
+    launched from backward once all of its hooked parameters have fired on this rank; a parameter
+    one rank reaches and another does not would put that bucket's reduce-scatter at different
+    points among the ranks' collectives (and leave ``had_grad`` rank-dependent).  Parameters that
+    no rank reaches are fine: their buckets are flushed, in the fixed order, at the end of backward.
+
     Parameters are grouped in reverse index order (the order backward produces a sequential
     model's grads) into buckets of at most ``bucket_bytes`` of full gradient.  A
     post-accumulate-grad hook marks a parameter ready; a complete bucket whose predecessors have
@@ -889,17 +895,25 @@ class ShardedOptimizer:
             if self.update:
                 self._retired.clear()
             self._collect_comm_time()
+        else:  # asynchronous steps: count the spans whose end the device has passed
+            self._collect_comm_time(completed_only=True)
         self.runtime.end_iteration()
         self.step_time += time.perf_counter() - step_start
         return loss
 
-    def _collect_comm_time(self):
+    def _collect_comm_time(self, completed_only: bool = False):
         """zero3.py:125,158: communication_time = from step() entry until the gradient reduction is
         done.  Measured on the device: step-entry event on the compute stream → event after the
-        last gradient collective on the side stream (0 when backward already finished them)."""
+        last gradient collective on the side stream (0 when backward already finished them).
+        ``completed_only`` (steps without a synchronize): only the spans the device has finished,
+        so the list stays a step or two long and the counter trails by as much."""
+        keep = []
         for e0, e1 in self._comm_spans:
+            if completed_only and not e1.query():
+                keep.append((e0, e1))
+                continue
             self.communication_time += max(0.0, e0.elapsed_time(e1) / 1e3)
-        self._comm_spans.clear()
+        self._comm_spans = keep
 
     def zero_grad(self, set_to_none: bool = True):
         self.optimizer.zero_grad(set_to_none=set_to_none)

@@ -37,3 +37,39 @@ def test_peer_link_denominators():
 
 def test_bf16_sum_tolerance_grows_with_ranks():
     assert bench._bf16_sum_tolerance(2) < bench._bf16_sum_tolerance(8) == 8 * 2.0 ** -8
+
+
+def test_copy_launch_groups_cover_buckets_in_order():
+    """Pack / unpack launch groups (zero_amd/engine.py launch_groups): every bucket exactly once,
+    in order; doubling runs (pack: the first bucket alone, unpack: the last bucket alone)."""
+    import sys
+
+    sys.path.insert(0, str(bench.REPO / "distributed-training-sandbox_amd"))
+    from zero_amd.engine import launch_groups
+
+    for K in range(1, 70):
+        for small_last in (False, True):
+            g = launch_groups(K, small_last=small_last)
+            assert [k for grp in g for k in grp] == list(range(K))
+            assert len(g) <= 2 + int(np.log2(K)) if K > 1 else len(g) == 1
+            assert len(g[-1 if small_last else 0]) == 1
+    assert [len(x) for x in launch_groups(24)] == [1, 1, 2, 4, 8, 8]
+
+
+def test_traffic_matcher_needs_equal_algorithmic_bytes(tmp_path):
+    """roofline.traffic is taken from a PMC summary only when the summary's algorithmic bytes per
+    launch are this run's: a stale measurement is reported as a note, not as traffic."""
+    import json
+
+    f = tmp_path / "x_pmc.json"
+    f.write_text(json.dumps({"config": {"workload": "C4"}, "hbm_bytes_per_launch": 100.0,
+                             "algorithmic_bytes_per_launch": 99}))
+    t, src, note = bench.match_traffic({"workload": "C4"}, 99.0, str(f))
+    assert t == 100.0 and src and note is None
+    t, src, note = bench.match_traffic({"workload": "C4"}, 120.0, str(f))
+    assert t is None and src is None and "not used" in note
+    # the committed summaries: the C4 split-master headline matches its own algorithmic bytes
+    want = {"workload": "C4", "zero": 2, "param_dtype": "bf16", "layout": "reference", "n_gpus": 1,
+            "master": "split"}
+    t, src, _ = bench.match_traffic(want, 79952564224.0)
+    assert t is not None and src.startswith("profiles/")

@@ -166,6 +166,57 @@ def test_frozen_and_unused_params(gpu):
     spawn_batch(2, [(_frozen_worker, (v, o)) for v in (1, 2) for o in (True, False)])
 
 
+def _unfreeze_worker(rank, ws, port, overlap):
+    """requires_grad changed after the optimizer was built (gradual unfreezing / freezing): a
+    parameter frozen at construction and unfrozen at step 2 is updated from then on (hooked when
+    it changes — no silent skip), one frozen at step 3 is skipped from then on, and the
+    overlapped buckets re-count what they wait for.  Against the oracle, every step."""
+    import sys
+    from conftest import PKG, REPO  # noqa: F401
+    from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
+    from _zero_run import rel
+    from oracle import zero_oracle as zo
+    from zero_amd import zero2
+
+    torch.cuda.set_device(0)
+    init_pg(rank, ws, port)
+    dev = torch.device("cuda:0")
+    shapes = [(40, 8), (40,), (24, 8), (24,), (16, 8), (16,)]
+    late, early = 2, 4  # trainable from step 2 on / frozen from step 3 on
+    g = torch.Generator().manual_seed(23)
+    init = [torch.randn(s, generator=g).numpy() for s in shapes]
+    steps = 5
+    lg = {(t, r, i): (torch.randn(s, generator=torch.Generator().manual_seed(100 * t + 10 * r + i))
+                      * 1e-2).numpy() for t in range(steps) for r in range(ws) for i, s in enumerate(shapes)}
+    skip = lambda t, i: (i == late and t < 2) or (i == early and t >= 3)  # noqa: E731
+    want = zo.simulate(2, ws, init, steps=steps,
+                       local_grads=lambda t, r, i: None if skip(t, i) else lg[(t, r, i)])
+    params = [torch.nn.Parameter(torch.from_numpy(a.copy()).to(dev), requires_grad=i != late)
+              for i, a in enumerate(init)]
+    opt = zero2.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=test_comm(),
+                                 overlap=overlap, overlap_bucket_mb=1e-3)
+    for t in range(steps):
+        if t == 2:
+            params[late].requires_grad_(True)
+        if t == 3:
+            params[early].requires_grad_(False)
+        opt.zero_grad()
+        loss = sum((p * torch.from_numpy(lg[(t, rank, i)].copy()).to(dev)).sum()
+                   for i, p in enumerate(params) if not skip(t, i))
+        loss.backward()
+        opt.step()
+        for i, p in enumerate(params):
+            assert rel(p.detach().cpu().numpy(), want["params"][t][rank][i]) <= 1e-6, (overlap, rank, t, i)
+    assert not torch.equal(params[late].detach().cpu(), torch.from_numpy(init[late]))
+    dist.barrier()
+    dist.destroy_process_group()
+    sys.stdout.flush()
+
+
+def test_requires_grad_changes_after_construction(gpu):
+    spawn_batch(2, [(_unfreeze_worker, (o,)) for o in (True, False)])
+
+
 OV_CASES = [(2, True), (3, True), (3, False), (4, True)]
 
 

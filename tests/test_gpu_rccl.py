@@ -170,12 +170,14 @@ def test_bench_share_gpu_zero3_paramset(gpu):
 
 def test_bench_share_gpu_zero3_mlp(gpu):
     """configs[2]'s hooked ZeRO-3 training iteration (the reference MLP, here C2-wide) at N = 2:
-    one real iteration through RCCL equals the unsharded plain-PyTorch iteration (bf16 params:
-    within 2^-7 of the largest element; fp32: 1e-5)."""
-    out = _bench2(["--zero", "3", "--config", "C2", "--steps", "2", "--warmup", "1"])
-    assert out["n_gpus"] == 2 and out["rehearsal"].startswith("share-gpu")
-    chk = out["exchange_check"]
-    assert chk["all_ranks_ok"] and chk["max_rel_err"] <= chk["tol"] == 2.0 ** -7
+    one real iteration through RCCL equals the unsharded plain-PyTorch iteration (fp32, the
+    reference MLP's dtype and the bench's default here: within 1e-5; bf16 params: 2^-7)."""
+    for dt, tol in (("fp32", 1e-5), ("bf16", 2.0 ** -7)):
+        out = _bench2(["--zero", "3", "--config", "C2", "--dtype", dt, "--steps", "2", "--warmup", "1"])
+        assert out["n_gpus"] == 2 and out["rehearsal"].startswith("share-gpu")
+        assert out["config"]["param_dtype"] == dt
+        chk = out["exchange_check"]
+        assert chk["all_ranks_ok"] and chk["max_rel_err"] <= chk["tol"] == tol, (dt, chk)
 
 
 @pytest.mark.parametrize("zero", [2, 3])
