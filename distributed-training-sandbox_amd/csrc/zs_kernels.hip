@@ -979,13 +979,13 @@ int zs_adamset_run(const zs_adamset* as, const zs_adam_hparams* h, uintptr_t str
 // zs_adam_step: one contiguous range through the same kernels.  Its two one-entry tables
 // (vector part + tail) are written on the caller's stream by a one-thread kernel into a
 // stream-ordered allocation, so the call neither synchronises nor keeps state between calls.
-int zs_adam_step(float* p, uint16_t* p_bf16, const void* g, int g_dtype, float* m, float* v,
-                 int64_t n, double lr, double beta1, double beta2, double eps, double weight_decay,
-                 int decoupled, int64_t step, double grad_div, float* carry, double carry_mul,
-                 uintptr_t stream) {
-  ZS_REQUIRE(n >= 0, "zs_adam_step: n < 0");
-  ZS_REQUIRE(g_dtype == ZS_F32 || g_dtype == ZS_BF16, "zs_adam_step: bad g_dtype %d", g_dtype);
-  ZS_REQUIRE(n == 0 || (p && m && v), "zs_adam_step: p, m and v must be non-NULL");
+int zs_adam_step_ex(float* p, uint16_t* p_bf16, const void* g, int g_dtype, float* m, float* v,
+                    int64_t n, double lr, double beta1, double beta2, double eps,
+                    double weight_decay, int decoupled, int64_t step, double grad_div, float* carry,
+                    double carry_mul, uintptr_t stream) {
+  ZS_REQUIRE(n >= 0, "zs_adam_step_ex: n < 0");
+  ZS_REQUIRE(g_dtype == ZS_F32 || g_dtype == ZS_BF16, "zs_adam_step_ex: bad g_dtype %d", g_dtype);
+  ZS_REQUIRE(n == 0 || (p && m && v), "zs_adam_step_ex: p, m and v must be non-NULL");
   zs_adam_hparams h;
   int rc = zs_adam_hparams_init(lr, beta1, beta2, eps, weight_decay, decoupled, 0, 0, step,
                                 grad_div, carry_mul, &h);
@@ -1036,10 +1036,26 @@ int zs_adam_step(float* p, uint16_t* p_bf16, const void* g, int g_dtype, float* 
   }
   const hipError_t ef = hipFreeAsync(d, st);  // after the launches, in stream order
   if (e != hipSuccess)
-    return zs::fail(ZS_ERR_HIP, "zs_adam_step: table kernel: %s", hipGetErrorString(e));
+    return zs::fail(ZS_ERR_HIP, "zs_adam_step_ex: table kernel: %s", hipGetErrorString(e));
   if (rc != ZS_OK) return rc;
   ZS_HIP(ef);
   return ZS_OK;
+}
+
+// SURVEY.md §8(b)'s literal signature: float scalars and grad_scale = 1/ws.  The divisor is the
+// integer nearest to 1/grad_scale when that is within float(1/ws)'s rounding (2^-24 relative) —
+// the world size, so the update divides as zero1.py:84 `p.grad /= ws` does — else 1/grad_scale;
+// the scalars are widened to double before torch's bias-correction arithmetic.  carry is read and
+// rewritten (A_{t-1} -> A_t) although the reference signature spells it const.
+int zs_adam_step(float* p, uint16_t* p_bf16, const void* g, int g_dtype, float* m, float* v,
+                 int64_t n, float lr, float b1, float b2, float eps, float wd, int decoupled,
+                 int64_t step, float grad_scale, const float* carry, float carry_scale,
+                 uintptr_t stream) {
+  ZS_REQUIRE(grad_scale > 0.0f && std::isfinite(grad_scale), "zs_adam_step: grad_scale must be > 0");
+  const double r = 1.0 / double(grad_scale), k = std::nearbyint(r);
+  const double div = (k >= 1.0 && std::fabs(r - k) <= 1e-6 * k) ? k : r;
+  return zs_adam_step_ex(p, p_bf16, g, g_dtype, m, v, n, lr, b1, b2, eps, wd, decoupled, step, div,
+                         const_cast<float*>(carry), carry_scale, stream);
 }
 
 int zs_adamset_destroy(zs_adamset* as) {

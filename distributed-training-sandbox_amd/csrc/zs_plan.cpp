@@ -191,33 +191,33 @@ static void plan_buckets(zs_plan* p) {
 
 extern "C" {
 
-int zs_plan_create(int64_t n_params, const int64_t* numels, const int64_t* dim0, int ws, int rank,
-                   int layout, int64_t align_elems, int64_t window_elems, int bucket_mode,
-                   zs_plan** out) {
-  ZS_REQUIRE(out != nullptr, "zs_plan_create: out is NULL");
+int zs_plan_create_ex(int64_t n_params, const int64_t* numels, const int64_t* dim0, int ws,
+                      int rank, int layout, int64_t align_elems, int64_t window_elems,
+                      int bucket_mode, zs_plan** out) {
+  ZS_REQUIRE(out != nullptr, "zs_plan_create_ex: out is NULL");
   *out = nullptr;
-  ZS_REQUIRE(n_params >= 0, "zs_plan_create: n_params < 0");
-  ZS_REQUIRE(n_params == 0 || numels != nullptr, "zs_plan_create: numels is NULL");
-  ZS_REQUIRE(ws >= 1, "zs_plan_create: ws must be >= 1 (got %d)", ws);
-  ZS_REQUIRE(rank >= 0 && rank < ws, "zs_plan_create: rank %d out of [0,%d)", rank, ws);
+  ZS_REQUIRE(n_params >= 0, "zs_plan_create_ex: n_params < 0");
+  ZS_REQUIRE(n_params == 0 || numels != nullptr, "zs_plan_create_ex: numels is NULL");
+  ZS_REQUIRE(ws >= 1, "zs_plan_create_ex: ws must be >= 1 (got %d)", ws);
+  ZS_REQUIRE(rank >= 0 && rank < ws, "zs_plan_create_ex: rank %d out of [0,%d)", rank, ws);
   ZS_REQUIRE(layout == ZS_LAYOUT_R || layout == ZS_LAYOUT_Z || layout == ZS_LAYOUT_F,
-             "zs_plan_create: unknown layout %d", layout);
-  ZS_REQUIRE(align_elems >= 1, "zs_plan_create: align_elems must be >= 1");
-  ZS_REQUIRE(window_elems >= 0, "zs_plan_create: window_elems < 0");
+             "zs_plan_create_ex: unknown layout %d", layout);
+  ZS_REQUIRE(align_elems >= 1, "zs_plan_create_ex: align_elems must be >= 1");
+  ZS_REQUIRE(window_elems >= 0, "zs_plan_create_ex: window_elems < 0");
   ZS_REQUIRE(bucket_mode == ZS_BUCKETS_RAGGED || bucket_mode == ZS_BUCKETS_PADDED,
-             "zs_plan_create: unknown bucket_mode %d", bucket_mode);
-  ZS_REQUIRE(layout != ZS_LAYOUT_Z || dim0 != nullptr, "zs_plan_create: layout Z needs dim0");
+             "zs_plan_create_ex: unknown bucket_mode %d", bucket_mode);
+  ZS_REQUIRE(layout != ZS_LAYOUT_Z || dim0 != nullptr, "zs_plan_create_ex: layout Z needs dim0");
   for (int64_t i = 0; i < n_params; ++i) {
-    ZS_REQUIRE(numels[i] >= 0, "zs_plan_create: numel[%lld] < 0", (long long)i);
+    ZS_REQUIRE(numels[i] >= 0, "zs_plan_create_ex: numel[%lld] < 0", (long long)i);
     if (layout == ZS_LAYOUT_Z) {
       ZS_REQUIRE((dim0[i] == 0 && numels[i] == 0) || (dim0[i] >= 1 && numels[i] % dim0[i] == 0),
-                 "zs_plan_create: param %lld numel %lld not divisible by dim0 %lld", (long long)i,
+                 "zs_plan_create_ex: param %lld numel %lld not divisible by dim0 %lld", (long long)i,
                  (long long)numels[i], (long long)dim0[i]);
     }
   }
 
   zs_plan* p = new (std::nothrow) zs_plan();
-  if (!p) return zs::fail(ZS_ERR_NOMEM, "zs_plan_create: out of memory");
+  if (!p) return zs::fail(ZS_ERR_NOMEM, "zs_plan_create_ex: out of memory");
   p->n = n_params;
   p->ws = ws;
   p->rank = rank;
@@ -282,6 +282,20 @@ int zs_plan_create(int64_t n_params, const int64_t* numels, const int64_t* dim0,
   if (W > 0) plan_buckets(p);
   *out = p;
   return ZS_OK;
+}
+
+// SURVEY.md §8(b)'s literal signature: the bucket size in bytes of fp32 elements (a bf16 bucket of
+// the same plan holds the same elements in half the bytes), 64-element alignment, ragged buckets.
+int zs_plan_create(int64_t n_params, const int64_t* numels, const int64_t* dim0, int ws, int rank,
+                   int layout, int64_t bucket_bytes, zs_plan** out) {
+  ZS_REQUIRE(bucket_bytes >= 0, "zs_plan_create: bucket_bytes < 0");
+  ZS_REQUIRE(ws >= 1, "zs_plan_create: ws must be >= 1 (got %d)", ws);
+  constexpr int64_t kAlign = 64;
+  int64_t window = 0;
+  if (bucket_bytes > 0 && ws > 1)
+    window = std::max<int64_t>(kAlign, bucket_bytes / (int64_t(ws) * 4) / kAlign * kAlign);
+  return zs_plan_create_ex(n_params, numels, dim0, ws, rank, layout, kAlign, window,
+                           ZS_BUCKETS_RAGGED, out);
 }
 
 int zs_plan_destroy(zs_plan* plan) {

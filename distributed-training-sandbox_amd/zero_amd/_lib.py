@@ -20,20 +20,20 @@ ZS_OK, ZS_ERR_INVALID, ZS_ERR_HIP, ZS_ERR_RCCL, ZS_ERR_NOMEM = 0, 1, 2, 3, 4
 ZS_F32, ZS_BF16, ZS_U8, ZS_BF16_SPLIT = 0, 1, 2, 3
 ZS_LAYOUT_R, ZS_LAYOUT_Z, ZS_LAYOUT_F = 0, 1, 2
 ZS_BUCKETS_RAGGED, ZS_BUCKETS_PADDED = 0, 1
-ABI_VERSION = 6
+ABI_VERSION = 7
 ZS_UNIQUE_ID_BYTES = 128
 
 # Every symbol include/zero_amd.h declares (tests check the library exports all of them).
 EXPORTED = (
     "zs_abi_version", "zs_last_error", "zs_range_push", "zs_range_pop",
-    "zs_plan_create", "zs_plan_destroy", "zs_plan_info", "zs_plan_owner_range", "zs_plan_owner_of",
+    "zs_plan_create", "zs_plan_create_ex", "zs_plan_destroy", "zs_plan_info", "zs_plan_owner_range", "zs_plan_owner_of",
     "zs_plan_stream_len", "zs_plan_num_pieces", "zs_plan_pieces", "zs_plan_bucket",
     "zs_plan_num_segments", "zs_plan_segments", "zs_plan_num_buckets", "zs_plan_bucket_bytes",
     "zs_pack", "zs_unpack",
     "zs_copyset_create", "zs_copyset_run", "zs_copyset_destroy", "zs_scale",
     "zs_convert", "zs_fp8_quantize_rows", "zs_fp8_dequantize_rows",
     "zs_adam_hparams_init", "zs_adamset_create", "zs_adamset_run", "zs_adamset_destroy",
-    "zs_adamset_stats", "zs_adam_step",
+    "zs_adamset_stats", "zs_adam_step", "zs_adam_step_ex",
     "zs_comm_unique_id", "zs_comm_init", "zs_comm_destroy", "zs_reduce_scatter", "zs_all_gather",
     "zs_all_reduce", "zs_reduce", "zs_broadcast", "zs_reduce_group", "zs_broadcast_group", "zs_all_gather_group", "zs_reduce_scatter_group", "zs_group_start", "zs_group_end", "zs_rccl_version",
 )
@@ -74,8 +74,10 @@ _SIGS = {
     "zs_last_error": ([], ctypes.c_char_p),
     "zs_range_push": ([ctypes.c_char_p], ctypes.c_int),
     "zs_range_pop": ([], ctypes.c_int),
-    "zs_plan_create": ([_I64, _PI64, _PI64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _I64, _I64,
-                        ctypes.c_int, ctypes.POINTER(_P)], ctypes.c_int),
+    "zs_plan_create": ([_I64, _PI64, _PI64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _I64,
+                        ctypes.POINTER(_P)], ctypes.c_int),
+    "zs_plan_create_ex": ([_I64, _PI64, _PI64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _I64, _I64,
+                           ctypes.c_int, ctypes.POINTER(_P)], ctypes.c_int),
     "zs_plan_destroy": ([_P], ctypes.c_int),
     "zs_plan_info": ([_P, _PI64], ctypes.c_int),
     "zs_plan_owner_range": ([_P, ctypes.c_int, _PI64, _PI64], ctypes.c_int),
@@ -106,8 +108,10 @@ _SIGS = {
     "zs_adamset_run": ([_P, ctypes.POINTER(AdamHParams), _U], ctypes.c_int),
     "zs_adamset_destroy": ([_P], ctypes.c_int),
     "zs_adamset_stats": ([_P, _PI64, _PI64], ctypes.c_int),
-    "zs_adam_step": ([_P, _P, _P, ctypes.c_int, _P, _P, _I64] + [ctypes.c_double] * 5 +
-                     [ctypes.c_int, _I64, ctypes.c_double, _P, ctypes.c_double, _U], ctypes.c_int),
+    "zs_adam_step": ([_P, _P, _P, ctypes.c_int, _P, _P, _I64] + [ctypes.c_float] * 5 +
+                     [ctypes.c_int, _I64, ctypes.c_float, _P, ctypes.c_float, _U], ctypes.c_int),
+    "zs_adam_step_ex": ([_P, _P, _P, ctypes.c_int, _P, _P, _I64] + [ctypes.c_double] * 5 +
+                        [ctypes.c_int, _I64, ctypes.c_double, _P, ctypes.c_double, _U], ctypes.c_int),
     "zs_comm_unique_id": ([_P], ctypes.c_int),
     "zs_comm_init": ([_P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)], ctypes.c_int),
     "zs_comm_destroy": ([_P], ctypes.c_int),

@@ -2,7 +2,7 @@
 
 ``CopySet``  — one launch of the descriptor-driven gather/scatter copy (pack / unpack).
 ``AdamSet``  — one launch of the fused Adam/AdamW update over a list of segments.
-``adam_step`` — the same update over one contiguous range (zs_adam_step; no table to keep).
+``adam_step`` — the same update over one contiguous range (zs_adam_step_ex; no table to keep).
 
 Both upload their segment table once; ``run(stream)`` only enqueues a kernel on ``stream``.
 They raise ``ZeroAmdError`` on any failure; there is no CPU path.
@@ -112,7 +112,7 @@ def adam_step(p, g, m, v, *, step, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, we
     g_dtype = _lib.ZS_BF16 if g is not None and g.dtype == torch.bfloat16 else _lib.ZS_F32
     ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
     st = torch.cuda.current_stream(p.device) if stream is None else stream
-    _lib.call("zs_adam_step", ptr(p), ptr(p_bf16), ptr(g), g_dtype, ptr(m), ptr(v), n, float(lr),
+    _lib.call("zs_adam_step_ex", ptr(p), ptr(p_bf16), ptr(g), g_dtype, ptr(m), ptr(v), n, float(lr),
               float(beta1), float(beta2), float(eps), float(weight_decay), int(bool(decoupled)),
               int(step), float(grad_div), ptr(carry), float(carry_mul), stream_handle(st))
 

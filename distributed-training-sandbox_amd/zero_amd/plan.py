@@ -64,7 +64,7 @@ class Plan:
             d0 = np.ascontiguousarray(np.asarray(dim0, dtype=np.int64))
             assert d0.shape == numels.shape
         h = ctypes.c_void_p()
-        _lib.call("zs_plan_create", len(numels), _i64p(numels) if len(numels) else None,
+        _lib.call("zs_plan_create_ex", len(numels), _i64p(numels) if len(numels) else None,
                   _i64p(d0) if d0 is not None else None, int(ws), int(rank), self.layout,
                   int(align_elems), int(window_elems), BUCKET_MODES[buckets], ctypes.byref(h))
         self._h = h

@@ -90,6 +90,16 @@ class _GatherRuntime:
         self.n_prefetch_hits = 0
         self.gather_events = None  # optional list of (start, end, bus_bytes) per gather group
         self._tables = {}          # key -> grouped all-gather pointer table (see _table)
+        # key -> (ready, done) events, re-recorded every iteration: a wait enqueued on an event
+        # keeps the record it saw, and a key's next launch comes after its materialise has
+        # enqueued that wait (creating two HIP events per gather cost host time every iteration)
+        self._events = {}
+
+    def _key_events(self, key):
+        ev = self._events.get(key)
+        if ev is None:
+            ev = self._events[key] = (torch.cuda.Event(), torch.cuda.Event())
+        return ev
 
     def launch(self, key, managers):
         """Enqueue the all-gather of ``managers`` on the side stream; returns immediately."""
@@ -100,7 +110,7 @@ class _GatherRuntime:
             self.pending[key] = ([(m, m._gather_prepare(None)[1]) for m in managers], None, None)
             self.n_gathers += 1
             return
-        ev_ready = torch.cuda.Event()
+        ev_ready, ev = self._key_events(key)
         ev_ready.record(torch.cuda.current_stream(self.device))  # shards may just have been updated
         timed = self.gather_events is not None and self.ws > 1
         plan = self._table(key, managers)
@@ -113,11 +123,13 @@ class _GatherRuntime:
             if plan is not None:
                 # one allocation for the module's full tensors and ONE library call for its RCCL
                 # group of all-gathers (zero-copy from the chunk-arena slots)
-                send, count, offs, total, dt, es, spans = plan
+                send, count, offs, total, dt, es, views = plan
                 hold = torch.empty(total, dtype=managers[0].shard.dtype, device=self.device)
-                recv = np.uint64(hold.data_ptr()) + offs * np.uint64(es)
+                recv = offs + np.uint64(hold.data_ptr())
                 self.comm.all_gather_group(send, recv, count, dt, self.stream)
-                out = [(m, hold[o:o + n]) for m, (o, n) in zip(managers, spans)]
+                # each manager's full tensor: one strided view of the allocation (no slice + view)
+                out = [(m, hold.as_strided(shape, stride, off)) for m, (shape, stride, off)
+                       in zip(managers, views)]
             else:
                 # kernels (fp8 quantisation) before the RCCL group, dequantisation after: an RCCL
                 # group only launches its collectives at group end; every buffer a collective of
@@ -127,7 +139,6 @@ class _GatherRuntime:
                     for m, st in zip(managers, states):
                         m._gather_issue(self.comm, self.stream, st)
                 out = [(m, m._gather_finish(self.stream, st)) for m, st in zip(managers, states)]
-            ev = torch.cuda.Event()
             ev.record(self.stream)
             if timed:  # ring all-gather bus bytes: (ws-1)/ws of the gathered tensor, per rank
                 bus = sum(m.gather_bytes() for m in managers) * (self.ws - 1)
@@ -153,10 +164,18 @@ class _GatherRuntime:
                 o += -(-n // ALIGN_ELEMS) * ALIGN_ELEMS  # every full tensor 64-element aligned
             from .comm import zs_dtype
 
+            views = []
+            for off, m in zip(offs, managers):
+                shape = tuple(m.full_shape)
+                stride, acc = [], 1
+                for d in reversed(shape):
+                    stride.append(acc)
+                    acc *= d
+                views.append((shape, tuple(reversed(stride)), off))
             plan = (np.array([m.send_slot.data_ptr() for m in managers], np.uint64),
-                    np.array([m.S for m in managers], np.int64), np.array(offs, np.uint64),
-                    max(o, 1), zs_dtype(managers[0].shard.dtype), es,
-                    [(off, m.numel) for off, m in zip(offs, managers)])
+                    np.array([m.S for m in managers], np.int64),
+                    np.array(offs, np.uint64) * np.uint64(es), max(o, 1),
+                    zs_dtype(managers[0].shard.dtype), es, views)
         self._tables[key] = plan
         return plan
 
@@ -184,11 +203,14 @@ class _GatherRuntime:
             return
         cur = torch.cuda.current_stream(self.device)
         cur.wait_event(ev)
-        if hold is not None:  # one allocation behind all of the module's full tensors
-            hold.record_stream(cur)
+        if hold is not None:  # one allocation behind all of the module's full tensors, whose
+            hold.record_stream(cur)  # views already have the full shapes
+            for m, full in out:
+                m.full_data = full
+                m.param.data = full
+            return
         for m, full in out:
-            if hold is None:
-                full.record_stream(cur)
+            full.record_stream(cur)
             m._install_full(full)
 
     def end_iteration(self):
@@ -494,6 +516,7 @@ class _GradReducer:
             self.bucket_of[g] = k
         self._size = np.array([len(g) for g in groups], np.int64)
         self.ev_done = [torch.cuda.Event() for _ in range(self.K)]
+        self.ev_ready = [torch.cuda.Event() for _ in range(self.K)]
         self.timing = None  # optional list of (start, end, bus_bytes) per launched bucket
         self._rs_tables = {}
         self.reset()
@@ -608,7 +631,7 @@ class _GradReducer:
                     send = torch.zeros(ws * S, dtype=wdt, device=dev)
                     send[:N].copy_(flat)
             sends.append((i, send))
-        ready = torch.cuda.Event()
+        ready = self.ev_ready[k]
         ready.record(cur)
         cs = opt.runtime.stream
         cs.wait_event(ready)

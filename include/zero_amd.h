@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ZS_ABI_VERSION 6
+#define ZS_ABI_VERSION 7
 
 enum zs_status {
   ZS_OK = 0,
@@ -72,12 +72,18 @@ typedef struct zs_plan zs_plan;
 
 /* Replaces ShardedOptimizer.__init__'s ownership computation (zero1.py:44-62, zero2.py:39-58,
  * zero3.py:82-110).  numels[i] = params[i].numel(); dim0[i] = params[i].shape[0] (1 for 0-d;
- * only read for ZS_LAYOUT_Z, may be NULL otherwise).  align_elems: every piece starts at a
- * multiple of this in its rank's stream (>=1).  window_elems: per-rank elements per bucket
- * (0 = one bucket holding the whole longest stream).  bucket_mode: ZS_BUCKETS_*. */
+ * only read for ZS_LAYOUT_Z, may be NULL otherwise).  SURVEY.md §8(b)'s signature: bucket_bytes
+ * is the size of one bucket buffer in fp32 elements' bytes (a bf16 bucket of the same plan holds
+ * the same elements in half the bytes; 0 = one bucket holding the whole longest stream); pieces
+ * are 64-element aligned; ragged buckets (ZS_BUCKETS_RAGGED). */
 int zs_plan_create(int64_t n_params, const int64_t* numels, const int64_t* dim0, int ws, int rank,
-                   int layout, int64_t align_elems, int64_t window_elems, int bucket_mode,
-                   zs_plan** out);
+                   int layout, int64_t bucket_bytes, zs_plan** out);
+/* The general form the Python engine uses: align_elems: every piece starts at a multiple of this
+ * in its rank's stream (>=1).  window_elems: per-rank elements per bucket (0 = one bucket holding
+ * the whole longest stream).  bucket_mode: ZS_BUCKETS_*. */
+int zs_plan_create_ex(int64_t n_params, const int64_t* numels, const int64_t* dim0, int ws,
+                      int rank, int layout, int64_t align_elems, int64_t window_elems,
+                      int bucket_mode, zs_plan** out);
 int zs_plan_destroy(zs_plan* plan);
 
 /* info[0..9] = {n_params, ws, rank, layout, window_elems W, num_buckets K, max_stream_len M,
@@ -229,20 +235,28 @@ int zs_adamset_destroy(zs_adamset* as);
 /* total elements covered by the set and algorithmic HBM bytes one run moves */
 int zs_adamset_stats(const zs_adamset* as, int64_t* elems, int64_t* bytes);
 
-/* Single-range form (SURVEY.md §8(b) `zs_adam_step`): one torch.optim.Adam/AdamW step over n
+/* Single-range form, SURVEY.md §8(b)'s signature: one torch.optim.Adam/AdamW step over n
  * contiguous elements — the update of one flat shard (zero1.py:88 on a flattened group) with no
  * table to build.  p: fp32 master/param, updated in place; p_bf16: optional bf16 copy of the
  * result (NULL = none); g: reduced gradient sum (g_dtype ZS_F32 or ZS_BF16; NULL = zero); m, v:
- * fp32 exp_avg / exp_avg_sq, in place; carry: ZeRO-1's A_{t-1}, rewritten with A_t (NULL = none).
- * The scalars are doubles because torch derives them from Python floats (adam.py:508-515); the
- * gradient is DIVIDED by grad_div (the world size), as zero1.py:84 `p.grad /= ws` does — for a
- * non-power-of-two ws that is not the same as multiplying by 1/ws.  Same kernels and bits as
- * zs_adamset_run; amsgrad / maximize / the split master need an adamset.  Asynchronous on
- * `stream`; its two-entry table is a stream-ordered allocation freed in stream order. */
+ * fp32 exp_avg / exp_avg_sq, in place; carry: ZeRO-1's A_{t-1}, READ AND REWRITTEN with A_t
+ * (NULL = none) although spelled const here; carry_scale: ws-1.  grad_scale = 1/ws: the update
+ * divides by the float nearest to 1/grad_scale (the world size), as zero1.py:84 `p.grad /= ws`.
+ * The float scalars are widened to double before torch's bias-correction arithmetic; torch
+ * derives them from Python doubles (adam.py:508-515), so for torch's bits with hyper-parameters
+ * not exactly representable in fp32 (lr=1e-3, betas 0.9 / 0.999) use zs_adam_step_ex.  Same
+ * kernels as zs_adamset_run; amsgrad / maximize / the split master need an adamset.
+ * Asynchronous on `stream`; its two-entry table is a stream-ordered allocation. */
 int zs_adam_step(float* p, uint16_t* p_bf16, const void* g, int g_dtype, float* m, float* v,
-                 int64_t n, double lr, double beta1, double beta2, double eps, double weight_decay,
-                 int decoupled, int64_t step, double grad_div, float* carry, double carry_mul,
+                 int64_t n, float lr, float b1, float b2, float eps, float wd, int decoupled,
+                 int64_t step, float grad_scale, const float* carry, float carry_scale,
                  uintptr_t stream);
+/* The same with torch's double scalars and the divisor itself (grad_div = ws; for a
+ * non-power-of-two ws dividing is not multiplying by 1/ws): bit-exact with torch's arithmetic. */
+int zs_adam_step_ex(float* p, uint16_t* p_bf16, const void* g, int g_dtype, float* m, float* v,
+                    int64_t n, double lr, double beta1, double beta2, double eps,
+                    double weight_decay, int decoupled, int64_t step, double grad_div, float* carry,
+                    double carry_mul, uintptr_t stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* RCCL over xGMI.  Replaces the per-tensor dist.all_reduce (zero1.py:83, zero3.py:146),        */

@@ -21,8 +21,14 @@ int main(void) {
   int64_t numels[12];
   for (int i = 0; i < 12; ++i) numels[i] = (i % 2 == 0) ? 64 * 64 : 64;
   zs_plan* plan = NULL;
-  CHECK(zs_plan_create(12, numels, NULL, 8, 3, ZS_LAYOUT_R, 64, 256, ZS_BUCKETS_RAGGED, &plan) ==
+  CHECK(zs_plan_create_ex(12, numels, NULL, 8, 3, ZS_LAYOUT_R, 64, 256, ZS_BUCKETS_RAGGED, &plan) ==
         ZS_OK);
+  /* SURVEY.md §8(b)'s literal form: 64 KiB buckets (fp32 bytes) over 8 ranks */
+  zs_plan* lit = NULL;
+  CHECK(zs_plan_create(12, numels, NULL, 8, 3, ZS_LAYOUT_R, 64 << 10, &lit) == ZS_OK);
+  int64_t ls = -1, le = -1;
+  CHECK(zs_plan_owner_range(lit, 3, &ls, &le) == ZS_OK && ls == 6 && le == 8);
+  CHECK(zs_plan_destroy(lit) == ZS_OK);
   /* ws = 8, n = 12: ranges [0,2),[2,4),[4,6),[6,8),[8],[9],[10],[11] */
   int64_t s = -1, e = -1;
   CHECK(zs_plan_owner_range(plan, 3, &s, &e) == ZS_OK && s == 6 && e == 8);
@@ -47,8 +53,10 @@ int main(void) {
   /* errors come back as codes with a message, never as a crash */
   CHECK(zs_plan_bucket_bytes(plan, k, ZS_BF16, &total) == ZS_ERR_INVALID);
   CHECK(strstr(zs_last_error(), "out of range") != NULL);
-  CHECK(zs_adam_step(NULL, NULL, NULL, ZS_F32, NULL, NULL, 16, 1e-3, 0.9, 0.999, 1e-8, 0.0, 0, 1,
-                     1.0, NULL, 0.0, 0) == ZS_ERR_INVALID);
+  CHECK(zs_adam_step_ex(NULL, NULL, NULL, ZS_F32, NULL, NULL, 16, 1e-3, 0.9, 0.999, 1e-8, 0.0, 0, 1,
+                        1.0, NULL, 0.0, 0) == ZS_ERR_INVALID);
+  CHECK(zs_adam_step(NULL, NULL, NULL, ZS_F32, NULL, NULL, 16, 1e-3f, 0.9f, 0.999f, 1e-8f, 0.0f, 0, 1,
+                     0.125f, NULL, 0.0f, 0) == ZS_ERR_INVALID);
   CHECK(zs_range_push("optimizer_step") == ZS_OK && zs_range_pop() == ZS_OK);
   CHECK(zs_plan_destroy(plan) == ZS_OK);
   printf("c-abi ok: %lld buckets\n", (long long)k);

@@ -35,9 +35,9 @@ def test_library_is_gfx950_code_object():
 def test_abi_version_and_error_text():
     from zero_amd import _lib
 
-    assert _lib.lib.zs_abi_version() == _lib.ABI_VERSION == 6
+    assert _lib.lib.zs_abi_version() == _lib.ABI_VERSION == 7
     h = ctypes.c_void_p()
-    rc = _lib.lib.zs_plan_create(0, None, None, 0, 0, 0, 64, 0, 0, ctypes.byref(h))
+    rc = _lib.lib.zs_plan_create_ex(0, None, None, 0, 0, 0, 64, 0, 0, ctypes.byref(h))
     assert rc == _lib.ZS_ERR_INVALID
     assert b"ws must be >= 1" in _lib.lib.zs_last_error()
 
@@ -80,7 +80,7 @@ def test_new_entry_points_validate_arguments():
     lib = _lib.lib
     h = ctypes.c_void_p()
     numels = (ctypes.c_int64 * 2)(4, 4)
-    assert lib.zs_plan_create(2, numels, None, 2, 0, 0, 64, 0, 7, ctypes.byref(h)) == _lib.ZS_ERR_INVALID
+    assert lib.zs_plan_create_ex(2, numels, None, 2, 0, 0, 64, 0, 7, ctypes.byref(h)) == _lib.ZS_ERR_INVALID
     assert b"bucket_mode" in lib.zs_last_error()
     assert lib.zs_scale(None, 16, 9, 2.0, 0) == _lib.ZS_ERR_INVALID
     assert lib.zs_scale(None, 16, _lib.ZS_F32, 0.0, 0) == _lib.ZS_ERR_INVALID
@@ -145,15 +145,62 @@ def test_contract_entry_points_validate_without_gpu():
     assert lib.zs_pack(plan._h, 0, ptrs, None, _lib.ZS_F32, 0) == _lib.ZS_ERR_INVALID
     assert lib.zs_unpack(plan._h, 0, 4096, ptrs, _lib.ZS_F32, 0) == _lib.ZS_ERR_INVALID
     assert b"param_ptrs" in lib.zs_last_error()  # unpack has nowhere to put a NULL param
-    f = ctypes.c_double
-    args = lambda n_, gd, step: (None, None, None, gd, None, None, n_, f(1e-3), f(0.9), f(0.999),  # noqa: E731
-                                 f(1e-8), f(0.0), 0, step, f(1.0), None, f(0.0), 0)
-    assert lib.zs_adam_step(*args(-1, _lib.ZS_F32, 1)) == _lib.ZS_ERR_INVALID
-    assert lib.zs_adam_step(*args(8, _lib.ZS_U8, 1)) == _lib.ZS_ERR_INVALID
-    assert lib.zs_adam_step(*args(8, _lib.ZS_F32, 1)) == _lib.ZS_ERR_INVALID
-    assert b"non-NULL" in lib.zs_last_error()
-    assert lib.zs_adam_step(*args(0, _lib.ZS_F32, 0)) == _lib.ZS_ERR_INVALID  # step must be >= 1
-    assert lib.zs_adam_step(*args(0, _lib.ZS_BF16, 1)) == _lib.ZS_OK  # empty: nothing to launch
+    for fn, f in ((lib.zs_adam_step_ex, ctypes.c_double), (lib.zs_adam_step, ctypes.c_float)):
+        args = lambda n_, gd, step: (None, None, None, gd, None, None, n_, f(1e-3), f(0.9), f(0.999),  # noqa: E731
+                                     f(1e-8), f(0.0), 0, step, f(1.0), None, f(0.0), 0)
+        assert fn(*args(-1, _lib.ZS_F32, 1)) == _lib.ZS_ERR_INVALID
+        assert fn(*args(8, _lib.ZS_U8, 1)) == _lib.ZS_ERR_INVALID
+        assert fn(*args(8, _lib.ZS_F32, 1)) == _lib.ZS_ERR_INVALID
+        assert b"non-NULL" in lib.zs_last_error()
+        assert fn(*args(0, _lib.ZS_F32, 0)) == _lib.ZS_ERR_INVALID  # step must be >= 1
+        assert fn(*args(0, _lib.ZS_BF16, 1)) == _lib.ZS_OK  # empty: nothing to launch
+    bad = (None, None, None, _lib.ZS_F32, None, None, 0) + tuple(ctypes.c_float(x) for x in
+                                                                 (1e-3, 0.9, 0.999, 1e-8, 0.0))
+    assert lib.zs_adam_step(*bad, 0, 1, ctypes.c_float(0.0), None, ctypes.c_float(0.0), 0) == _lib.ZS_ERR_INVALID
+    assert b"grad_scale" in lib.zs_last_error()
+
+
+def test_literal_plan_create_is_the_general_form():
+    """SURVEY.md §8(b)'s zs_plan_create(…, bucket_bytes, out) = zs_plan_create_ex with 64-element
+    alignment, ragged buckets and window = bucket_bytes / (4·ws) elements (64-aligned): the same
+    ownership, pieces and buckets."""
+    from zero_amd import _lib
+    from zero_amd.plan import Plan
+
+    lib = _lib.lib
+    numels = [4096, 64, 300, 7, 100000, 5, 12288, 1]
+    arr = (ctypes.c_int64 * len(numels))(*numels)
+    for ws in (1, 2, 3, 8):
+        for rank in range(ws):
+            for bucket_bytes in (0, 4096, 1 << 16, 1 << 20):
+                h = ctypes.c_void_p()
+                assert lib.zs_plan_create(len(numels), arr, None, ws, rank, 0, bucket_bytes,
+                                          ctypes.byref(h)) == _lib.ZS_OK
+                win = 0 if (bucket_bytes == 0 or ws == 1) else max(64, bucket_bytes // (4 * ws) // 64 * 64)
+                want = Plan(numels, ws, rank, "reference", align_elems=64, window_elems=win)
+                info = (ctypes.c_int64 * 10)()
+                assert lib.zs_plan_info(h, info) == _lib.ZS_OK
+                winfo = (ctypes.c_int64 * 10)()
+                assert lib.zs_plan_info(want._h, winfo) == _lib.ZS_OK
+                assert list(info) == list(winfo), (ws, rank, bucket_bytes)
+                for r in range(ws):
+                    s, e = ctypes.c_int64(), ctypes.c_int64()
+                    assert lib.zs_plan_owner_range(h, r, ctypes.byref(s), ctypes.byref(e)) == 0
+                    assert (s.value, e.value) == tuple(want.owner_range(r))
+                lib.zs_plan_destroy(h)
+
+
+def test_literal_adam_step_divisor_is_the_world_size():
+    """zs_adam_step's grad_scale = float(1/ws) gives back the divisor ws (the integer nearest to
+    1/grad_scale, which float(1/ws)'s 2^-24 relative rounding keeps within 1e-6·ws) for every ws
+    checked here (1..4096 and the powers of two below 2^24), so the update divides as zero1.py:84
+    does — while float(1/float(1/ws)) alone is not ws for ws = 7, 13, 14, ..."""
+    import numpy as np
+
+    for ws in list(range(1, 4097)) + [2 ** k for k in range(13, 24)]:
+        r = 1.0 / float(np.float32(1.0 / ws))
+        k = round(r)
+        assert k == ws and abs(r - k) <= 1e-6 * k, ws  # the rule in zs_kernels.hip zs_adam_step
 
 
 def test_plain_c_client(tmp_path):

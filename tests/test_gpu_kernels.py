@@ -310,6 +310,50 @@ def test_adam_step_single_range_vs_oracle(gpu, case):
         assert np.array_equal(C.cpu().numpy().view(np.uint32), rc.view(np.uint32))
 
 
+@pytest.mark.parametrize("ws", [1, 3, 4, 7])
+def test_adam_step_literal_signature_vs_oracle(gpu, ws):
+    """SURVEY.md §8(b)'s literal zs_adam_step (float scalars, grad_scale = 1/ws, const carry):
+    with hyper-parameters exactly representable in fp32 the scalars it derives are torch's, so
+    it is bit-exact against the C oracle with the same double scalars — grad / ws (ws = 7: the
+    divisor is recovered from float(1/7)), ZeRO-1 carry with carry_scale = ws - 1, bf16 copy."""
+    import ctypes
+
+    from zero_amd import _lib
+    from zero_amd.kernels import stream_handle
+
+    rng = _seed(70 + ws)
+    n = 50_001
+    lr, b1, b2, eps, wd = 2.0 ** -10, 0.875, 1 - 2.0 ** -10, 2.0 ** -27, 2.0 ** -7
+    p0 = (rng.standard_normal(n) * 0.02).astype(np.float32)
+    P = torch.from_numpy(p0.copy()).to(gpu)
+    M, V = torch.zeros(n, device=gpu), torch.zeros(n, device=gpu)
+    C = torch.zeros(n, device=gpu) if ws > 1 else None
+    PB = torch.zeros(n, dtype=torch.bfloat16, device=gpu)
+    G = torch.zeros(n, device=gpu)
+    rp, rm, rv = p0.copy(), np.zeros(n, np.float32), np.zeros(n, np.float32)
+    rc = np.zeros(n, np.float32) if ws > 1 else None
+    f = ctypes.c_float
+    st = torch.cuda.current_stream(gpu)
+    for t in range(1, 4):
+        gt = (rng.standard_normal(n) * 1e-2).astype(np.float32)
+        G.copy_(torch.from_numpy(gt))
+        _lib.call("zs_adam_step", P.data_ptr(), PB.data_ptr(), G.data_ptr(), _lib.ZS_F32,
+                  M.data_ptr(), V.data_ptr(), n, f(lr), f(b1), f(b2), f(eps), f(wd), 1, t,
+                  f(np.float32(1.0 / ws)), None if C is None else C.data_ptr(), f(ws - 1),
+                  stream_handle(st))
+        hp = c_oracle.hparams(lr, b1, b2, eps, wd, step=t, decoupled=True, grad_div=float(ws),
+                              carry_mul=float(ws - 1))
+        c_oracle.adam_f32(rp, gt.copy(), rm, rv, hp, carry=rc)
+    torch.cuda.synchronize()
+    assert np.array_equal(P.cpu().numpy().view(np.uint32), rp.view(np.uint32))
+    assert np.array_equal(M.cpu().numpy().view(np.uint32), rm.view(np.uint32))
+    assert np.array_equal(V.cpu().numpy().view(np.uint32), rv.view(np.uint32))
+    want_b = torch.from_numpy(rp).to(torch.bfloat16).view(torch.int16).numpy()
+    assert np.array_equal(PB.cpu().view(torch.int16).numpy(), want_b)
+    if C is not None:
+        assert np.array_equal(C.cpu().numpy().view(np.uint32), rc.view(np.uint32))
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_pack_unpack_through_plan_bit_exact(gpu, dtype):
     """zs_pack / zs_unpack against the plan's own segment table, bit-exact, at

@@ -1,0 +1,136 @@
+"""Roofline table of the gfx950 kernels beside Adam: each kernel at the size the
+product launches it with, its algorithmic HBM bytes per launch, the average launch time from HIP
+events on the launch stream, achieved GB/s and the fraction of the 8 TB/s HBM peak.  Run it under
+``rocprofv3 --kernel-trace --stats`` as well; the two must agree on the per-kernel durations.
+
+  convert_kernel<true>   fp32 -> bf16 RNE, C3-size gradient (983,116,800 elements): the
+                         grad_comm="bf16" conversion before the exchange; 4 + 2 B/element
+  convert_kernel<false>  bf16 -> fp32, same size; 2 + 4 B/element
+  fp8_quantize_rows      one C5 decoder layer's matrices (bf16, row-scaled E4M3, the ZeRO-3
+                         gather_dtype="fp8" send side): 2 + 1 B/element + 4 B/row
+  fp8_dequantize_rows    the same layer gathered (receive side): 1 + 2 B/element + 4 B/row
+  scale_kernel           DDP's grad /= ws on a 256 MiB bf16 bucket and a 256 MiB fp32 bucket
+                         (in place): 2 x element size per element
+  copy_segments_kernel   pack of the C4 set's grads into one rank-major arena (every tensor a
+                         segment, bf16): 2 x 2 B/element
+
+Usage: python tools/kernel_table.py [--iters 20] [--out profiles/r03_kernels_table.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO / "distributed-training-sandbox_amd"))
+
+HBM_PEAK_GBS = 8000.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    from zero_amd import _lib
+    from zero_amd.engine import probed_zeros
+    from zero_amd.kernels import CopySet, convert, stream_handle
+    from zero_amd.shapes import decoder_shapes, mlp_shapes, smollm3_3b_shapes
+
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream(dev)
+    rows = []
+
+    def timed(name, launch, alg_bytes, note):
+        launch()  # warm
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(args.iters):
+            launch()
+        e1.record(st)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / args.iters
+        gbs = alg_bytes / (ms / 1e3) / 1e9
+        row = {"kernel": name, "avg_launch_ms": ms, "alg_bytes_per_launch": int(alg_bytes),
+               "achieved_gbs": gbs, "frac": gbs / HBM_PEAK_GBS, "workload": note}
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+
+    # convert: C3-size gradient (6 x Linear(12800, 12800) + biases)
+    n = int(sum(int(np.prod(s)) for s in mlp_shapes(12800)))
+    src, _ = probed_zeros(n, torch.float32, dev)
+    dst, _ = probed_zeros(n, torch.bfloat16, dev)
+    src.normal_()
+    timed("convert_kernel<true> (fp32->bf16)", lambda: convert(src, dst, st), 6 * n,
+          f"C3 gradient, {n:,} elements (grad_comm='bf16')")
+    timed("convert_kernel<false> (bf16->fp32)", lambda: convert(dst, src, st), 6 * n,
+          f"C3 gradient, {n:,} elements")
+    del src, dst
+    torch.cuda.empty_cache()
+
+    # fp8 row quantise / dequantise: one C5 decoder layer's matrices (bf16)
+    layer = [s for s in decoder_shapes("C5", 1)[1:10] if len(s) == 2]
+    mats = [torch.randn(s, device=dev).to(torch.bfloat16) for s in layer]
+    qs = [torch.empty(s, dtype=torch.uint8, device=dev) for s in layer]
+    scs = [torch.empty(s[0], dtype=torch.float32, device=dev) for s in layer]
+    outs = [torch.empty(s, dtype=torch.bfloat16, device=dev) for s in layer]
+    elems = sum(int(np.prod(s)) for s in layer)
+    nrows = sum(s[0] for s in layer)
+
+    def quant():
+        for x, q, sc in zip(mats, qs, scs):
+            _lib.call("zs_fp8_quantize_rows", x.data_ptr(), _lib.ZS_BF16, q.data_ptr(), sc.data_ptr(),
+                      x.shape[0], x.shape[1], stream_handle(st))
+
+    def dequant():
+        for q, sc, y in zip(qs, scs, outs):
+            _lib.call("zs_fp8_dequantize_rows", q.data_ptr(), sc.data_ptr(), y.data_ptr(),
+                      _lib.ZS_BF16, q.shape[0], q.shape[1], stream_handle(st))
+
+    timed("fp8_quantize_rows_kernel<bf16> (7 launches, one per matrix)", quant,
+          3 * elems + 4 * nrows, f"one C5 decoder layer, {elems:,} bf16 elements")
+    timed("fp8_dequantize_rows_kernel<bf16> (7 launches)", dequant, 3 * elems + 4 * nrows,
+          f"one C5 decoder layer, {elems:,} elements")
+    del mats, qs, scs, outs
+    torch.cuda.empty_cache()
+
+    # DDP scale: one 256 MiB bucket, bf16 and fp32, in place
+    for dt, code, es in ((torch.bfloat16, _lib.ZS_BF16, 2), (torch.float32, _lib.ZS_F32, 4)):
+        m = (256 << 20) // es
+        b = torch.randn(m, device=dev).to(dt)
+        timed(f"scale_kernel<{'bf16' if es == 2 else 'f32'}> (/3, in place)",
+              lambda b=b, code=code: _lib.call("zs_scale", b.data_ptr(), b.numel(), code, 3.0,
+                                               stream_handle(st)),
+              2 * es * m, f"DDP bucket, 256 MiB {dt}")
+        del b
+
+    # pack: the C4 set's bf16 grads (326 segments) into one rank-major arena
+    shapes = smollm3_3b_shapes()
+    total = int(sum(int(np.prod(s)) for s in shapes))
+    grads, _ = probed_zeros(total, torch.bfloat16, dev)
+    arena, _ = probed_zeros(total + 64 * len(shapes), torch.bfloat16, dev)
+    src, dst, nb, o, a = [], [], [], 0, 0
+    for s in shapes:
+        k = int(np.prod(s))
+        src.append(grads.data_ptr() + 2 * o)
+        dst.append(arena.data_ptr() + 2 * a)
+        nb.append(2 * k)
+        o += k
+        a += -(-k // 64) * 64
+    cs = CopySet(src, dst, nb)
+    timed("copy_segments_kernel (pack, 326 segments)", lambda: cs.run(st), 2 * cs.nbytes,
+          f"C4 bf16 grads, {total:,} elements, one launch")
+    if args.out:
+        Path(args.out).write_text(json.dumps({"iters": args.iters, "peak_gbs": HBM_PEAK_GBS,
+                                              "rows": rows}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
