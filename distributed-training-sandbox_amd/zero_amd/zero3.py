@@ -344,7 +344,25 @@ class Zero3ParamManager:
         self.full_data = None
 
 
-def register_zero3_hooks(model, param_managers, units=None, reshard_after_forward=True):
+def _grad_tensors(output):
+    """The tensors of a module's output (nested tuples / lists / dicts) that autograd will
+    differentiate through."""
+    out = []
+    stack = [output]
+    while stack:
+        o = stack.pop()
+        if torch.is_tensor(o):
+            if o.requires_grad:
+                out.append(o)
+        elif isinstance(o, (tuple, list)):
+            stack.extend(o)
+        elif isinstance(o, dict):
+            stack.extend(o.values())
+    return out
+
+
+def register_zero3_hooks(model, param_managers, units=None, reshard_after_forward=True,
+                         backward_hooks="tensor"):
     """zero3.py:56-77: forward / backward pre-hooks materialise a module's direct parameters (one
     grouped all-gather, prefetched on the side stream), post-hooks release them.
 
@@ -357,7 +375,19 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
     ``reshard_after_forward`` (FSDP2's flag, fsdp/train_fsdp.py:84-94): True (the reference's
     hooks, FSDP2 "ZeRO-3") releases after forward and gathers again for backward; False (FSDP2
     "ZeRO-2") keeps the gathered parameters from forward through backward — one gather per group
-    per step instead of two, full parameters resident between forward and backward."""
+    per step instead of two, full parameters resident between forward and backward.
+
+    ``backward_hooks``: how the backward gather / release is attached.  "module" — the reference's
+    ``register_full_backward_pre_hook`` / ``register_full_backward_hook`` (zero3.py:75-76), which
+    wrap every hooked module's inputs and outputs in identity autograd nodes on each forward.
+    "tensor" (default) — the same two moments without them: the forward post-hook registers a
+    grad hook on the module's output tensors (fires when the first output gradient is computed,
+    i.e. before the module's backward: materialise), and a post-accumulate-grad hook on each of
+    its parameters counts them in (once the last has its gradient the module's backward is done:
+    release); an end-of-backward callback releases whatever never counted in (frozen or unused
+    parameters).  Same gathers in the same order, less host time per module."""
+    if backward_hooks not in ("tensor", "module"):
+        raise ValueError(f"backward_hooks must be 'tensor' or 'module' (got {backward_hooks!r})")
     if all(m.world_size == 1 and not m.fp8 for m in param_managers.values()):
         # one rank: every shard is its whole parameter, so materialize / release are identities —
         # hooks would only cost host time (a forward whose host enqueue falls behind the GPU)
@@ -417,16 +447,75 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
         return post_hook
 
     handles = []
-    for m in model.modules():
-        # the reference hooks every module (zero3.py:73-77); a module without managed parameters
-        # has nothing to gather or release, so it is left unhooked (a full backward hook would
-        # only wrap its inputs and outputs in autograd nodes for nothing)
-        if not mod_managers[id(m)]:
-            continue
+    if backward_hooks == "module":
+        for m in model.modules():
+            # the reference hooks every module (zero3.py:73-77); a module without managed
+            # parameters has nothing to gather or release, so it is left unhooked (a full backward
+            # hook would only wrap its inputs and outputs in autograd nodes for nothing)
+            if not mod_managers[id(m)]:
+                continue
+            handles.append(m.register_forward_pre_hook(make_pre("fwd")))
+            handles.append(m.register_forward_hook(make_post("fwd")))
+            handles.append(m.register_full_backward_pre_hook(make_pre("bwd")))
+            handles.append(m.register_full_backward_hook(make_post("bwd")))
+        return handles
+
+    # backward_hooks == "tensor"
+    pre_bwd = make_pre("bwd")
+    post_fwd = make_post("fwd")
+    hooked = [m for m in model.modules() if mod_managers[id(m)]]
+    n_req = {id(m): sum(1 for mg in mod_managers[id(m)] if mg.param.requires_grad) for m in hooked}
+    param_mods = {}
+    for m in hooked:
+        for mg in mod_managers[id(m)]:
+            if mg.param.requires_grad:
+                param_mods.setdefault(mg.param, []).append(id(m))
+    open_ = {}     # id(module) -> managers gathered for its backward, not released yet
+    pending = {}   # id(module) -> parameter gradients still to come this backward
+    queued = [False]
+
+    def end_backward():
+        queued[0] = False
+        for ms in open_.values():
+            for mg in ms:
+                mg.release()
+        open_.clear()
+
+    def backward_pre(module):
+        mid = id(module)
+        if not queued[0]:
+            queued[0] = True
+            torch.autograd.Variable._execution_engine.queue_callback(end_backward)
+        pre_bwd(module)
+        if n_req[mid]:
+            open_[mid] = mod_managers[mid]
+            pending[mid] = n_req[mid]
+        else:  # nothing will count in: released at the end of backward
+            open_[mid] = mod_managers[mid]
+            pending[mid] = -1
+
+    def forward_post(module, args, output):
+        post_fwd(module)
+        if torch.is_grad_enabled():
+            ts = _grad_tensors(output)
+            if ts:
+                torch.autograd.graph.register_multi_grad_hook(
+                    ts, lambda _g, module=module: backward_pre(module), mode="any")
+        return None
+
+    def grad_ready(p):
+        for mid in param_mods[p]:
+            if mid in open_:
+                pending[mid] -= 1
+                if pending[mid] == 0:
+                    for mg in open_.pop(mid):
+                        mg.release()
+
+    for m in hooked:
         handles.append(m.register_forward_pre_hook(make_pre("fwd")))
-        handles.append(m.register_forward_hook(make_post("fwd")))
-        handles.append(m.register_full_backward_pre_hook(make_pre("bwd")))
-        handles.append(m.register_full_backward_hook(make_post("bwd")))
+        handles.append(m.register_forward_hook(forward_post))
+    for p in param_mods:
+        handles.append(p.register_post_accumulate_grad_hook(grad_ready))
     return handles
 
 

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--profile", type=int, default=5)
     ap.add_argument("--layers", type=int, default=None)
+    ap.add_argument("--bwd-hooks", default="tensor", choices=["tensor", "module"])
     args = ap.parse_args()
 
     import torch
@@ -58,7 +59,7 @@ def main():
         else real_get(what, dm)
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
                                  sync=False, comm=bench._NoComm(ws))
-    zero3.register_zero3_hooks(model, opt.param_managers)
+    zero3.register_zero3_hooks(model, opt.param_managers, backward_hooks=args.bwd_hooks)
     x = torch.zeros(1, device=dev, requires_grad=True)
 
     def step():
@@ -78,7 +79,8 @@ def main():
     el = (time.perf_counter() - t0) / args.iters * 1e3
     ev, opt.timing_events = opt.timing_events, None
     adam_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / args.iters
-    out = {"config": args.config, "simulated_ws": ws, "layers": len(model.layers),
+    out = {"config": args.config, "simulated_ws": ws, "backward_hooks": args.bwd_hooks,
+           "layers": len(model.layers),
            "tensors": len(shapes), "ms_per_iteration": el, "host_enqueue_ms_per_iteration": host,
            "adam_ms_per_iteration": adam_ms, "gathers_per_iteration": 2 * len(model.layers),
            "reduce_buckets": opt._reducer.K}
