@@ -362,7 +362,7 @@ def _grad_tensors(output):
 
 
 def register_zero3_hooks(model, param_managers, units=None, reshard_after_forward=True,
-                         backward_hooks="tensor"):
+                         backward_hooks=None):
     """zero3.py:56-77: forward / backward pre-hooks materialise a module's direct parameters (one
     grouped all-gather, prefetched on the side stream), post-hooks release them.
 
@@ -385,7 +385,14 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
     i.e. before the module's backward: materialise), and a post-accumulate-grad hook on each of
     its parameters counts them in (once the last has its gradient the module's backward is done:
     release); an end-of-backward callback releases whatever never counted in (frozen or unused
-    parameters).  Same gathers in the same order, less host time per module."""
+    parameters).  Same gathers in the same order, less host time per module.  Default (None):
+    "tensor" in update mode; "module" in reference mode, whose release after backward shrinks the
+    gradients already accumulated — with module hooks exactly the ones the reference shrinks (not
+    Linear 0's, whose full backward hook fires before its weight gradient exists), an observable
+    the reference-mode tests pin."""
+    if backward_hooks is None:
+        backward_hooks = "tensor" if all(m.keep_full_grad for m in param_managers.values()) \
+            else "module"
     if backward_hooks not in ("tensor", "module"):
         raise ValueError(f"backward_hooks must be 'tensor' or 'module' (got {backward_hooks!r})")
     if all(m.world_size == 1 and not m.fp8 for m in param_managers.values()):

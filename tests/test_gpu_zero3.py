@@ -133,10 +133,12 @@ def _update_injected(rank, ws, name, dev, comm=None, dtype=torch.float32):
             assert rel(st["exp_avg"].cpu().numpy(), _chunk(z[key], ws, rank)) <= 1e-6
 
 
-def _update_hooks(rank, ws, name, dev, comm=None):
+def _update_hooks(rank, ws, name, dev, comm=None, backward_hooks=None):
     """update=True through the real hooks: forward / backward all-gathers, gradients
     reduce-scattered from the post-accumulate-grad hooks during backward, fused Adam on the
-    chunks.  Grads come from hipBLAS GEMMs, so the bound vs the CPU reference is 1e-4."""
+    chunks.  Grads come from hipBLAS GEMMs, so the bound vs the CPU reference is 1e-4.  Backward
+    gathers / releases attached through output-tensor hooks (the default in update mode) or the
+    reference's module backward hooks."""
     from zero_amd import zero3
 
     z = np.load(GOLDEN / name)
@@ -144,13 +146,15 @@ def _update_hooks(rank, ws, name, dev, comm=None):
     kw = {} if comm is None else {"comm": comm}
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
                                  bucket_mb=2e-3, **kw)  # ~2 KB buckets: several launches in backward
-    zero3.register_zero3_hooks(model, opt.param_managers)
+    zero3.register_zero3_hooks(model, opt.param_managers, backward_hooks=backward_hooks)
     params = list(model.parameters())
     x, y = _xy(z, rank, dev)
     for t in range(int(z["steps"])):
         opt.zero_grad()
         loss = torch.nn.functional.mse_loss(model(x), y)
         loss.backward()
+        # every parameter is back to its shard after backward
+        assert all(p.data.shape == opt._arena.shard_shapes[i] for i, p in enumerate(params))
         if ws > 1:  # backward left every grad as its summed chunk, full grads already released
             assert opt._reducer.next == opt._reducer.K and opt._reducer.launched_in_backward > 0
             assert [tuple(p.grad.shape) for p in params] == [tuple(p.shape) for p in params]
@@ -163,6 +167,10 @@ def _update_hooks(rank, ws, name, dev, comm=None):
     assert ws == 1 or opt.runtime.n_prefetch_hits > 0  # (ws=1: no hooks, nothing to gather)
     if ws > 1:
         assert opt.communication_time >= 0.0
+
+
+def _update_hooks_module(rank, ws, name, dev, comm=None):
+    _update_hooks(rank, ws, name, dev, comm=comm, backward_hooks="module")
 
 
 @pytest.fixture
@@ -207,7 +215,8 @@ Z3_CASES = [("_ref_mode", w, f"traj_z3_ws{w}_d16_distinct.npz") for w in (2, 4, 
     [("_ref_injected", w, f"traj_z3_ws{w}_d16_ref.npz") for w in (2, 4, 8)] + \
     [("_update_injected", w, f"traj_z2_ws{w}_d16_distinct.npz") for w in (2, 3, 4, 8)] + \
     [("_update_hooks", w, f"traj_z2_ws{w}_d16_{m}.npz")
-     for w, m in ((2, "distinct"), (3, "distinct"), (4, "distinct"), (8, "ref"), (8, "distinct"))]
+     for w, m in ((2, "distinct"), (3, "distinct"), (4, "distinct"), (8, "ref"), (8, "distinct"))] + \
+    [("_update_hooks_module", w, f"traj_z2_ws{w}_d16_distinct.npz") for w in (2, 4)]
 
 
 @pytest.mark.parametrize("ws", [2, 3, 4, 8])
