@@ -195,16 +195,22 @@ def comm_selfcheck(comm, world, rank, dev):
     import torch
 
     st = torch.cuda.Stream(device=dev)
+    cur = torch.cuda.current_stream(dev)
     n = 4096
     i = torch.arange(world * n, device=dev, dtype=torch.float32)
     out = {}
     buf = rank + i / 1024
+    # the inputs are written on the current stream and the collectives run on `st`: every call
+    # waits for them (without the wait, RCCL read half-written inputs on ranks 6-7 of an N=8
+    # one-GPU rehearsal and the check failed a correct communicator)
+    st.wait_stream(cur)
     comm.reduce_scatter(buf, buf[rank * n:(rank + 1) * n], st)
     st.synchronize()
     want = world * (world - 1) / 2 + i[rank * n:(rank + 1) * n] * world / 1024
     out["reduce_scatter"] = bool(torch.equal(buf[rank * n:(rank + 1) * n], want))
     buf = torch.full((world * n,), -1.0, device=dev)
     buf[rank * n:(rank + 1) * n] = rank + i[:n] / 1024
+    st.wait_stream(cur)
     comm.all_gather(buf[rank * n:(rank + 1) * n], buf, st)
     st.synchronize()
     out["all_gather"] = bool(torch.equal(buf, (i // n) + (i % n) / 1024))
@@ -212,6 +218,7 @@ def comm_selfcheck(comm, world, rank, dev):
     offs = [sum(lens[:r]) for r in range(world)]
     tot = sum(lens)
     buf = rank + torch.arange(tot, device=dev, dtype=torch.float32) / 1024
+    st.wait_stream(cur)
     comm.reduce_v(buf, offs, lens, st)
     st.synchronize()
     o, m = offs[rank], lens[rank]
@@ -219,6 +226,7 @@ def comm_selfcheck(comm, world, rank, dev):
     out["reduce_v"] = bool(torch.equal(buf[o:o + m], want))
     buf = torch.full((tot,), -1.0, device=dev)
     buf[o:o + m] = rank + 0.5
+    st.wait_stream(cur)
     comm.broadcast_v(buf, offs, lens, st)
     st.synchronize()
     want = torch.cat([torch.full((lens[r],), r + 0.5, device=dev) for r in range(world)])
