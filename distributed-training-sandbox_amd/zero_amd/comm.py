@@ -157,6 +157,34 @@ class RcclComm:
                   recv.ctypes.data_as(_PU64), count.ctypes.data_as(_PI64), int(dtype),
                   stream_handle(stream))
 
+    def all_gather_group_bound(self, send, recv, count, dtype: int):
+        """all_gather_group with its tables bound once: returns ``run(stream)``, which issues the
+        group from the arrays' current contents (the caller refills ``recv`` in place) — the
+        per-call ctypes conversions of the table form, paid once (ZeRO-3 gathers every module
+        twice per iteration)."""
+        fn = _lib.lib.zs_all_gather_group
+        n = len(count)
+        sp, rp, cp = send.ctypes.data_as(_PU64), recv.ctypes.data_as(_PU64), count.ctypes.data_as(_PI64)
+        h, dt = self._h, int(dtype)
+        keep = (send, recv, count)  # the pointers stay valid while the closure lives
+
+        def run(stream, _keep=keep):
+            _lib.check(fn(h, n, sp, rp, cp, dt, stream_handle(stream)), "zs_all_gather_group")
+        return run
+
+    def reduce_scatter_group_bound(self, send, recv, count, dtype: int):
+        """reduce_scatter_group with its tables bound once (see all_gather_group_bound): the
+        caller refills ``send`` in place before each ``run(stream)``."""
+        fn = _lib.lib.zs_reduce_scatter_group
+        n = len(count)
+        sp, rp, cp = send.ctypes.data_as(_PU64), recv.ctypes.data_as(_PU64), count.ctypes.data_as(_PI64)
+        h, dt = self._h, int(dtype)
+        keep = (send, recv, count)
+
+        def run(stream, _keep=keep):
+            _lib.check(fn(h, n, sp, rp, cp, dt, stream_handle(stream)), "zs_reduce_scatter_group")
+        return run
+
     def reduce_scatter_group(self, send, recv, count, dtype: int, stream) -> None:
         """One RCCL group of SUM reduce-scatters (a ZeRO-3 gradient bucket): entry i reduces
         ``ws * count[i]`` elements at ``send[i]`` and leaves this rank's ``count[i]`` at

@@ -101,7 +101,7 @@ class _GatherRuntime:
             ev = self._events[key] = (torch.cuda.Event(), torch.cuda.Event())
         return ev
 
-    def launch(self, key, managers):
+    def launch(self, key, managers, cur=None):
         """Enqueue the all-gather of ``managers`` on the side stream; returns immediately."""
         if key in self.pending or not managers:
             return
@@ -111,38 +111,48 @@ class _GatherRuntime:
             self.n_gathers += 1
             return
         ev_ready, ev = self._key_events(key)
-        ev_ready.record(torch.cuda.current_stream(self.device))  # shards may just have been updated
+        if cur is None:
+            cur = torch.cuda.current_stream(self.device)
+        ev_ready.record(cur)  # shards may just have been updated
         timed = self.gather_events is not None and self.ws > 1
-        plan = self._table(key, managers)
-        with torch.cuda.stream(self.stream):
-            self.stream.wait_event(ev_ready)
-            if timed:
-                e0 = torch.cuda.Event(enable_timing=True)
-                e0.record(self.stream)
-            hold = None
-            if plan is not None:
-                # one allocation for the module's full tensors and ONE library call for its RCCL
-                # group of all-gathers (zero-copy from the chunk-arena slots)
-                send, count, offs, total, dt, es, views = plan
-                hold = torch.empty(total, dtype=managers[0].shard.dtype, device=self.device)
-                recv = offs + np.uint64(hold.data_ptr())
-                self.comm.all_gather_group(send, recv, count, dt, self.stream)
-                # each manager's full tensor: one strided view of the allocation (no slice + view)
-                out = [(m, hold.as_strided(shape, stride, off)) for m, (shape, stride, off)
-                       in zip(managers, views)]
+        plan = self._tables[key] if key in self._tables else self._table(key, managers)
+        side = self.stream
+        side.wait_event(ev_ready)
+        if timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record(side)
+        hold = None
+        if plan is not None:
+            # one allocation for the module's full tensors and ONE library call for its RCCL group
+            # of all-gathers (zero-copy from the chunk-arena slots).  Allocated on the compute
+            # stream (which reads it once the gather's event has passed); the side stream that
+            # writes it is recorded on it, so a prefetch dropped unconsumed keeps its memory until
+            # the gather has finished
+            send, count, offs, total, dt, es, views, recv, raw = plan
+            hold = torch.empty(total, dtype=managers[0].shard.dtype, device=self.device)
+            hold.record_stream(side)
+            np.add(offs, np.uint64(hold.data_ptr()), out=recv)
+            if raw is not None:  # cached ctypes pointers of the tables: one foreign call
+                raw(side)
             else:
+                self.comm.all_gather_group(send, recv, count, dt, side)
+            # each manager's full tensor: one strided view of the allocation (no slice + view)
+            out = [(m, hold.as_strided(shape, stride, off)) for m, (shape, stride, off)
+                   in zip(managers, views)]
+        else:
+            with torch.cuda.stream(side):
                 # kernels (fp8 quantisation) before the RCCL group, dequantisation after: an RCCL
                 # group only launches its collectives at group end; every buffer a collective of
                 # the group touches is referenced from `states` until the group has ended
-                states = [m._gather_prepare(self.stream) for m in managers]
+                states = [m._gather_prepare(side) for m in managers]
                 with _group_ctx(self.comm):
                     for m, st in zip(managers, states):
-                        m._gather_issue(self.comm, self.stream, st)
-                out = [(m, m._gather_finish(self.stream, st)) for m, st in zip(managers, states)]
-            ev.record(self.stream)
-            if timed:  # ring all-gather bus bytes: (ws-1)/ws of the gathered tensor, per rank
-                bus = sum(m.gather_bytes() for m in managers) * (self.ws - 1)
-                self.gather_events.append((e0, _timed_after(self.stream), bus))
+                        m._gather_issue(self.comm, side, st)
+                out = [(m, m._gather_finish(side, st)) for m, st in zip(managers, states)]
+        ev.record(side)
+        if timed:  # ring all-gather bus bytes: (ws-1)/ws of the gathered tensor, per rank
+            bus = sum(m.gather_bytes() for m in managers) * (self.ws - 1)
+            self.gather_events.append((e0, _timed_after(side), bus))
         self.pending[key] = (out, ev, hold)
         self.n_gathers += 1
 
@@ -172,17 +182,23 @@ class _GatherRuntime:
                     stride.append(acc)
                     acc *= d
                 views.append((shape, tuple(reversed(stride)), off))
-            plan = (np.array([m.send_slot.data_ptr() for m in managers], np.uint64),
-                    np.array([m.S for m in managers], np.int64),
-                    np.array(offs, np.uint64) * np.uint64(es), max(o, 1),
-                    zs_dtype(managers[0].shard.dtype), es, views)
+            send = np.array([m.send_slot.data_ptr() for m in managers], np.uint64)
+            count = np.array([m.S for m in managers], np.int64)
+            recv = np.zeros(len(managers), np.uint64)  # refilled per gather (allocation + offs)
+            dt = zs_dtype(managers[0].shard.dtype)
+            raw = None
+            bind = getattr(self.comm, "all_gather_group_bound", None)
+            if bind is not None:
+                raw = bind(send, recv, count, dt)
+            plan = (send, count, np.array(offs, np.uint64) * np.uint64(es), max(o, 1), dt, es,
+                    views, recv, raw)
         self._tables[key] = plan
         return plan
 
-    def _prefetch(self, i):
+    def _prefetch(self, i, cur=None):
         if 0 <= i < len(self.sequence):
             key = self.sequence[i]
-            self.launch(key, self.key_managers.get(key))
+            self.launch(key, self.key_managers.get(key), cur)
 
     def materialize(self, key, managers):
         if self.recording:
@@ -195,17 +211,16 @@ class _GatherRuntime:
             self._prefetch(self.pos)  # the next group, while this one computes
         if key in self.pending:
             self.n_prefetch_hits += 1
-        self.launch(key, managers)
+        cur = torch.cuda.current_stream(self.device)
+        self.launch(key, managers, cur)
         out, ev, hold = self.pending.pop(key)
         if ev is None:  # ws == 1
             for m, full in out:
                 m._install_full(full)
             return
-        cur = torch.cuda.current_stream(self.device)
         cur.wait_event(ev)
-        if hold is not None:  # one allocation behind all of the module's full tensors, whose
-            hold.record_stream(cur)  # views already have the full shapes
-            for m, full in out:
+        if hold is not None:  # one allocation (on this stream) behind all of the module's full
+            for m, full in out:  # tensors, whose views already have the full shapes
                 m.full_data = full
                 m.param.data = full
             return
@@ -505,7 +520,9 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
         post_fwd(module)
         if torch.is_grad_enabled():
             ts = _grad_tensors(output)
-            if ts:
+            if len(ts) == 1:  # one output: a plain tensor hook (cheaper than a multi-grad hook)
+                ts[0].register_hook(lambda _g, module=module: backward_pre(module))
+            elif ts:
                 torch.autograd.graph.register_multi_grad_hook(
                     ts, lambda _g, module=module: backward_pre(module), mode="any")
         return None
@@ -611,6 +628,12 @@ class _GradReducer:
         for k, g in enumerate(groups):
             self.bucket_of[g] = k
         self._size = np.array([len(g) for g in groups], np.int64)
+        # per-element bookkeeping in plain lists (numpy scalar indexing costs more per hook call)
+        self._size_l = [len(g) for g in groups]
+        self._bucket_of_l = self.bucket_of.tolist()
+        self._S_l = [int(x) for x in arena.S]
+        self._N_l = [int(x) for x in arena.numel]
+        self._shard_grad = [None] * n  # cached grad-arena views handed out as shard grads
         self.ev_done = [torch.cuda.Event() for _ in range(self.K)]
         self.ev_ready = [torch.cuda.Event() for _ in range(self.K)]
         self.timing = None  # optional list of (start, end, bus_bytes) per launched bucket
@@ -621,8 +644,8 @@ class _GradReducer:
         n = len(self.opt.params)
         # buckets the last backward launched before it ended (the rest: flushed at its end)
         self.last_launched_in_backward = getattr(self, "launched_in_backward", 0)
-        self.pending = self._size.copy()
-        self.marked = np.zeros(n, bool)
+        self.pending = list(self._size_l)
+        self.marked = [False] * n
         self.had_grad = np.zeros(n, bool)
         self.local_grads = [None] * n  # ws == 1: the grad itself is the chunk's gradient
         self.next = 0
@@ -639,7 +662,7 @@ class _GradReducer:
                 "zero_amd ZeRO-3: gradient of parameter %d accumulated twice before step(); "
                 "update mode reduce-scatters each gradient once per step" % i)
         self.marked[i] = True
-        self.pending[self.bucket_of[i]] -= 1
+        self.pending[self._bucket_of_l[i]] -= 1
         if not self.callback_queued:
             self.callback_queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._end_backward)
@@ -667,11 +690,17 @@ class _GradReducer:
         cur = torch.cuda.current_stream(opt._arena.device)
         if self.K:
             cur.wait_event(self.ev_done[self.K - 1])
-        for i, p in enumerate(opt.params):
-            if (self.had_grad[i] and p.data.shape == opt._arena.shard_shapes[i]
-                    and opt._G.dtype == p.dtype):  # (a bf16 exchange's chunks stay internal)
-                s, n = int(opt._arena.slot[i]), int(opt._arena.ln[i])
-                p.grad = opt._G[s:s + n].view(opt._arena.shard_shapes[i])
+        if opt._G.dtype != opt.params[0].dtype:  # a bf16 exchange's chunks stay internal
+            return
+        shapes, views = opt._arena.shard_shapes, self._shard_grad
+        for i in np.nonzero(self.had_grad)[0].tolist():
+            p = opt.params[i]
+            if p.data.shape == shapes[i]:
+                v = views[i]
+                if v is None:
+                    s, n = int(opt._arena.slot[i]), int(opt._arena.ln[i])
+                    v = views[i] = opt._G[s:s + n].view(shapes[i])
+                p.grad = v
 
     def _rs_table(self, k: int):
         """Bucket k's reduce-scatter destinations (grad chunk-arena slots) and counts, cached."""
@@ -681,8 +710,12 @@ class _GradReducer:
 
             opt, idx = self.opt, np.asarray(self.groups[k], np.int64)
             G = opt._G
-            t = (np.uint64(G.data_ptr()) + (opt._arena.slot[idx] * G.element_size()).astype(np.uint64),
-                 np.ascontiguousarray(opt._arena.S[idx], np.int64), zs_dtype(G.dtype))
+            recv = np.uint64(G.data_ptr()) + (opt._arena.slot[idx] * G.element_size()).astype(np.uint64)
+            count = np.ascontiguousarray(opt._arena.S[idx], np.int64)
+            send = np.zeros(len(idx), np.uint64)  # refilled per launch with the grads' addresses
+            bind = getattr(opt.comm, "reduce_scatter_group_bound", None)
+            raw = bind(send, recv, count, zs_dtype(G.dtype)) if bind is not None else None
+            t = (recv, count, zs_dtype(G.dtype), send, raw)
             self._rs_tables[k] = t
         return t
 
@@ -703,10 +736,11 @@ class _GradReducer:
         cur = torch.cuda.current_stream(dev)
         wdt = opt._G.dtype  # on the wire: the param dtype, or bf16 for grad_comm="bf16"
         sends = []  # (param index, send buffer): alive until the RCCL group has been enqueued
+        S_l, N_l = self._S_l, self._N_l
         for i in self.groups[k]:
             p = opt.params[i]
             g = p.grad
-            S, N = int(ar.S[i]), int(ar.numel[i])
+            S, N = S_l[i], N_l[i]
             if g is None:
                 send = torch.zeros(ws * S, dtype=wdt, device=dev)  # every rank takes part
             else:
@@ -735,9 +769,13 @@ class _GradReducer:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record(cs)
         if hasattr(opt.comm, "reduce_scatter_group"):  # the bucket's RCCL group: ONE call
-            recv, count, dt = self._rs_table(k)
-            sp = np.fromiter((t.data_ptr() for _, t in sends), np.uint64, len(sends))
-            opt.comm.reduce_scatter_group(sp, recv, count, dt, cs)
+            recv, count, dt, sp, raw = self._rs_table(k)
+            for j, (_, t) in enumerate(sends):
+                sp[j] = t.data_ptr()
+            if raw is not None:  # tables bound once (comm.reduce_scatter_group_bound)
+                raw(cs)
+            else:
+                opt.comm.reduce_scatter_group(sp, recv, count, dt, cs)
         else:
             with _group_ctx(opt.comm):
                 for i, send in sends:
@@ -844,6 +882,8 @@ class ShardedOptimizer:
         self._G = torch.zeros(L, dtype=gdt, device=ar.device) if self.world_size > 1 else None
         self._steps = np.zeros(len(self.params), np.int64)
         self._adam_cache = {}
+        self._fast_sig = self._fast_sets = None
+        self._step_shared = self._step_shared_sig = None
         self._retired = []
         self._expose_state()
 
@@ -860,6 +900,7 @@ class ShardedOptimizer:
 
     def _expose_state(self):
         """optimizer.state[p]: views of the flat state (chunk-shaped) and torch's ``step``."""
+        self._step_shared_sig = None  # per-param step tensors again: the next step re-shares
         step_t = {}
         for i, p in enumerate(self.params):
             st = self.optimizer.state[p]
@@ -955,9 +996,28 @@ class ShardedOptimizer:
         hps = {gi: adam_group_hparams(self._groups[gi], self.optimizer) for gi in set(self._group_of)}
         if any(h["amsgrad"] for h in hps.values()) and self._vmax is None:
             self._ensure_vmax()
-        if len(idx):
+        steps = self._steps[idx]
+        uniform = len(idx) > 0 and bool((steps == steps[0]).all())
+        # (ws == 1: Adam reads the local grads themselves, whose addresses change — no fast path)
+        sig = (idx.tobytes(), self._vmax is None) if self.world_size > 1 else None
+        fast = self._fast_sets if uniform and sig is not None and self._fast_sig == sig else None
+        if fast is not None:  # the same parameters as last step, one step count: cached sets
+            for gi, aset in fast:
+                h = hps[gi]
+                hp = adam_hparams(h["lr"], h["beta1"], h["beta2"], h["eps"], h["weight_decay"],
+                                  int(steps[0]), decoupled=h["decoupled"], amsgrad=h["amsgrad"],
+                                  maximize=h["maximize"], grad_div=float(self.world_size))
+                if self.timing_events is not None:
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e0.record(cur)
+                    aset.run(hp, cur)
+                    self.timing_events.append((e0, _timed_after(cur), aset.bytes))
+                else:
+                    aset.run(hp, cur)
+        elif len(idx):
             rows = self._adam_rows(idx)
             keys = np.stack([np.asarray(self._group_of)[idx], self._steps[idx]], axis=1)
+            used = []
             for key in np.unique(keys, axis=0):
                 sel = np.nonzero((keys == key).all(axis=1))[0]
                 sub = np.ascontiguousarray(rows[sel])
@@ -982,13 +1042,29 @@ class ShardedOptimizer:
                     self.timing_events.append((e0, _timed_after(cur), hit[1].bytes))
                 else:
                     hit[1].run(hp, cur)
-        step_t = {}
-        for i in idx:
-            s = int(self._steps[i])
-            t = step_t.get(s)
+                used.append((int(key[0]), hit[1]))
+            # one set per param group and one step count: next step takes the cached sets
+            self._fast_sig = sig if uniform else None
+            self._fast_sets = used if uniform else None
+        if uniform:  # torch's state['step'] (a CPU tensor): one shared tensor, updated in place
+            t = self._step_shared
             if t is None:
-                t = step_t[s] = torch.tensor(float(s))
-            self.optimizer.state[self.params[i]]["step"] = t
+                t = self._step_shared = torch.tensor(float(steps[0]))
+            else:
+                t.fill_(float(steps[0]))
+            if sig is None or self._step_shared_sig != sig:
+                for i in idx.tolist():
+                    self.optimizer.state[self.params[i]]["step"] = t
+                self._step_shared_sig = sig
+        else:
+            self._step_shared_sig = None
+            step_t = {}
+            for i in idx:
+                s_ = int(self._steps[i])
+                t = step_t.get(s_)
+                if t is None:
+                    t = step_t[s_] = torch.tensor(float(s_))
+                self.optimizer.state[self.params[i]]["step"] = t
         for p in self.params:  # zero3.py:150-153: no grad survives the step
             p.grad = None
         red.reset()

@@ -124,7 +124,9 @@ def _zero3_cases(ws):
 def test_rccl_zero3(gpu, rccl_env, ws):
     """ZeRO-3 through real RCCL: table gathers from the module hooks (reference and update mode),
     backward reduce-scatters, uneven chunks (ws = 3), bf16 gradient exchange, sharded gradient
-    memory, fp8 gathers, SmolLM3 ZeRO-3 AdamW bit for bit against the C oracle."""
+    memory, fp8 gathers, SmolLM3 ZeRO-3 AdamW bit for bit against the C oracle, checkpointing;
+    at ws = 8 every exchange the 8-GPU run executes (hooked gathers in forward and backward,
+    backward reduce-scatters, the reference mode's shard all-reduce, the bf16 exchange)."""
     _batch(ws, _zero3_cases(ws))
 
 

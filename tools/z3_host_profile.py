@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--profile", type=int, default=5)
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--bwd-hooks", default="tensor", choices=["tensor", "module"])
+    ap.add_argument("--blocks", type=int, default=5, help="timing blocks of --iters iterations")
     args = ap.parse_args()
 
     import torch
@@ -79,12 +80,74 @@ def main():
     el = (time.perf_counter() - t0) / args.iters * 1e3
     ev, opt.timing_events = opt.timing_events, None
     adam_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / args.iters
-    out = {"config": args.config, "simulated_ws": ws, "backward_hooks": args.bwd_hooks,
+    import gc
+
+    blocks = []
+    for gc_on in [True] * args.blocks:
+        (gc.enable if gc_on else gc.disable)()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.iters):
+            step()
+        torch.cuda.synchronize()
+        blocks.append((gc_on, round((time.perf_counter() - t1) / args.iters * 1e3, 3)))
+    gc.enable()
+    out_blocks = {"blocks_ms_per_iteration(gc_enabled, ms)": blocks}
+    out = {"config": args.config, "simulated_ws": ws, "backward_hooks": args.bwd_hooks, **out_blocks,
            "layers": len(model.layers),
            "tensors": len(shapes), "ms_per_iteration": el, "host_enqueue_ms_per_iteration": host,
            "adam_ms_per_iteration": adam_ms, "gathers_per_iteration": 2 * len(model.layers),
            "reduce_buckets": opt._reducer.K}
     print(json.dumps(out), flush=True)
+    # inclusive host time of the runtime's entry points, on whatever thread runs them (backward
+    # hooks run on autograd's device thread, which cProfile does not see)
+    acc = {}
+
+    def timed(owner, name):
+        fn = getattr(owner, name)
+
+        def wrapper(*a, **k):
+            t = time.perf_counter()
+            try:
+                return fn(*a, **k)
+            finally:
+                key = f"{owner.__name__}.{name}"
+                tot, n = acc.get(key, (0.0, 0))
+                acc[key] = (tot + time.perf_counter() - t, n + 1)
+        setattr(owner, name, wrapper)
+        return fn
+
+    patched = [(o, n, timed(o, n)) for o, n in (
+        (zero3._GatherRuntime, "launch"), (zero3._GatherRuntime, "materialize"),
+        (zero3.Zero3ParamManager, "release"), (zero3._GradReducer, "on_grad_ready"),
+        (zero3._GradReducer, "_launch"), (zero3._GradReducer, "_end_backward"),
+        (zero3.ShardedOptimizer, "step"), (zero3.ShardedOptimizer, "zero_grad"))]
+    n_t = 10
+    phases = {"zero_grad": 0.0, "forward": 0.0, "backward": 0.0, "step": 0.0}
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n_t):
+        ta = time.perf_counter()
+        opt.zero_grad()
+        tb = time.perf_counter()
+        y = model(x).sum()
+        tc = time.perf_counter()
+        y.backward()
+        td = time.perf_counter()
+        opt.step()
+        te = time.perf_counter()
+        for k, d in zip(phases, (tb - ta, tc - tb, td - tc, te - td)):
+            phases[k] += d
+    wall = (time.perf_counter() - t0) / n_t * 1e3
+    torch.cuda.synchronize()
+    for o, n, fn in patched:
+        setattr(o, n, fn)
+    print(json.dumps({"instrumented_ms_per_iteration": wall,
+                      "phase_ms_per_iteration": {k: round(v / n_t * 1e3, 3) for k, v in phases.items()},
+                      "inclusive_ms_per_iteration": {k: round(v[0] / n_t * 1e3, 3)
+                                                     for k, v in sorted(acc.items())},
+                      "calls_per_iteration": {k: v[1] / n_t for k, v in sorted(acc.items())}}),
+          flush=True)
     if args.profile:
         pr = cProfile.Profile()
         pr.enable()
