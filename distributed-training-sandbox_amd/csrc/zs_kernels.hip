@@ -455,10 +455,9 @@ __device__ __forceinline__ float qclamp(float x, float inv) {
   return __builtin_amdgcn_fmed3f(x * inv, kE4M3Max, -kE4M3Max);
 }
 
-// One workgroup per row (grid-stride over rows): amax by wave shuffles + 4-entry LDS, then the
-// row is re-read (L2-resident: <= 64 KiB) and converted.  VEC: 8 elements per lane per access
-// (16 B bf16 / 2 x 16 B fp32 loads, 8 B fp8 stores) when row_len % 8 == 0 and rows are aligned.
-template <typename T, bool VEC>
+// Block-per-row fallback for any row length and alignment (scalar accesses): amax by wave
+// shuffles + a 4-entry LDS exchange, then the row is re-read (L2-resident) and converted.
+template <typename T>
 __global__ __launch_bounds__(kThreads) void fp8_quantize_rows_kernel(
     const T* __restrict__ src, unsigned char* __restrict__ dst, float* __restrict__ scales,
     int64_t rows, int64_t row_len) {
@@ -468,26 +467,7 @@ __global__ __launch_bounds__(kThreads) void fp8_quantize_rows_kernel(
     const gptr<const T> x = glob(src + r * row_len);
     const gptr<unsigned char> q = glob(dst + r * row_len);
     float amax = 0.0f;
-    if constexpr (VEC) {
-      for (int64_t i = int64_t(threadIdx.x) * 8; i < row_len; i += kThreads * 8) {
-        float v[8];
-        if constexpr (sizeof(T) == 2) {
-          const uint4 raw = *reinterpret_cast<gptr<const uint4>>(x + i);
-          const unsigned short* h = reinterpret_cast<const unsigned short*>(&raw);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = bf16_to_f32(h[j]);
-        } else {
-          const float4 a = *reinterpret_cast<gptr<const float4>>(x + i);
-          const float4 b = *reinterpret_cast<gptr<const float4>>(x + i + 4);
-          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-          v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[j]));
-      }
-    } else {
-      for (int64_t i = threadIdx.x; i < row_len; i += kThreads) amax = fmaxf(amax, fabsf(to_f32<T>(x[i])));
-    }
+    for (int64_t i = threadIdx.x; i < row_len; i += kThreads) amax = fmaxf(amax, fabsf(to_f32<T>(x[i])));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
@@ -496,37 +476,133 @@ __global__ __launch_bounds__(kThreads) void fp8_quantize_rows_kernel(
     __syncthreads();
     const float inv = amax > 0.0f ? kE4M3Max / amax : 1.0f;
     if (threadIdx.x == 0) glob(scales)[r] = amax > 0.0f ? amax / kE4M3Max : 1.0f;
-    if constexpr (VEC) {
-      for (int64_t i = int64_t(threadIdx.x) * 8; i < row_len; i += kThreads * 8) {
-        float v[8];
-        if constexpr (sizeof(T) == 2) {
-          const uint4 raw = *reinterpret_cast<gptr<const uint4>>(x + i);
-          const unsigned short* h = reinterpret_cast<const unsigned short*>(&raw);
+    for (int64_t i = threadIdx.x; i < row_len; i += kThreads) {
+      const float c = qclamp(to_f32<T>(x[i]), inv);
+      q[i] = (unsigned char)(__builtin_amdgcn_cvt_pk_fp8_f32(c, c, 0, false) & 0xff);
+    }
+  }
+}
+
+// Wave-per-row variant (the vector path): each 64-lane wave owns rows r = 4*block + wave (grid
+// stride), reads the row as lane-contiguous 16-byte chunks (one wave instruction = 1 KiB), reduces
+// amax with wave shuffles only (no LDS, no block barrier), and converts.  NREG > 0: the row's
+// chunks stay in registers between the two passes (rows of at most 64 * NREG chunks: 4096 bf16 /
+// 2048 fp32 elements at NREG = 8) — one read of the row; NREG == 0: the second pass re-reads it
+// (from L2: the wave has just streamed it).  Same arithmetic, same bits as the block-per-row
+// kernel: amax = max|x|, inv = 448/amax, e4m3(RNE(clamp(x*inv))), scale = amax/448.
+template <typename T, int NREG>
+__global__ __launch_bounds__(kThreads) void fp8_quantize_rows_wave_kernel(
+    const T* __restrict__ src, unsigned char* __restrict__ dst, float* __restrict__ scales,
+    int64_t rows, int64_t row_len) {
+#pragma clang fp contract(off)
+  constexpr int E = 16 / int(sizeof(T));  // elements per 16-byte chunk
+  constexpr int R = NREG > 0 ? NREG : 1;
+  const int lane = threadIdx.x & 63;
+  const int64_t wpb = kThreads / 64;
+  for (int64_t r = int64_t(blockIdx.x) * wpb + (threadIdx.x >> 6); r < rows;
+       r += int64_t(gridDim.x) * wpb) {
+    const gptr<const T> x = glob(src + r * row_len);
+    const gptr<unsigned char> q = glob(dst + r * row_len);
+    auto unpack = [](const uint4& raw, float* v) {
+      if constexpr (sizeof(T) == 2) {
+        const unsigned short* h = reinterpret_cast<const unsigned short*>(&raw);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = bf16_to_f32(h[j]);
-        } else {
-          const float4 a = *reinterpret_cast<gptr<const float4>>(x + i);
-          const float4 b = *reinterpret_cast<gptr<const float4>>(x + i + 4);
-          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-          v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-        }
+        for (int j = 0; j < 8; ++j) v[j] = bf16_to_f32(h[j]);
+      } else {
+        v[0] = __uint_as_float(raw.x); v[1] = __uint_as_float(raw.y);
+        v[2] = __uint_as_float(raw.z); v[3] = __uint_as_float(raw.w);
+      }
+    };
+    float amax = 0.0f;
+    uint4 keep[R];
+    if constexpr (NREG > 0) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {  // every load issued before any max
+        const int64_t i = (int64_t(u) * 64 + lane) * E;
+        keep[u] = i < row_len ? nt_ld16(x + i) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        float v[E];
+        unpack(keep[u], v);
+#pragma unroll
+        for (int j = 0; j < E; ++j) amax = fmaxf(amax, fabsf(v[j]));
+      }
+    } else {
+      for (int64_t i = int64_t(lane) * E; i < row_len; i += 64 * E) {
+        float v[E];
+        unpack(*reinterpret_cast<gptr<const uint4>>(x + i), v);
+#pragma unroll
+        for (int j = 0; j < E; ++j) amax = fmaxf(amax, fabsf(v[j]));
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+    const float inv = amax > 0.0f ? kE4M3Max / amax : 1.0f;
+    if (lane == 0) glob(scales)[r] = amax > 0.0f ? amax / kE4M3Max : 1.0f;
+    auto emit = [&](int64_t i, const uint4& raw) {
+      float v[E];
+      unpack(raw, v);
+      if constexpr (sizeof(T) == 2) {
         uint2 out;
         out.x = e4m3x4(qclamp(v[0], inv), qclamp(v[1], inv), qclamp(v[2], inv), qclamp(v[3], inv));
         out.y = e4m3x4(qclamp(v[4], inv), qclamp(v[5], inv), qclamp(v[6], inv), qclamp(v[7], inv));
-        *reinterpret_cast<gptr<uint2>>(q + i) = out;
+        nt_st8(q + i, out);
+      } else {
+        *reinterpret_cast<gptr<uint32_t>>(q + i) =
+            e4m3x4(qclamp(v[0], inv), qclamp(v[1], inv), qclamp(v[2], inv), qclamp(v[3], inv));
+      }
+    };
+    if constexpr (NREG > 0) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const int64_t i = (int64_t(u) * 64 + lane) * E;
+        if (i < row_len) emit(i, keep[u]);
       }
     } else {
-      for (int64_t i = threadIdx.x; i < row_len; i += kThreads) {
-        const float c = qclamp(to_f32<T>(x[i]), inv);
-        q[i] = (unsigned char)(__builtin_amdgcn_cvt_pk_fp8_f32(c, c, 0, false) & 0xff);
+      for (int64_t i = int64_t(lane) * E; i < row_len; i += 64 * E)
+        emit(i, *reinterpret_cast<gptr<const uint4>>(x + i));
+    }
+  }
+}
+
+// Wave-per-row dequantise (the vector path): one scale load per row, 8 fp8 bytes -> 8 outputs per
+// lane per step (no per-element row division).
+template <typename T>
+__global__ __launch_bounds__(kThreads) void fp8_dequantize_rows_wave_kernel(
+    const unsigned char* __restrict__ src, const float* __restrict__ scales, T* __restrict__ dst,
+    int64_t rows, int64_t row_len) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63;
+  const int64_t wpb = kThreads / 64;
+  for (int64_t r = int64_t(blockIdx.x) * wpb + (threadIdx.x >> 6); r < rows;
+       r += int64_t(gridDim.x) * wpb) {
+    const gptr<const unsigned char> q = glob(src + r * row_len);
+    const gptr<T> y = glob(dst + r * row_len);
+    const float sc = glob(scales)[r];
+    for (int64_t i = int64_t(lane) * 8; i < row_len; i += 64 * 8) {
+      const uint2 raw = nt_ld8(q + i);
+      const int lo = int(raw.x), hi = int(raw.y);
+      float v[8] = {__builtin_amdgcn_cvt_f32_fp8(lo, 0) * sc, __builtin_amdgcn_cvt_f32_fp8(lo, 1) * sc,
+                    __builtin_amdgcn_cvt_f32_fp8(lo, 2) * sc, __builtin_amdgcn_cvt_f32_fp8(lo, 3) * sc,
+                    __builtin_amdgcn_cvt_f32_fp8(hi, 0) * sc, __builtin_amdgcn_cvt_f32_fp8(hi, 1) * sc,
+                    __builtin_amdgcn_cvt_f32_fp8(hi, 2) * sc, __builtin_amdgcn_cvt_f32_fp8(hi, 3) * sc};
+      if constexpr (sizeof(T) == 2) {
+        uint32_t w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          w[j] = uint32_t(f32_to_bf16(v[2 * j])) | (uint32_t(f32_to_bf16(v[2 * j + 1])) << 16);
+        nt_st16(y + i, make_uint4(w[0], w[1], w[2], w[3]));
+      } else {
+        st4(reinterpret_cast<float*>(y + i), 0, make_float4(v[0], v[1], v[2], v[3]));
+        st4(reinterpret_cast<float*>(y + i), 4, make_float4(v[4], v[5], v[6], v[7]));
       }
     }
   }
 }
 
-// Grid-stride over 8-element groups (VEC) or elements; a group never straddles rows (row_len % 8
-// == 0 in the VEC instantiation).
-template <typename T, bool VEC>
+// Scalar fallback for any row length and alignment: grid-stride over elements.
+template <typename T>
 __global__ __launch_bounds__(kThreads) void fp8_dequantize_rows_kernel(
     const unsigned char* __restrict__ src, const float* __restrict__ scales, T* __restrict__ dst,
     int64_t n, int64_t row_len) {
@@ -534,32 +610,9 @@ __global__ __launch_bounds__(kThreads) void fp8_dequantize_rows_kernel(
   const gptr<const unsigned char> q = glob(src);
   const gptr<T> y = glob(dst);
   const int64_t stride = int64_t(gridDim.x) * kThreads;
-  if constexpr (VEC) {
-    for (int64_t g = int64_t(blockIdx.x) * kThreads + threadIdx.x; g < n / 8; g += stride) {
-      const int64_t i = g * 8;
-      const float sc = glob(scales)[i / row_len];
-      const uint2 raw = *reinterpret_cast<gptr<const uint2>>(q + i);
-      const int lo = int(raw.x), hi = int(raw.y);
-      float v[8] = {__builtin_amdgcn_cvt_f32_fp8(lo, 0) * sc, __builtin_amdgcn_cvt_f32_fp8(lo, 1) * sc,
-                    __builtin_amdgcn_cvt_f32_fp8(lo, 2) * sc, __builtin_amdgcn_cvt_f32_fp8(lo, 3) * sc,
-                    __builtin_amdgcn_cvt_f32_fp8(hi, 0) * sc, __builtin_amdgcn_cvt_f32_fp8(hi, 1) * sc,
-                    __builtin_amdgcn_cvt_f32_fp8(hi, 2) * sc, __builtin_amdgcn_cvt_f32_fp8(hi, 3) * sc};
-      if constexpr (sizeof(T) == 2) {
-        uint4 o;
-        unsigned short* h = reinterpret_cast<unsigned short*>(&o);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) h[j] = f32_to_bf16(v[j]);
-        *reinterpret_cast<gptr<uint4>>(y + i) = o;
-      } else {
-        *reinterpret_cast<gptr<float4>>(y + i) = make_float4(v[0], v[1], v[2], v[3]);
-        *reinterpret_cast<gptr<float4>>(y + i + 4) = make_float4(v[4], v[5], v[6], v[7]);
-      }
-    }
-  } else {
-    for (int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x; i < n; i += stride) {
-      const float v = __builtin_amdgcn_cvt_f32_fp8(int(q[i]), 0) * glob(scales)[i / row_len];
-      y[i] = from_f32<T>(v);
-    }
+  for (int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x; i < n; i += stride) {
+    const float v = __builtin_amdgcn_cvt_f32_fp8(int(q[i]), 0) * glob(scales)[i / row_len];
+    y[i] = from_f32<T>(v);
   }
 }
 
@@ -791,17 +844,29 @@ int zs_fp8_quantize_rows(const void* src, int src_dtype, void* dst, float* scale
   if (rows == 0 || row_len == 0) return ZS_OK;
   ZS_REQUIRE(src && dst && scales, "zs_fp8_quantize_rows: NULL buffer");
   const bool vec = row_len % 8 == 0 && aligned(uint64_t(src), 16) && aligned(uint64_t(dst), 8);
-  const int grid = int(std::min<int64_t>(rows, grid_cap()));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   unsigned char* q = static_cast<unsigned char*>(dst);
-  if (src_dtype == ZS_F32) {
-    const float* x = static_cast<const float*>(src);
-    if (vec) hipLaunchKernelGGL((fp8_quantize_rows_kernel<float, true>), dim3(grid), dim3(kThreads), 0, st, x, q, scales, rows, row_len);
-    else hipLaunchKernelGGL((fp8_quantize_rows_kernel<float, false>), dim3(grid), dim3(kThreads), 0, st, x, q, scales, rows, row_len);
-  } else {
-    const unsigned short* x = static_cast<const unsigned short*>(src);
-    if (vec) hipLaunchKernelGGL((fp8_quantize_rows_kernel<unsigned short, true>), dim3(grid), dim3(kThreads), 0, st, x, q, scales, rows, row_len);
-    else hipLaunchKernelGGL((fp8_quantize_rows_kernel<unsigned short, false>), dim3(grid), dim3(kThreads), 0, st, x, q, scales, rows, row_len);
+  if (vec) {  // wave per row, 4 rows per workgroup
+    const int grid = int(std::min<int64_t>((rows + 3) / 4, grid_cap()));
+    if (src_dtype == ZS_F32) {
+      const float* x = static_cast<const float*>(src);
+      if (row_len <= 64 * 4 * 8)
+        hipLaunchKernelGGL((fp8_quantize_rows_wave_kernel<float, 8>), dim3(grid), dim3(kThreads), 0, st, x, q, scales, rows, row_len);
+      else
+        hipLaunchKernelGGL((fp8_quantize_rows_wave_kernel<float, 0>), dim3(grid), dim3(kThreads), 0, st, x, q, scales, rows, row_len);
+    } else {
+      const unsigned short* x = static_cast<const unsigned short*>(src);
+      if (row_len <= 64 * 8 * 8)
+        hipLaunchKernelGGL((fp8_quantize_rows_wave_kernel<unsigned short, 8>), dim3(grid), dim3(kThreads), 0, st, x, q, scales, rows, row_len);
+      else
+        hipLaunchKernelGGL((fp8_quantize_rows_wave_kernel<unsigned short, 0>), dim3(grid), dim3(kThreads), 0, st, x, q, scales, rows, row_len);
+    }
+  } else {  // any row length / alignment: block per row, scalar accesses
+    const int grid = int(std::min<int64_t>(rows, grid_cap()));
+    if (src_dtype == ZS_F32)
+      hipLaunchKernelGGL((fp8_quantize_rows_kernel<float>), dim3(grid), dim3(kThreads), 0, st, static_cast<const float*>(src), q, scales, rows, row_len);
+    else
+      hipLaunchKernelGGL((fp8_quantize_rows_kernel<unsigned short>), dim3(grid), dim3(kThreads), 0, st, static_cast<const unsigned short*>(src), q, scales, rows, row_len);
   }
   ZS_HIP(hipGetLastError());
   return ZS_OK;
@@ -816,19 +881,20 @@ int zs_fp8_dequantize_rows(const void* src, const float* scales, void* dst, int 
   ZS_REQUIRE(src && dst && scales, "zs_fp8_dequantize_rows: NULL buffer");
   const int64_t n = rows * row_len;
   const bool vec = row_len % 8 == 0 && aligned(uint64_t(src), 8) && aligned(uint64_t(dst), 16);
-  const int64_t work = vec ? n / 8 : n;
-  const int grid = int(std::min<int64_t>(std::max<int64_t>(1, (work + kThreads - 1) / kThreads),
-                                         grid_cap()));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const unsigned char* q = static_cast<const unsigned char*>(src);
-  if (dst_dtype == ZS_F32) {
-    float* y = static_cast<float*>(dst);
-    if (vec) hipLaunchKernelGGL((fp8_dequantize_rows_kernel<float, true>), dim3(grid), dim3(kThreads), 0, st, q, scales, y, n, row_len);
-    else hipLaunchKernelGGL((fp8_dequantize_rows_kernel<float, false>), dim3(grid), dim3(kThreads), 0, st, q, scales, y, n, row_len);
+  if (vec) {  // wave per row, 4 rows per workgroup
+    const int grid = int(std::min<int64_t>((rows + 3) / 4, grid_cap()));
+    if (dst_dtype == ZS_F32)
+      hipLaunchKernelGGL((fp8_dequantize_rows_wave_kernel<float>), dim3(grid), dim3(kThreads), 0, st, q, scales, static_cast<float*>(dst), rows, row_len);
+    else
+      hipLaunchKernelGGL((fp8_dequantize_rows_wave_kernel<unsigned short>), dim3(grid), dim3(kThreads), 0, st, q, scales, static_cast<unsigned short*>(dst), rows, row_len);
   } else {
-    unsigned short* y = static_cast<unsigned short*>(dst);
-    if (vec) hipLaunchKernelGGL((fp8_dequantize_rows_kernel<unsigned short, true>), dim3(grid), dim3(kThreads), 0, st, q, scales, y, n, row_len);
-    else hipLaunchKernelGGL((fp8_dequantize_rows_kernel<unsigned short, false>), dim3(grid), dim3(kThreads), 0, st, q, scales, y, n, row_len);
+    const int grid = int(std::min<int64_t>(std::max<int64_t>(1, (n + kThreads - 1) / kThreads), grid_cap()));
+    if (dst_dtype == ZS_F32)
+      hipLaunchKernelGGL((fp8_dequantize_rows_kernel<float>), dim3(grid), dim3(kThreads), 0, st, q, scales, static_cast<float*>(dst), n, row_len);
+    else
+      hipLaunchKernelGGL((fp8_dequantize_rows_kernel<unsigned short>), dim3(grid), dim3(kThreads), 0, st, q, scales, static_cast<unsigned short*>(dst), n, row_len);
   }
   ZS_HIP(hipGetLastError());
   return ZS_OK;

@@ -34,7 +34,10 @@ def _port():
     return free_port()
 
 
-@pytest.mark.parametrize("rows,row_len", [(5, 64), (3, 37), (17, 12800), (4, 8), (1, 11008)])
+# (the vector path keeps rows of <= 4096 bf16 / 2048 fp32 elements in registers, longer rows are
+# read twice; 37 takes the scalar fallback)
+@pytest.mark.parametrize("rows,row_len", [(5, 64), (3, 37), (17, 12800), (4, 8), (1, 11008),
+                                          (9, 4096), (6, 2048), (5, 14336), (7, 4104)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_fp8_rows_kernels_bit_exact(gpu, rows, row_len, dtype):
     from zero_amd import _lib
