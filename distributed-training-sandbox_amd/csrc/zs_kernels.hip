@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -23,7 +24,9 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int64_t kCopyChunkBytes = int64_t(kThreads) * 16 * 4;  // 16 KiB per workgroup step
+// segment copy: U 16-byte accesses in flight per lane, a workgroup step moves 256 * 16 * U bytes
+constexpr int kCopyUnrollDefault = 4;
+constexpr int64_t copy_chunk_bytes(int u) { return int64_t(kThreads) * 16 * u; }
 // float4 groups per thread: 2 (2048-element chunks); 4 (4096) for the split master, whose 26 B/elem
 // stream has one fp32 array fewer in flight per group (+1 % measured, profiles/r01_adam_split_master.log)
 constexpr int adam_groups(bool split) { return split ? 4 : 2; }
@@ -93,27 +96,29 @@ struct CopySeg {
   int64_t vec;  // 1 if src and dst are 16-byte aligned (or src is null and dst aligned)
 };
 
+template <int U>
 __global__ __launch_bounds__(kThreads) void copy_segments_kernel(
     const CopySeg* __restrict__ segs, const int64_t* __restrict__ chunk_prefix, int64_t nseg,
     int64_t total_chunks) {
+  constexpr int64_t kChunk = copy_chunk_bytes(U);
   int64_t seg = 0;
   for (int64_t c = blockIdx.x; c < total_chunks; c += gridDim.x) {
     while (chunk_prefix[seg + 1] <= c) ++seg;  // uniform forward scan
     const CopySeg s = segs[seg];
-    const int64_t b0 = (c - chunk_prefix[seg]) * kCopyChunkBytes;
-    const int64_t b1 = min(b0 + kCopyChunkBytes, s.nbytes);
+    const int64_t b0 = (c - chunk_prefix[seg]) * kChunk;
+    const int64_t b1 = min(b0 + kChunk, s.nbytes);
     const gptr<const unsigned char> src = glob(s.src);
     const gptr<unsigned char> dst = glob(s.dst);
     if (s.vec) {
-      uint4 val[4];
+      uint4 val[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {  // all loads first: 4 x 16 B in flight per lane
+      for (int u = 0; u < U; ++u) {  // all loads first: U x 16 B in flight per lane
         const int64_t off = b0 + (int64_t(u) * kThreads + threadIdx.x) * 16;
         val[u] = make_uint4(0, 0, 0, 0);
         if (src && off + 16 <= b1) val[u] = nt_ld16(s.src + off);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int64_t off = b0 + (int64_t(u) * kThreads + threadIdx.x) * 16;
         if (off + 16 <= b1) {
           nt_st16(s.dst + off, val[u]);
@@ -624,7 +629,19 @@ struct zs_copyset {
   CopySeg* d_segs = nullptr;
   int64_t* d_prefix = nullptr;
   int64_t nseg = 0, total_chunks = 0;
+  int unroll = kCopyUnrollDefault;  // 16-B accesses in flight per lane (chunk = 4 KiB * unroll)
 };
+
+// ZERO_AMD_COPY_UNROLL (diagnostic A/B): 2, 4 (default) or 8 accesses in flight per lane.
+static int copy_unroll() {
+  static int u = 0;
+  if (u == 0) {
+    const char* e = std::getenv("ZERO_AMD_COPY_UNROLL");
+    const int v = e ? std::atoi(e) : kCopyUnrollDefault;
+    u = (v == 2 || v == 4 || v == 8) ? v : kCopyUnrollDefault;
+  }
+  return u;
+}
 
 struct zs_adamset {
   // vector table (aligned, n % 4 == 0) and scalar table (tails, unaligned segments)
@@ -743,6 +760,8 @@ int zs_copyset_create(const uint64_t* src, const uint64_t* dst, const int64_t* n
   ZS_REQUIRE(n == 0 || (src && dst && nbytes), "zs_copyset_create: NULL table");
   std::vector<CopySeg> segs;
   std::vector<int64_t> prefix(1, 0);
+  const int unroll = copy_unroll();
+  const int64_t chunk = copy_chunk_bytes(unroll);
   for (int64_t i = 0; i < n; ++i) {
     ZS_REQUIRE(nbytes[i] >= 0, "zs_copyset_create: nbytes[%lld] < 0", (long long)i);
     if (nbytes[i] == 0) continue;
@@ -753,12 +772,13 @@ int zs_copyset_create(const uint64_t* src, const uint64_t* dst, const int64_t* n
     s.nbytes = nbytes[i];
     s.vec = aligned(src[i], 16) && aligned(dst[i], 16) ? 1 : 0;
     segs.push_back(s);
-    prefix.push_back(prefix.back() + (nbytes[i] + kCopyChunkBytes - 1) / kCopyChunkBytes);
+    prefix.push_back(prefix.back() + (nbytes[i] + chunk - 1) / chunk);
   }
   zs_copyset* cs = new (std::nothrow) zs_copyset();
   if (!cs) return zs::fail(ZS_ERR_NOMEM, "zs_copyset_create: out of memory");
   cs->nseg = int64_t(segs.size());
   cs->total_chunks = prefix.back();
+  cs->unroll = unroll;
   int rc = upload(segs, &cs->d_segs);
   if (rc == ZS_OK) rc = upload(prefix, &cs->d_prefix);
   if (rc != ZS_OK) {
@@ -773,9 +793,16 @@ int zs_copyset_run(const zs_copyset* cs, uintptr_t stream) {
   ZS_REQUIRE(cs != nullptr, "zs_copyset_run: NULL set");
   if (cs->total_chunks == 0) return ZS_OK;
   const int grid = int(std::min<int64_t>(cs->total_chunks, grid_cap()));
-  hipLaunchKernelGGL(copy_segments_kernel, dim3(grid), dim3(kThreads), 0,
-                     reinterpret_cast<hipStream_t>(stream), cs->d_segs, cs->d_prefix, cs->nseg,
-                     cs->total_chunks);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (cs->unroll == 8)
+    hipLaunchKernelGGL(copy_segments_kernel<8>, dim3(grid), dim3(kThreads), 0, st, cs->d_segs,
+                       cs->d_prefix, cs->nseg, cs->total_chunks);
+  else if (cs->unroll == 2)
+    hipLaunchKernelGGL(copy_segments_kernel<2>, dim3(grid), dim3(kThreads), 0, st, cs->d_segs,
+                       cs->d_prefix, cs->nseg, cs->total_chunks);
+  else
+    hipLaunchKernelGGL(copy_segments_kernel<4>, dim3(grid), dim3(kThreads), 0, st, cs->d_segs,
+                       cs->d_prefix, cs->nseg, cs->total_chunks);
   ZS_HIP(hipGetLastError());
   return ZS_OK;
 }
