@@ -201,6 +201,7 @@ class _GatherRuntime:
             self.launch(key, self.key_managers.get(key), cur)
 
     def materialize(self, key, managers):
+        cur = torch.cuda.current_stream(self.device)
         if self.recording:
             self.sequence.append(key)
         else:
@@ -208,10 +209,9 @@ class _GatherRuntime:
                 self.pos += 1
             elif key in self.sequence[self.pos:]:
                 self.pos = self.sequence.index(key, self.pos) + 1
-            self._prefetch(self.pos)  # the next group, while this one computes
+            self._prefetch(self.pos, cur)  # the next group, while this one computes
         if key in self.pending:
             self.n_prefetch_hits += 1
-        cur = torch.cuda.current_stream(self.device)
         self.launch(key, managers, cur)
         out, ev, hold = self.pending.pop(key)
         if ev is None:  # ws == 1

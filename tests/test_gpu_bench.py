@@ -35,6 +35,20 @@ def test_bench_json_line_n1(gpu):
     assert KEYS <= set(out) and out["n_gpus"] == 1 and out["value"] > 0
     rf = out["roofline"]
     assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1.2 and rf["achieved"] > 0
+    assert "fp32_master" not in out  # fp32 parameters: the master is the parameter
+
+
+def test_bench_fp32_master_line_beside_split_headline(gpu):
+    """bf16 parameters at N=1: the split-master line carries the same step with the exact fp32
+    master beside it (VERDICT r2 weak #8), measured after the headline's timed region."""
+    out = _run([sys.executable, "bench.py", "--config", "C2", "--steps", "3", "--warmup", "1",
+                "--no-cpu-baseline"])
+    assert out["config"]["master"] == "split"
+    fm = out["fp32_master"]
+    assert out["fp32_master_ms_per_step"] == fm["ms_per_step"] > 0 and fm["steps"] == 3
+    # 28 vs 26 B per element over the same elements
+    ratio = fm["alg_bytes_per_launch"] / out["roofline"]["alg_bytes_per_launch"]
+    assert abs(ratio - 28 / 26) < 1e-3, ratio
 
 
 def test_bench_harness_two_ranks_gloo_staged(gpu):
