@@ -360,69 +360,98 @@ __device__ __forceinline__ T from_f32(float x) {
   else return f32_to_bf16(x);
 }
 
-// 16 B per lane per access; the tail (n % (16/sizeof(T))) is done by the first lanes of block 0.
+// In place, kScaleU 16-B accesses per lane in flight: a wave step covers kScaleU contiguous 1 KiB
+// blocks (lane l of block u at 16-B chunk 64u + l), every load issued before the first store;
+// default cache policy (not non-temporal): a DDP bucket (64 MiB) is scaled right after the
+// all-reduce wrote it, while it is still in the 256 MB MALL; grid-stride over wave steps; the tail
+// (n % elements per step) by block 0.
+// (Round 2's one access in flight per lane measured 0.61 of 8 TB/s on a 4 GiB buffer.)
 // fp32: IEEE division (x / div), or an exact reciprocal multiply when div is a power of two;
 // bf16: the same in fp32, rounded to bf16 (RNE) — torch's div_ on a bf16 tensor.
+constexpr int kScaleU = 4;
+
 template <typename T>
 __global__ __launch_bounds__(kThreads) void scale_kernel(T* __restrict__ x, int64_t n, float div,
                                                          float inv, int pow2) {
 #pragma clang fp contract(off)
   constexpr int V = 16 / sizeof(T);
+  constexpr int64_t kSpan = int64_t(64) * V * kScaleU;  // elements per wave step
   const gptr<T> gx = glob(x);
-  const int64_t nv = n / V;
+  const int64_t steps = n / kSpan;
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = int64_t(gridDim.x) * (kThreads / 64);
   auto op = [&](float f) { return pow2 ? f * inv : f / div; };
-  for (int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x; i < nv;
-       i += int64_t(gridDim.x) * kThreads) {
-    uint4 raw = *reinterpret_cast<gptr<const uint4>>(gx + i * V);
-    T* e = reinterpret_cast<T*>(&raw);
+  for (int64_t w = int64_t(blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6); w < steps;
+       w += nwaves) {
+    T* base = x + w * kSpan + int64_t(lane) * V;
+    uint4 raw[kScaleU];
 #pragma unroll
-    for (int j = 0; j < V; ++j) e[j] = from_f32<T>(op(to_f32<T>(e[j])));
-    *reinterpret_cast<gptr<uint4>>(gx + i * V) = raw;
+    for (int u = 0; u < kScaleU; ++u) raw[u] = *reinterpret_cast<gptr<const uint4>>(glob(base + u * 64 * V));
+#pragma unroll
+    for (int u = 0; u < kScaleU; ++u) {
+      T* e = reinterpret_cast<T*>(&raw[u]);
+#pragma unroll
+      for (int j = 0; j < V; ++j) e[j] = from_f32<T>(op(to_f32<T>(e[j])));
+      *reinterpret_cast<gptr<uint4>>(glob(base + u * 64 * V)) = raw[u];
+    }
   }
   if (blockIdx.x == 0) {
-    const int64_t i = nv * V + threadIdx.x;
-    if (i < n) gx[i] = from_f32<T>(op(to_f32<T>(gx[i])));
+    for (int64_t i = steps * kSpan + threadIdx.x; i < n; i += kThreads)
+      gx[i] = from_f32<T>(op(to_f32<T>(gx[i])));
   }
 }
 
 // ----------------------------------------------------------------------------------------------
 // fp32 <-> bf16 conversion (the bf16 gradient exchange of fp32-parameter models)
 // ----------------------------------------------------------------------------------------------
-// 8 elements per lane per iteration: 32 B of fp32 (two 16-B loads) <-> 16 B of bf16 (one 16-B
-// store), non-temporal (each byte is touched once); grid-stride; the n % 8 tail by block 0.
+// Wave-dense accesses: a wave step covers kConvSpan elements in kConvU blocks of 256; in block u
+// lane l converts elements [256u + 4l, +4) — one 16-B fp32 access and one 8-B bf16 access per
+// block, so every wave instruction touches one contiguous 1 KiB (fp32) or 512 B (bf16) span.
+// (Round 2's lane-contiguous 8 elements per lane gave each fp32 instruction a 32-B lane stride —
+// half-dense — and measured 0.58 of 8 TB/s bf16 -> fp32, profiles/r03_kernels_table.json.)
+// All kConvU loads are issued before the first store; non-temporal (each byte is touched once);
+// grid-stride over wave steps; the n % kConvSpan tail by block 0.
 // fp32 -> bf16 rounds to nearest even (v_cvt_pk_bf16_f32), NaN stays NaN; bf16 -> fp32 is exact.
+constexpr int kConvU = 4;
+constexpr int64_t kConvSpan = 256 * kConvU;
+
 template <bool TO_BF16>
 __global__ __launch_bounds__(kThreads) void convert_kernel(const void* __restrict__ src,
                                                            void* __restrict__ dst, int64_t n) {
-  const int64_t n8 = n / 8;
-  const int64_t stride = int64_t(gridDim.x) * kThreads;
-  for (int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x; i < n8; i += stride) {
+  const int64_t steps = n / kConvSpan;
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = int64_t(gridDim.x) * (kThreads / 64);
+  for (int64_t w = int64_t(blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6); w < steps;
+       w += nwaves) {
+    const int64_t base = w * kConvSpan + 4 * lane;
     if constexpr (TO_BF16) {
-      const float* s = static_cast<const float*>(src) + i * 8;
-      const float4 a = ld4(s, 0), b = ld4(s, 4);
-      const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-      uint32_t w[4];
+      const float* s = static_cast<const float*>(src) + base;
+      float4 a[kConvU];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        w[j] = uint32_t(f32_to_bf16(v[2 * j])) | (uint32_t(f32_to_bf16(v[2 * j + 1])) << 16);
-      nt_st16(static_cast<unsigned short*>(dst) + i * 8, make_uint4(w[0], w[1], w[2], w[3]));
-    } else {
-      const uint4 h = nt_ld16(static_cast<const unsigned short*>(src) + i * 8);
-      const uint32_t w[4] = {h.x, h.y, h.z, h.w};
-      float v[8];
+      for (int u = 0; u < kConvU; ++u) a[u] = ld4(s, 256 * u);
+      unsigned short* d = static_cast<unsigned short*>(dst) + base;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[2 * j] = __uint_as_float(w[j] << 16);
-        v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+      for (int u = 0; u < kConvU; ++u) {
+        const uint32_t lo = uint32_t(f32_to_bf16(a[u].x)) | (uint32_t(f32_to_bf16(a[u].y)) << 16);
+        const uint32_t hi = uint32_t(f32_to_bf16(a[u].z)) | (uint32_t(f32_to_bf16(a[u].w)) << 16);
+        nt_st8(d + 256 * u, make_uint2(lo, hi));
       }
-      float* d = static_cast<float*>(dst) + i * 8;
-      st4(d, 0, make_float4(v[0], v[1], v[2], v[3]));
-      st4(d, 4, make_float4(v[4], v[5], v[6], v[7]));
+    } else {
+      const unsigned short* s = static_cast<const unsigned short*>(src) + base;
+      uint2 h[kConvU];
+#pragma unroll
+      for (int u = 0; u < kConvU; ++u) h[u] = nt_ld8(s + 256 * u);
+      float* d = static_cast<float*>(dst) + base;
+#pragma unroll
+      for (int u = 0; u < kConvU; ++u)
+        st4(d, 256 * u, make_float4(__uint_as_float(h[u].x << 16),
+                                    __uint_as_float(h[u].x & 0xffff0000u),
+                                    __uint_as_float(h[u].y << 16),
+                                    __uint_as_float(h[u].y & 0xffff0000u)));
     }
   }
   if (blockIdx.x == 0) {
-    const int64_t i = n8 * 8 + threadIdx.x;
-    if (i < n) {
+    for (int64_t i = steps * kConvSpan + threadIdx.x; i < n; i += kThreads) {
       if constexpr (TO_BF16)
         glob(static_cast<unsigned short*>(dst))[i] = f32_to_bf16(glob(static_cast<const float*>(src))[i]);
       else
@@ -491,52 +520,49 @@ __global__ __launch_bounds__(kThreads) void fp8_quantize_rows_kernel(
 // Wave-per-row variant (the vector path): each 64-lane wave owns rows r = 4*block + wave (grid
 // stride), reads the row as lane-contiguous 16-byte chunks (one wave instruction = 1 KiB), reduces
 // amax with wave shuffles only (no LDS, no block barrier), and converts.  NREG > 0: the row's
-// chunks stay in registers between the two passes (rows of at most 64 * NREG chunks: 4096 bf16 /
-// 2048 fp32 elements at NREG = 8) — one read of the row; NREG == 0: the second pass re-reads it
-// (from L2: the wave has just streamed it).  Same arithmetic, same bits as the block-per-row
-// kernel: amax = max|x|, inv = 448/amax, e4m3(RNE(clamp(x*inv))), scale = amax/448.
+// chunks stay in registers between the two passes (rows of at most 64 * NREG chunks: NREG = 8, 16
+// or 32, i.e. up to 16384 bf16 / 8192 fp32 elements — every row of the C5 set) — one read of the
+// row, all of its loads in flight at once; NREG == 0 (longer rows): both passes stream the row in
+// batches of 8 loads in flight per lane, the second from L2 / MALL where it is still cached.  Same
+// arithmetic, same bits as the block-per-row kernel: amax = max|x|, inv = 448/amax,
+// e4m3(RNE(clamp(x*inv))), scale = amax/448.
 template <typename T, int NREG>
 __global__ __launch_bounds__(kThreads) void fp8_quantize_rows_wave_kernel(
     const T* __restrict__ src, unsigned char* __restrict__ dst, float* __restrict__ scales,
     int64_t rows, int64_t row_len) {
 #pragma clang fp contract(off)
   constexpr int E = 16 / int(sizeof(T));  // elements per 16-byte chunk
-  constexpr int R = NREG > 0 ? NREG : 1;
+  constexpr int R = NREG > 0 ? NREG : 8;  // chunks in flight per lane
   const int lane = threadIdx.x & 63;
   const int64_t wpb = kThreads / 64;
+  auto unpack = [](const uint4& raw, float* v) {
+    if constexpr (sizeof(T) == 2) {
+      const unsigned short* h = reinterpret_cast<const unsigned short*>(&raw);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = bf16_to_f32(h[j]);
+    } else {
+      v[0] = __uint_as_float(raw.x); v[1] = __uint_as_float(raw.y);
+      v[2] = __uint_as_float(raw.z); v[3] = __uint_as_float(raw.w);
+    }
+  };
   for (int64_t r = int64_t(blockIdx.x) * wpb + (threadIdx.x >> 6); r < rows;
        r += int64_t(gridDim.x) * wpb) {
     const gptr<const T> x = glob(src + r * row_len);
     const gptr<unsigned char> q = glob(dst + r * row_len);
-    auto unpack = [](const uint4& raw, float* v) {
-      if constexpr (sizeof(T) == 2) {
-        const unsigned short* h = reinterpret_cast<const unsigned short*>(&raw);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = bf16_to_f32(h[j]);
-      } else {
-        v[0] = __uint_as_float(raw.x); v[1] = __uint_as_float(raw.y);
-        v[2] = __uint_as_float(raw.z); v[3] = __uint_as_float(raw.w);
-      }
+    auto load = [&](int64_t i) {
+      if (i >= row_len) return make_uint4(0, 0, 0, 0);
+      if constexpr (NREG > 0) return nt_ld16(x + i);  // read once
+      else return *reinterpret_cast<gptr<const uint4>>(x + i);  // read again in pass 2
     };
     float amax = 0.0f;
     uint4 keep[R];
-    if constexpr (NREG > 0) {
+    for (int64_t b0 = 0; b0 < row_len; b0 += int64_t(64) * R * E) {  // NREG > 0: one batch
 #pragma unroll
-      for (int u = 0; u < R; ++u) {  // every load issued before any max
-        const int64_t i = (int64_t(u) * 64 + lane) * E;
-        keep[u] = i < row_len ? nt_ld16(x + i) : make_uint4(0, 0, 0, 0);
-      }
+      for (int u = 0; u < R; ++u) keep[u] = load(b0 + (int64_t(u) * 64 + lane) * E);
 #pragma unroll
       for (int u = 0; u < R; ++u) {
         float v[E];
         unpack(keep[u], v);
-#pragma unroll
-        for (int j = 0; j < E; ++j) amax = fmaxf(amax, fabsf(v[j]));
-      }
-    } else {
-      for (int64_t i = int64_t(lane) * E; i < row_len; i += 64 * E) {
-        float v[E];
-        unpack(*reinterpret_cast<gptr<const uint4>>(x + i), v);
 #pragma unroll
         for (int j = 0; j < E; ++j) amax = fmaxf(amax, fabsf(v[j]));
       }
@@ -565,42 +591,68 @@ __global__ __launch_bounds__(kThreads) void fp8_quantize_rows_wave_kernel(
         if (i < row_len) emit(i, keep[u]);
       }
     } else {
-      for (int64_t i = int64_t(lane) * E; i < row_len; i += 64 * E)
-        emit(i, *reinterpret_cast<gptr<const uint4>>(x + i));
+      for (int64_t b0 = 0; b0 < row_len; b0 += int64_t(64) * R * E) {
+#pragma unroll
+        for (int u = 0; u < R; ++u) keep[u] = load(b0 + (int64_t(u) * 64 + lane) * E);
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+          const int64_t i = b0 + (int64_t(u) * 64 + lane) * E;
+          if (i < row_len) emit(i, keep[u]);
+        }
+      }
     }
   }
 }
 
-// Wave-per-row dequantise (the vector path): one scale load per row, 8 fp8 bytes -> 8 outputs per
-// lane per step (no per-element row division).
+// Dequantise (the vector path): work items are (row, segment) pairs — a segment is kDqU wave
+// accesses of E elements per lane (E = 8 for bf16 output: an 8-B fp8 load and a 16-B store per
+// lane; E = 4 for fp32: 4 B -> 16 B), so every store instruction covers one contiguous 1 KiB and
+// a short matrix (1024 rows of a k/v projection) still spreads over every SIMD.  All kDqU loads
+// are issued before the first store; the row's scale is loaded once per item.
+constexpr int kDqU = 4;
+
 template <typename T>
 __global__ __launch_bounds__(kThreads) void fp8_dequantize_rows_wave_kernel(
     const unsigned char* __restrict__ src, const float* __restrict__ scales, T* __restrict__ dst,
     int64_t rows, int64_t row_len) {
 #pragma clang fp contract(off)
+  constexpr int E = sizeof(T) == 2 ? 8 : 4;
+  constexpr int64_t SEG = int64_t(64) * E * kDqU;
   const int lane = threadIdx.x & 63;
-  const int64_t wpb = kThreads / 64;
-  for (int64_t r = int64_t(blockIdx.x) * wpb + (threadIdx.x >> 6); r < rows;
-       r += int64_t(gridDim.x) * wpb) {
+  const int64_t per_row = (row_len + SEG - 1) / SEG;
+  const int64_t items = rows * per_row;
+  const int64_t nwaves = int64_t(gridDim.x) * (kThreads / 64);
+  for (int64_t it = int64_t(blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6); it < items;
+       it += nwaves) {
+    const int64_t r = it / per_row;
+    const int64_t s0 = (it - r * per_row) * SEG;
     const gptr<const unsigned char> q = glob(src + r * row_len);
     const gptr<T> y = glob(dst + r * row_len);
     const float sc = glob(scales)[r];
-    for (int64_t i = int64_t(lane) * 8; i < row_len; i += 64 * 8) {
-      const uint2 raw = nt_ld8(q + i);
-      const int lo = int(raw.x), hi = int(raw.y);
-      float v[8] = {__builtin_amdgcn_cvt_f32_fp8(lo, 0) * sc, __builtin_amdgcn_cvt_f32_fp8(lo, 1) * sc,
-                    __builtin_amdgcn_cvt_f32_fp8(lo, 2) * sc, __builtin_amdgcn_cvt_f32_fp8(lo, 3) * sc,
-                    __builtin_amdgcn_cvt_f32_fp8(hi, 0) * sc, __builtin_amdgcn_cvt_f32_fp8(hi, 1) * sc,
-                    __builtin_amdgcn_cvt_f32_fp8(hi, 2) * sc, __builtin_amdgcn_cvt_f32_fp8(hi, 3) * sc};
-      if constexpr (sizeof(T) == 2) {
-        uint32_t w[4];
+    uint2 raw[kDqU];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          w[j] = uint32_t(f32_to_bf16(v[2 * j])) | (uint32_t(f32_to_bf16(v[2 * j + 1])) << 16);
-        nt_st16(y + i, make_uint4(w[0], w[1], w[2], w[3]));
+    for (int u = 0; u < kDqU; ++u) {
+      const int64_t i = s0 + (int64_t(u) * 64 + lane) * E;
+      raw[u] = make_uint2(0, 0);
+      if (i < row_len) {
+        if constexpr (E == 8) raw[u] = nt_ld8(q + i);
+        else raw[u].x = __builtin_nontemporal_load(reinterpret_cast<gptr<const uint32_t>>(q + i));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kDqU; ++u) {
+      const int64_t i = s0 + (int64_t(u) * 64 + lane) * E;
+      if (i >= row_len) continue;
+      const int lo = int(raw[u].x), hi = int(raw[u].y);
+      const float a0 = __builtin_amdgcn_cvt_f32_fp8(lo, 0) * sc, a1 = __builtin_amdgcn_cvt_f32_fp8(lo, 1) * sc;
+      const float a2 = __builtin_amdgcn_cvt_f32_fp8(lo, 2) * sc, a3 = __builtin_amdgcn_cvt_f32_fp8(lo, 3) * sc;
+      if constexpr (E == 8) {
+        const float b0 = __builtin_amdgcn_cvt_f32_fp8(hi, 0) * sc, b1 = __builtin_amdgcn_cvt_f32_fp8(hi, 1) * sc;
+        const float b2 = __builtin_amdgcn_cvt_f32_fp8(hi, 2) * sc, b3 = __builtin_amdgcn_cvt_f32_fp8(hi, 3) * sc;
+        auto pk = [](float a, float b) { return uint32_t(f32_to_bf16(a)) | (uint32_t(f32_to_bf16(b)) << 16); };
+        nt_st16(y + i, make_uint4(pk(a0, a1), pk(a2, a3), pk(b0, b1), pk(b2, b3)));
       } else {
-        st4(reinterpret_cast<float*>(y + i), 0, make_float4(v[0], v[1], v[2], v[3]));
-        st4(reinterpret_cast<float*>(y + i), 4, make_float4(v[4], v[5], v[6], v[7]));
+        st4(reinterpret_cast<float*>(y + i), 0, make_float4(a0, a1, a2, a3));
       }
     }
   }
@@ -825,8 +877,8 @@ int zs_scale(void* x, int64_t n, int dtype, double div, uintptr_t stream) {
   int e = 0;
   const int pow2 = std::frexp(div, &e) == 0.5 ? 1 : 0;
   const float fdiv = float(div), inv = float(1.0 / div);
-  const int V = dtype == ZS_F32 ? 4 : 8;
-  const int64_t blocks = std::max<int64_t>(1, (n / V + kThreads - 1) / kThreads);
+  const int64_t span = int64_t(64) * kScaleU * (dtype == ZS_F32 ? 4 : 8);  // elements per wave step
+  const int64_t blocks = std::max<int64_t>(1, (n / span + 3) / 4);
   const int grid = int(std::min<int64_t>(blocks, grid_cap()));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (dtype == ZS_F32)
@@ -849,8 +901,9 @@ int zs_convert(const void* src, int src_dtype, void* dst, int dst_dtype, int64_t
   ZS_REQUIRE(src && dst, "zs_convert: NULL buffer");
   const bool to_bf16 = src_dtype == ZS_F32;
   const bool vec = aligned(uint64_t(src), 16) && aligned(uint64_t(dst), 16);
-  const int64_t work = vec ? std::max<int64_t>(1, n / 8) : n;
-  const int grid = int(std::min<int64_t>((work + kThreads - 1) / kThreads, grid_cap()));
+  // vector path: one wave per kConvSpan-element step (4 waves per workgroup)
+  const int64_t work = vec ? std::max<int64_t>(1, (n / kConvSpan + 3) / 4) : (n + kThreads - 1) / kThreads;
+  const int grid = int(std::min<int64_t>(work, grid_cap()));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (vec) {
     if (to_bf16) hipLaunchKernelGGL(convert_kernel<true>, dim3(grid), dim3(kThreads), 0, st, src, dst, n);
@@ -875,19 +928,22 @@ int zs_fp8_quantize_rows(const void* src, int src_dtype, void* dst, float* scale
   unsigned char* q = static_cast<unsigned char*>(dst);
   if (vec) {  // wave per row, 4 rows per workgroup
     const int grid = int(std::min<int64_t>((rows + 3) / 4, grid_cap()));
+    // 16-B chunks per lane the row needs: the smallest register-resident variant that holds it
+    const int64_t chunks = (row_len + 64 * (src_dtype == ZS_F32 ? 4 : 8) - 1) / (64 * (src_dtype == ZS_F32 ? 4 : 8));
+    const int nreg = chunks <= 8 ? 8 : chunks <= 16 ? 16 : chunks <= 32 ? 32 : 0;
+#define ZS_Q(T, N, X) hipLaunchKernelGGL((fp8_quantize_rows_wave_kernel<T, N>), dim3(grid), dim3(kThreads), 0, st, X, q, scales, rows, row_len)
+#define ZS_QSEL(T, X) \
+    switch (nreg) { case 8: ZS_Q(T, 8, X); break; case 16: ZS_Q(T, 16, X); break; \
+                    case 32: ZS_Q(T, 32, X); break; default: ZS_Q(T, 0, X); }
     if (src_dtype == ZS_F32) {
       const float* x = static_cast<const float*>(src);
-      if (row_len <= 64 * 4 * 8)
-        hipLaunchKernelGGL((fp8_quantize_rows_wave_kernel<float, 8>), dim3(grid), dim3(kThreads), 0, st, x, q, scales, rows, row_len);
-      else
-        hipLaunchKernelGGL((fp8_quantize_rows_wave_kernel<float, 0>), dim3(grid), dim3(kThreads), 0, st, x, q, scales, rows, row_len);
+      ZS_QSEL(float, x)
     } else {
       const unsigned short* x = static_cast<const unsigned short*>(src);
-      if (row_len <= 64 * 8 * 8)
-        hipLaunchKernelGGL((fp8_quantize_rows_wave_kernel<unsigned short, 8>), dim3(grid), dim3(kThreads), 0, st, x, q, scales, rows, row_len);
-      else
-        hipLaunchKernelGGL((fp8_quantize_rows_wave_kernel<unsigned short, 0>), dim3(grid), dim3(kThreads), 0, st, x, q, scales, rows, row_len);
+      ZS_QSEL(unsigned short, x)
     }
+#undef ZS_QSEL
+#undef ZS_Q
   } else {  // any row length / alignment: block per row, scalar accesses
     const int grid = int(std::min<int64_t>(rows, grid_cap()));
     if (src_dtype == ZS_F32)
@@ -910,8 +966,10 @@ int zs_fp8_dequantize_rows(const void* src, const float* scales, void* dst, int 
   const bool vec = row_len % 8 == 0 && aligned(uint64_t(src), 8) && aligned(uint64_t(dst), 16);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const unsigned char* q = static_cast<const unsigned char*>(src);
-  if (vec) {  // wave per row, 4 rows per workgroup
-    const int grid = int(std::min<int64_t>((rows + 3) / 4, grid_cap()));
+  if (vec) {  // one wave per (row, segment) item, 4 per workgroup
+    const int64_t seg = int64_t(64) * kDqU * (dst_dtype == ZS_F32 ? 4 : 8);
+    const int64_t items = rows * ((row_len + seg - 1) / seg);
+    const int grid = int(std::min<int64_t>((items + 3) / 4, grid_cap()));
     if (dst_dtype == ZS_F32)
       hipLaunchKernelGGL((fp8_dequantize_rows_wave_kernel<float>), dim3(grid), dim3(kThreads), 0, st, q, scales, static_cast<float*>(dst), rows, row_len);
     else

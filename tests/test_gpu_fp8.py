@@ -34,10 +34,13 @@ def _port():
     return free_port()
 
 
-# (the vector path keeps rows of <= 4096 bf16 / 2048 fp32 elements in registers, longer rows are
-# read twice; 37 takes the scalar fallback)
+# (the vector path keeps rows in registers in 8, 16 or 32 16-B chunks per lane — up to 4096 / 8192
+# / 16384 bf16 or 2048 / 4096 / 8192 fp32 elements — longer rows are streamed twice in batches of 8;
+# 37 takes the scalar fallback; dequantisation items are (row, segment) pairs of 2048 bf16 / 1024
+# fp32 elements, so most row lengths here end in a partial segment)
 @pytest.mark.parametrize("rows,row_len", [(5, 64), (3, 37), (17, 12800), (4, 8), (1, 11008),
-                                          (9, 4096), (6, 2048), (5, 14336), (7, 4104)])
+                                          (9, 4096), (6, 2048), (5, 14336), (7, 4104), (4, 8192),
+                                          (3, 16392), (2, 40968), (1031, 24)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_fp8_rows_kernels_bit_exact(gpu, rows, row_len, dtype):
     from zero_amd import _lib

@@ -392,7 +392,7 @@ def test_pack_unpack_through_plan_bit_exact(gpu, dtype):
             assert torch.equal(o, torch.zeros_like(o) if g is None else g)
 
 
-@pytest.mark.parametrize("n", [1, 7, 8, 1000, 4099, 1 << 20])
+@pytest.mark.parametrize("n", [1, 7, 8, 1000, 1024, 1025, 4099, 3 * 1024 + 517, 1 << 20])
 @pytest.mark.parametrize("offset", [0, 1])
 def test_convert_fp32_bf16_bit_exact(gpu, n, offset):
     """zs_convert fp32 → bf16 is round-to-nearest-even bit for bit (numpy restatement), including

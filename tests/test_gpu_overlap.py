@@ -349,7 +349,8 @@ def test_ddp_sync_gradients(gpu, ws):
     spawn_batch(ws, cases)
 
 
-@pytest.mark.parametrize("n", [1, 7, 1000, 4099, 1 << 20])
+# (a wave step of the vector path covers 1024 fp32 / 2048 bf16 elements; the rest is the tail)
+@pytest.mark.parametrize("n", [1, 7, 1000, 1024, 2051, 4099, 5 * 2048 + 1000, 1 << 20])
 @pytest.mark.parametrize("div", [2.0, 3.0, 8.0, 6.0])
 def test_scale_kernel_bit_exact(gpu, n, div):
     from zero_amd import _lib

@@ -9,8 +9,8 @@ events on the launch stream, achieved GB/s and the fraction of the 8 TB/s HBM pe
   fp8_quantize_rows      one C5 decoder layer's matrices (bf16, row-scaled E4M3, the ZeRO-3
                          gather_dtype="fp8" send side): 2 + 1 B/element + 4 B/row
   fp8_dequantize_rows    the same layer gathered (receive side): 1 + 2 B/element + 4 B/row
-  scale_kernel           DDP's grad /= ws on a 256 MiB bf16 bucket and a 256 MiB fp32 bucket
-                         (in place): 2 x element size per element
+  scale_kernel           DDP's grad /= ws, in place, bf16 and fp32: a 256 MiB bucket (MALL-sized)
+                         and a 4 GiB buffer (HBM): 2 x element size per element
   copy_segments_kernel   pack of the C4 set's grads into one rank-major arena (every tensor a
                          segment, bf16): 2 x 2 B/element
 
@@ -101,15 +101,18 @@ def main():
     del mats, qs, scs, outs
     torch.cuda.empty_cache()
 
-    # DDP scale: one 256 MiB bucket, bf16 and fp32, in place
-    for dt, code, es in ((torch.bfloat16, _lib.ZS_BF16, 2), (torch.float32, _lib.ZS_F32, 4)):
-        m = (256 << 20) // es
-        b = torch.randn(m, device=dev).to(dt)
-        timed(f"scale_kernel<{'bf16' if es == 2 else 'f32'}> (/3, in place)",
-              lambda b=b, code=code: _lib.call("zs_scale", b.data_ptr(), b.numel(), code, 3.0,
-                                               stream_handle(st)),
-              2 * es * m, f"DDP bucket, 256 MiB {dt}")
-        del b
+    # DDP scale, in place: a 256 MiB bucket (fits the 256 MB MALL, so repeated launches partly hit
+    # it — the figure is not an HBM rate) and a 4 GiB buffer (HBM-bound)
+    for mib in (64, 256, 4096):
+        for dt, code, es in ((torch.bfloat16, _lib.ZS_BF16, 2), (torch.float32, _lib.ZS_F32, 4)):
+            m = (mib << 20) // es
+            b = torch.randn(m, device=dev).to(dt)
+            timed(f"scale_kernel<{'bf16' if es == 2 else 'f32'}> (/3, in place, {mib} MiB)",
+                  lambda b=b, code=code: _lib.call("zs_scale", b.data_ptr(), b.numel(), code, 3.0,
+                                                   stream_handle(st)),
+                  2 * es * m, f"DDP bucket, {mib} MiB {dt}" + (" (MALL-resident)" if mib <= 256 else ""))
+            del b
+            torch.cuda.empty_cache()
 
     # pack: the C4 set's bf16 grads (326 segments) into one rank-major arena
     shapes = smollm3_3b_shapes()
