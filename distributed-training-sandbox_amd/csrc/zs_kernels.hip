@@ -526,15 +526,15 @@ __global__ __launch_bounds__(kThreads) void fp8_quantize_rows_kernel(
 // batches of 8 loads in flight per lane, the second from L2 / MALL where it is still cached.  Same
 // arithmetic, same bits as the block-per-row kernel: amax = max|x|, inv = 448/amax,
 // e4m3(RNE(clamp(x*inv))), scale = amax/448.
+// One row, one wave (lane = threadIdx.x & 63): x -> q (row_len elements), *scale.
 template <typename T, int NREG>
-__global__ __launch_bounds__(kThreads) void fp8_quantize_rows_wave_kernel(
-    const T* __restrict__ src, unsigned char* __restrict__ dst, float* __restrict__ scales,
-    int64_t rows, int64_t row_len) {
+__device__ __forceinline__ void fp8_quantize_row(const T* __restrict__ src_row,
+                                                 unsigned char* __restrict__ dst_row,
+                                                 float* __restrict__ scale, int64_t row_len,
+                                                 int lane) {
 #pragma clang fp contract(off)
   constexpr int E = 16 / int(sizeof(T));  // elements per 16-byte chunk
   constexpr int R = NREG > 0 ? NREG : 8;  // chunks in flight per lane
-  const int lane = threadIdx.x & 63;
-  const int64_t wpb = kThreads / 64;
   auto unpack = [](const uint4& raw, float* v) {
     if constexpr (sizeof(T) == 2) {
       const unsigned short* h = reinterpret_cast<const unsigned short*>(&raw);
@@ -545,116 +545,199 @@ __global__ __launch_bounds__(kThreads) void fp8_quantize_rows_wave_kernel(
       v[2] = __uint_as_float(raw.z); v[3] = __uint_as_float(raw.w);
     }
   };
-  for (int64_t r = int64_t(blockIdx.x) * wpb + (threadIdx.x >> 6); r < rows;
-       r += int64_t(gridDim.x) * wpb) {
-    const gptr<const T> x = glob(src + r * row_len);
-    const gptr<unsigned char> q = glob(dst + r * row_len);
-    auto load = [&](int64_t i) {
-      if (i >= row_len) return make_uint4(0, 0, 0, 0);
-      if constexpr (NREG > 0) return nt_ld16(x + i);  // read once
-      else return *reinterpret_cast<gptr<const uint4>>(x + i);  // read again in pass 2
-    };
-    float amax = 0.0f;
-    uint4 keep[R];
-    for (int64_t b0 = 0; b0 < row_len; b0 += int64_t(64) * R * E) {  // NREG > 0: one batch
+  const gptr<const T> x = glob(src_row);
+  const gptr<unsigned char> q = glob(dst_row);
+  auto load = [&](int64_t i) {
+    if (i >= row_len) return make_uint4(0, 0, 0, 0);
+    if constexpr (NREG > 0) return nt_ld16(x + i);  // read once
+    else return *reinterpret_cast<gptr<const uint4>>(x + i);  // read again in pass 2
+  };
+  float amax = 0.0f;
+  uint4 keep[R];
+  for (int64_t b0 = 0; b0 < row_len; b0 += int64_t(64) * R * E) {  // NREG > 0: one batch
+#pragma unroll
+    for (int u = 0; u < R; ++u) keep[u] = load(b0 + (int64_t(u) * 64 + lane) * E);
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      float v[E];
+      unpack(keep[u], v);
+#pragma unroll
+      for (int j = 0; j < E; ++j) amax = fmaxf(amax, fabsf(v[j]));
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+  const float inv = amax > 0.0f ? kE4M3Max / amax : 1.0f;
+  if (lane == 0) *glob(scale) = amax > 0.0f ? amax / kE4M3Max : 1.0f;
+  auto emit = [&](int64_t i, const uint4& raw) {
+    float v[E];
+    unpack(raw, v);
+    if constexpr (sizeof(T) == 2) {
+      uint2 out;
+      out.x = e4m3x4(qclamp(v[0], inv), qclamp(v[1], inv), qclamp(v[2], inv), qclamp(v[3], inv));
+      out.y = e4m3x4(qclamp(v[4], inv), qclamp(v[5], inv), qclamp(v[6], inv), qclamp(v[7], inv));
+      nt_st8(q + i, out);
+    } else {
+      *reinterpret_cast<gptr<uint32_t>>(q + i) =
+          e4m3x4(qclamp(v[0], inv), qclamp(v[1], inv), qclamp(v[2], inv), qclamp(v[3], inv));
+    }
+  };
+  if constexpr (NREG > 0) {
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int64_t i = (int64_t(u) * 64 + lane) * E;
+      if (i < row_len) emit(i, keep[u]);
+    }
+  } else {
+    for (int64_t b0 = 0; b0 < row_len; b0 += int64_t(64) * R * E) {
 #pragma unroll
       for (int u = 0; u < R; ++u) keep[u] = load(b0 + (int64_t(u) * 64 + lane) * E);
 #pragma unroll
       for (int u = 0; u < R; ++u) {
-        float v[E];
-        unpack(keep[u], v);
-#pragma unroll
-        for (int j = 0; j < E; ++j) amax = fmaxf(amax, fabsf(v[j]));
-      }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
-    const float inv = amax > 0.0f ? kE4M3Max / amax : 1.0f;
-    if (lane == 0) glob(scales)[r] = amax > 0.0f ? amax / kE4M3Max : 1.0f;
-    auto emit = [&](int64_t i, const uint4& raw) {
-      float v[E];
-      unpack(raw, v);
-      if constexpr (sizeof(T) == 2) {
-        uint2 out;
-        out.x = e4m3x4(qclamp(v[0], inv), qclamp(v[1], inv), qclamp(v[2], inv), qclamp(v[3], inv));
-        out.y = e4m3x4(qclamp(v[4], inv), qclamp(v[5], inv), qclamp(v[6], inv), qclamp(v[7], inv));
-        nt_st8(q + i, out);
-      } else {
-        *reinterpret_cast<gptr<uint32_t>>(q + i) =
-            e4m3x4(qclamp(v[0], inv), qclamp(v[1], inv), qclamp(v[2], inv), qclamp(v[3], inv));
-      }
-    };
-    if constexpr (NREG > 0) {
-#pragma unroll
-      for (int u = 0; u < R; ++u) {
-        const int64_t i = (int64_t(u) * 64 + lane) * E;
+        const int64_t i = b0 + (int64_t(u) * 64 + lane) * E;
         if (i < row_len) emit(i, keep[u]);
-      }
-    } else {
-      for (int64_t b0 = 0; b0 < row_len; b0 += int64_t(64) * R * E) {
-#pragma unroll
-        for (int u = 0; u < R; ++u) keep[u] = load(b0 + (int64_t(u) * 64 + lane) * E);
-#pragma unroll
-        for (int u = 0; u < R; ++u) {
-          const int64_t i = b0 + (int64_t(u) * 64 + lane) * E;
-          if (i < row_len) emit(i, keep[u]);
-        }
       }
     }
   }
 }
 
-// Dequantise (the vector path): work items are (row, segment) pairs — a segment is kDqU wave
-// accesses of E elements per lane (E = 8 for bf16 output: an 8-B fp8 load and a 16-B store per
-// lane; E = 4 for fp32: 4 B -> 16 B), so every store instruction covers one contiguous 1 KiB and
-// a short matrix (1024 rows of a k/v projection) still spreads over every SIMD.  All kDqU loads
-// are issued before the first store; the row's scale is loaded once per item.
+template <typename T, int NREG>
+__global__ __launch_bounds__(kThreads) void fp8_quantize_rows_wave_kernel(
+    const T* __restrict__ src, unsigned char* __restrict__ dst, float* __restrict__ scales,
+    int64_t rows, int64_t row_len) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wpb = kThreads / 64;
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  for (int64_t r = int64_t(blockIdx.x) * wpb + wave; r < rows; r += int64_t(gridDim.x) * wpb)
+    fp8_quantize_row<T, NREG>(src + r * row_len, dst + r * row_len, scales + r, row_len, lane);
+}
+
+// A gather group's matrices in one launch (zs_fp8_quantize_rowset): global row g (one wave each,
+// grid-stride, so g only grows and the matrix lookup is a forward scan) of matrix m, local row
+// lr = g - prefix[m]; rows [rows[m], cs[m]) are the chunk's padding: q = 0, scale = 1.  The table
+// travels in the kernel arguments (constant, uniform: scalar loads).
+constexpr int kSetMax = 16;
+struct QSet {
+  const void* src[kSetMax];
+  unsigned char* q[kSetMax];
+  float* sc[kSetMax];
+  int64_t rows[kSetMax], row_len[kSetMax], prefix[kSetMax + 1];  // prefix over cs
+  int n;
+};
+
+template <typename T, int NREG>
+__global__ __launch_bounds__(kThreads) void fp8_quantize_rowset_kernel(const QSet set) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wpb = kThreads / 64;
+  const int64_t total = set.prefix[set.n];
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));  // uniform: scalar math
+  int m = 0;
+  for (int64_t g = int64_t(blockIdx.x) * wpb + wave; g < total; g += int64_t(gridDim.x) * wpb) {
+    while (set.prefix[m + 1] <= g) ++m;
+    const int64_t lr = g - set.prefix[m], len = set.row_len[m];
+    unsigned char* qrow = set.q[m] + lr * len;
+    if (lr < set.rows[m]) {
+      fp8_quantize_row<T, NREG>(static_cast<const T*>(set.src[m]) + lr * len, qrow, set.sc[m] + lr,
+                                len, lane);
+    } else {  // padding row of the chunk
+      for (int64_t i = int64_t(lane) * 8; i < len; i += 64 * 8) nt_st8(qrow + i, make_uint2(0, 0));
+      if (lane == 0) *glob(set.sc[m] + lr) = 1.0f;
+    }
+  }
+}
+
+// Dequantise: work items are (row, segment) pairs — a segment is kDqU wave accesses of E elements
+// per lane (E = 8 for bf16 output: an 8-B fp8 load and a 16-B store per lane; E = 4 for fp32:
+// 4 B -> 16 B), so every store instruction covers one contiguous 1 KiB and a short matrix (1024
+// rows of a k/v projection) still spreads over every SIMD.  All kDqU loads are issued before the
+// first store; the row's scale is loaded once per item.
 constexpr int kDqU = 4;
+
+template <typename T>
+__device__ __forceinline__ void fp8_dequantize_segment(const unsigned char* __restrict__ q_row,
+                                                       float sc, T* __restrict__ y_row,
+                                                       int64_t row_len, int64_t s0, int lane) {
+#pragma clang fp contract(off)
+  constexpr int E = sizeof(T) == 2 ? 8 : 4;
+  const gptr<const unsigned char> q = glob(q_row);
+  const gptr<T> y = glob(y_row);
+  uint2 raw[kDqU];
+#pragma unroll
+  for (int u = 0; u < kDqU; ++u) {
+    const int64_t i = s0 + (int64_t(u) * 64 + lane) * E;
+    raw[u] = make_uint2(0, 0);
+    if (i < row_len) {
+      if constexpr (E == 8) raw[u] = nt_ld8(q + i);
+      else raw[u].x = __builtin_nontemporal_load(reinterpret_cast<gptr<const uint32_t>>(q + i));
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kDqU; ++u) {
+    const int64_t i = s0 + (int64_t(u) * 64 + lane) * E;
+    if (i >= row_len) continue;
+    const int lo = int(raw[u].x), hi = int(raw[u].y);
+    const float a0 = __builtin_amdgcn_cvt_f32_fp8(lo, 0) * sc, a1 = __builtin_amdgcn_cvt_f32_fp8(lo, 1) * sc;
+    const float a2 = __builtin_amdgcn_cvt_f32_fp8(lo, 2) * sc, a3 = __builtin_amdgcn_cvt_f32_fp8(lo, 3) * sc;
+    if constexpr (E == 8) {
+      const float b0 = __builtin_amdgcn_cvt_f32_fp8(hi, 0) * sc, b1 = __builtin_amdgcn_cvt_f32_fp8(hi, 1) * sc;
+      const float b2 = __builtin_amdgcn_cvt_f32_fp8(hi, 2) * sc, b3 = __builtin_amdgcn_cvt_f32_fp8(hi, 3) * sc;
+      auto pk = [](float a, float b) { return uint32_t(f32_to_bf16(a)) | (uint32_t(f32_to_bf16(b)) << 16); };
+      nt_st16(y + i, make_uint4(pk(a0, a1), pk(a2, a3), pk(b0, b1), pk(b2, b3)));
+    } else {
+      st4(reinterpret_cast<float*>(y_row + i), 0, make_float4(a0, a1, a2, a3));
+    }
+  }
+}
 
 template <typename T>
 __global__ __launch_bounds__(kThreads) void fp8_dequantize_rows_wave_kernel(
     const unsigned char* __restrict__ src, const float* __restrict__ scales, T* __restrict__ dst,
     int64_t rows, int64_t row_len) {
-#pragma clang fp contract(off)
-  constexpr int E = sizeof(T) == 2 ? 8 : 4;
-  constexpr int64_t SEG = int64_t(64) * E * kDqU;
+  constexpr int64_t SEG = int64_t(64) * (sizeof(T) == 2 ? 8 : 4) * kDqU;
   const int lane = threadIdx.x & 63;
   const int64_t per_row = (row_len + SEG - 1) / SEG;
   const int64_t items = rows * per_row;
   const int64_t nwaves = int64_t(gridDim.x) * (kThreads / 64);
-  for (int64_t it = int64_t(blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6); it < items;
-       it += nwaves) {
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  for (int64_t it = int64_t(blockIdx.x) * (kThreads / 64) + wave; it < items; it += nwaves) {
     const int64_t r = it / per_row;
-    const int64_t s0 = (it - r * per_row) * SEG;
-    const gptr<const unsigned char> q = glob(src + r * row_len);
-    const gptr<T> y = glob(dst + r * row_len);
-    const float sc = glob(scales)[r];
-    uint2 raw[kDqU];
-#pragma unroll
-    for (int u = 0; u < kDqU; ++u) {
-      const int64_t i = s0 + (int64_t(u) * 64 + lane) * E;
-      raw[u] = make_uint2(0, 0);
-      if (i < row_len) {
-        if constexpr (E == 8) raw[u] = nt_ld8(q + i);
-        else raw[u].x = __builtin_nontemporal_load(reinterpret_cast<gptr<const uint32_t>>(q + i));
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kDqU; ++u) {
-      const int64_t i = s0 + (int64_t(u) * 64 + lane) * E;
-      if (i >= row_len) continue;
-      const int lo = int(raw[u].x), hi = int(raw[u].y);
-      const float a0 = __builtin_amdgcn_cvt_f32_fp8(lo, 0) * sc, a1 = __builtin_amdgcn_cvt_f32_fp8(lo, 1) * sc;
-      const float a2 = __builtin_amdgcn_cvt_f32_fp8(lo, 2) * sc, a3 = __builtin_amdgcn_cvt_f32_fp8(lo, 3) * sc;
-      if constexpr (E == 8) {
-        const float b0 = __builtin_amdgcn_cvt_f32_fp8(hi, 0) * sc, b1 = __builtin_amdgcn_cvt_f32_fp8(hi, 1) * sc;
-        const float b2 = __builtin_amdgcn_cvt_f32_fp8(hi, 2) * sc, b3 = __builtin_amdgcn_cvt_f32_fp8(hi, 3) * sc;
-        auto pk = [](float a, float b) { return uint32_t(f32_to_bf16(a)) | (uint32_t(f32_to_bf16(b)) << 16); };
-        nt_st16(y + i, make_uint4(pk(a0, a1), pk(a2, a3), pk(b0, b1), pk(b2, b3)));
-      } else {
-        st4(reinterpret_cast<float*>(y + i), 0, make_float4(a0, a1, a2, a3));
-      }
-    }
+    fp8_dequantize_segment<T>(src + r * row_len, glob(scales)[r], dst + r * row_len, row_len,
+                              (it - r * per_row) * SEG, lane);
+  }
+}
+
+// The receive side of a gather group (zs_fp8_dequantize_gathered): after one all-gather of every
+// rank's concatenated q (q_rank bytes each) and one of its scales (sc_rank each), full row R of
+// matrix m is rank R / cs[m]'s local row R % cs[m]; items as above, numbered over the matrices.
+struct DqSet {
+  const unsigned char* q;
+  const float* sc;
+  int64_t q_rank, sc_rank;
+  int64_t q_off[kSetMax], sc_off[kSetMax], cs[kSetMax], row_len[kSetMax], per_row[kSetMax];
+  int64_t prefix[kSetMax + 1];  // prefix over ws * cs[m] * per_row[m] items
+  void* dst[kSetMax];
+  int n;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void fp8_dequantize_gathered_kernel(const DqSet set) {
+  constexpr int64_t SEG = int64_t(64) * (sizeof(T) == 2 ? 8 : 4) * kDqU;
+  const int lane = threadIdx.x & 63;
+  const int64_t total = set.prefix[set.n];
+  const int64_t nwaves = int64_t(gridDim.x) * (kThreads / 64);
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));  // uniform: scalar math
+  int m = 0;
+  for (int64_t it = int64_t(blockIdx.x) * (kThreads / 64) + wave; it < total; it += nwaves) {
+    while (set.prefix[m + 1] <= it) ++m;
+    // 32-bit (scalar) divisions: the host checks every matrix has < 2^31 items and rows
+    const uint32_t j = uint32_t(it - set.prefix[m]), pr = uint32_t(set.per_row[m]);
+    const int64_t len = set.row_len[m];
+    const uint32_t R = j / pr, cs = uint32_t(set.cs[m]);
+    const uint32_t rk = R / cs, lr = R - rk * cs;
+    const float sc = glob(set.sc)[int64_t(rk) * set.sc_rank + set.sc_off[m] + lr];
+    fp8_dequantize_segment<T>(set.q + int64_t(rk) * set.q_rank + set.q_off[m] + lr * len, sc,
+                              static_cast<T*>(set.dst[m]) + R * len, len, int64_t(j - R * pr) * SEG,
+                              lane);
   }
 }
 
@@ -982,6 +1065,124 @@ int zs_fp8_dequantize_rows(const void* src, const float* scales, void* dst, int 
       hipLaunchKernelGGL((fp8_dequantize_rows_kernel<unsigned short>), dim3(grid), dim3(kThreads), 0, st, q, scales, static_cast<unsigned short*>(dst), n, row_len);
   }
   ZS_HIP(hipGetLastError());
+  return ZS_OK;
+}
+
+int zs_fp8_quantize_rowset(int64_t n, const uint64_t* src, const uint64_t* q, const uint64_t* scales,
+                           const int64_t* rows, const int64_t* cs, const int64_t* row_len,
+                           int src_dtype, uintptr_t stream) {
+  ZS_REQUIRE(n >= 0, "zs_fp8_quantize_rowset: n < 0");
+  ZS_REQUIRE(src_dtype == ZS_F32 || src_dtype == ZS_BF16, "zs_fp8_quantize_rowset: bad dtype %d",
+             src_dtype);
+  if (n == 0) return ZS_OK;
+  ZS_REQUIRE(src && q && scales && rows && cs && row_len, "zs_fp8_quantize_rowset: NULL table");
+  const int E = src_dtype == ZS_F32 ? 4 : 8;
+  for (int64_t m = 0; m < n; ++m) {
+    ZS_REQUIRE(rows[m] >= 0 && cs[m] >= rows[m] && row_len[m] > 0 && row_len[m] % 8 == 0,
+               "zs_fp8_quantize_rowset: matrix %lld: rows %lld, cs %lld, row_len %lld (needs "
+               "0 <= rows <= cs, row_len a positive multiple of 8)", (long long)m,
+               (long long)rows[m], (long long)cs[m], (long long)row_len[m]);
+    ZS_REQUIRE((rows[m] == 0 || (src[m] && aligned(src[m], 16))) && (cs[m] == 0 || (q[m] &&
+               aligned(q[m], 8) && scales[m] && aligned(scales[m], 4))),
+               "zs_fp8_quantize_rowset: matrix %lld: src must be 16-B and q 8-B aligned",
+               (long long)m);
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // one launch per register class (8 / 16 / 32 resident chunks per lane, or streamed) and per
+  // kSetMax matrices: a long-row matrix does not push the others into its low-occupancy variant
+  auto nreg_of = [&](int64_t len) {
+    const int64_t chunks = (len + 64 * E - 1) / (64 * E);
+    return chunks <= 8 ? 8 : chunks <= 16 ? 16 : chunks <= 32 ? 32 : 0;
+  };
+  for (int cls : {8, 16, 32, 0}) {
+    std::vector<int64_t> ms;
+    for (int64_t m = 0; m < n; ++m)
+      if (nreg_of(row_len[m]) == cls && cs[m] > 0) ms.push_back(m);
+    for (size_t k0 = 0; k0 < ms.size(); k0 += kSetMax) {
+      QSet set{};
+      set.n = int(std::min<size_t>(kSetMax, ms.size() - k0));
+      set.prefix[0] = 0;
+      for (int k = 0; k < set.n; ++k) {
+        const int64_t m = ms[k0 + k];
+        set.src[k] = reinterpret_cast<const void*>(src[m]);
+        set.q[k] = reinterpret_cast<unsigned char*>(q[m]);
+        set.sc[k] = reinterpret_cast<float*>(scales[m]);
+        set.rows[k] = rows[m];
+        set.row_len[k] = row_len[m];
+        set.prefix[k + 1] = set.prefix[k] + cs[m];
+      }
+      for (int k = set.n; k < kSetMax; ++k) set.prefix[k + 1] = set.prefix[set.n];
+      const int64_t total = set.prefix[set.n];
+      const int grid = int(std::min<int64_t>((total + 3) / 4, grid_cap()));
+#define ZS_QS(T, N) hipLaunchKernelGGL((fp8_quantize_rowset_kernel<T, N>), dim3(grid), dim3(kThreads), 0, st, set)
+#define ZS_QSSEL(T) \
+      switch (cls) { case 8: ZS_QS(T, 8); break; case 16: ZS_QS(T, 16); break; \
+                     case 32: ZS_QS(T, 32); break; default: ZS_QS(T, 0); }
+      if (src_dtype == ZS_F32) { ZS_QSSEL(float) } else { ZS_QSSEL(unsigned short) }
+#undef ZS_QSSEL
+#undef ZS_QS
+      ZS_HIP(hipGetLastError());
+    }
+  }
+  return ZS_OK;
+}
+
+int zs_fp8_dequantize_gathered(int64_t n, const void* q, const float* scales, int ws,
+                               int64_t q_rank_bytes, int64_t sc_rank_elems, const int64_t* q_off,
+                               const int64_t* sc_off, const int64_t* cs, const int64_t* row_len,
+                               const uint64_t* dst, int dst_dtype, uintptr_t stream) {
+  ZS_REQUIRE(n >= 0 && ws >= 1, "zs_fp8_dequantize_gathered: n %lld, ws %d", (long long)n, ws);
+  ZS_REQUIRE(dst_dtype == ZS_F32 || dst_dtype == ZS_BF16,
+             "zs_fp8_dequantize_gathered: bad dtype %d", dst_dtype);
+  if (n == 0) return ZS_OK;
+  ZS_REQUIRE(q && scales && q_off && sc_off && cs && row_len && dst,
+             "zs_fp8_dequantize_gathered: NULL buffer or table");
+  ZS_REQUIRE(aligned(uint64_t(q), 8) && aligned(uint64_t(scales), 4) && q_rank_bytes % 8 == 0 &&
+                 q_rank_bytes >= 0 && sc_rank_elems >= 0,
+             "zs_fp8_dequantize_gathered: q must be 8-B aligned with an 8-B multiple rank stride");
+  const int es = dst_dtype == ZS_F32 ? 4 : 2;
+  const int64_t seg = int64_t(64) * kDqU * (dst_dtype == ZS_F32 ? 4 : 8);
+  for (int64_t m = 0; m < n; ++m)
+    ZS_REQUIRE(cs[m] >= 0 && row_len[m] > 0 && row_len[m] % 8 == 0 && q_off[m] % 8 == 0 &&
+                   q_off[m] >= 0 && sc_off[m] >= 0 && (cs[m] == 0 || (dst[m] && aligned(dst[m], 16))),
+               "zs_fp8_dequantize_gathered: matrix %lld: cs %lld, row_len %lld, q_off %lld (needs "
+               "row_len and q_off multiples of 8, dst 16-B aligned)", (long long)m,
+               (long long)cs[m], (long long)row_len[m], (long long)q_off[m]);
+  for (int64_t m = 0; m < n; ++m)  // the kernel's item and row arithmetic is 32-bit
+    ZS_REQUIRE(cs[m] <= (int64_t(1) << 31) / ws &&
+                   int64_t(ws) * cs[m] * ((row_len[m] + seg - 1) / seg) < (int64_t(1) << 31),
+               "zs_fp8_dequantize_gathered: matrix %lld too large (%lld rows x %d ranks)",
+               (long long)m, (long long)cs[m], ws);
+  (void)es;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int64_t m0 = 0; m0 < n; m0 += kSetMax) {
+    DqSet set{};
+    set.q = static_cast<const unsigned char*>(q);
+    set.sc = scales;
+    set.q_rank = q_rank_bytes;
+    set.sc_rank = sc_rank_elems;
+    set.n = int(std::min<int64_t>(kSetMax, n - m0));
+    set.prefix[0] = 0;
+    for (int k = 0; k < set.n; ++k) {
+      const int64_t m = m0 + k;
+      set.q_off[k] = q_off[m];
+      set.sc_off[k] = sc_off[m];
+      set.cs[k] = cs[m];
+      set.row_len[k] = row_len[m];
+      set.per_row[k] = (row_len[m] + seg - 1) / seg;
+      set.dst[k] = reinterpret_cast<void*>(dst[m]);
+      set.prefix[k + 1] = set.prefix[k] + int64_t(ws) * cs[m] * set.per_row[k];
+    }
+    for (int k = set.n; k < kSetMax; ++k) set.prefix[k + 1] = set.prefix[set.n];
+    const int64_t total = set.prefix[set.n];
+    if (total == 0) continue;
+    const int grid = int(std::min<int64_t>((total + 3) / 4, grid_cap()));
+    if (dst_dtype == ZS_F32)
+      hipLaunchKernelGGL((fp8_dequantize_gathered_kernel<float>), dim3(grid), dim3(kThreads), 0, st, set);
+    else
+      hipLaunchKernelGGL((fp8_dequantize_gathered_kernel<unsigned short>), dim3(grid), dim3(kThreads), 0, st, set);
+    ZS_HIP(hipGetLastError());
+  }
   return ZS_OK;
 }
 

@@ -20,7 +20,7 @@ ZS_OK, ZS_ERR_INVALID, ZS_ERR_HIP, ZS_ERR_RCCL, ZS_ERR_NOMEM = 0, 1, 2, 3, 4
 ZS_F32, ZS_BF16, ZS_U8, ZS_BF16_SPLIT = 0, 1, 2, 3
 ZS_LAYOUT_R, ZS_LAYOUT_Z, ZS_LAYOUT_F = 0, 1, 2
 ZS_BUCKETS_RAGGED, ZS_BUCKETS_PADDED = 0, 1
-ABI_VERSION = 7
+ABI_VERSION = 8
 ZS_UNIQUE_ID_BYTES = 128
 
 # Every symbol include/zero_amd.h declares (tests check the library exports all of them).
@@ -31,7 +31,8 @@ EXPORTED = (
     "zs_plan_num_segments", "zs_plan_segments", "zs_plan_num_buckets", "zs_plan_bucket_bytes",
     "zs_pack", "zs_unpack",
     "zs_copyset_create", "zs_copyset_run", "zs_copyset_destroy", "zs_scale",
-    "zs_convert", "zs_fp8_quantize_rows", "zs_fp8_dequantize_rows",
+    "zs_convert", "zs_fp8_quantize_rows", "zs_fp8_dequantize_rows", "zs_fp8_quantize_rowset",
+    "zs_fp8_dequantize_gathered",
     "zs_adam_hparams_init", "zs_adamset_create", "zs_adamset_run", "zs_adamset_destroy",
     "zs_adamset_stats", "zs_adam_step", "zs_adam_step_ex",
     "zs_comm_unique_id", "zs_comm_init", "zs_comm_destroy", "zs_reduce_scatter", "zs_all_gather",
@@ -100,6 +101,9 @@ _SIGS = {
     "zs_convert": ([_P, ctypes.c_int, _P, ctypes.c_int, _I64, _U], ctypes.c_int),
     "zs_fp8_quantize_rows": ([_P, ctypes.c_int, _P, _P, _I64, _I64, _U], ctypes.c_int),
     "zs_fp8_dequantize_rows": ([_P, _P, _P, ctypes.c_int, _I64, _I64, _U], ctypes.c_int),
+    "zs_fp8_quantize_rowset": ([_I64, _P, _P, _P, _P, _P, _P, ctypes.c_int, _U], ctypes.c_int),
+    "zs_fp8_dequantize_gathered": ([_I64, _P, _P, ctypes.c_int, _I64, _I64, _P, _P, _P, _P, _P,
+                                    ctypes.c_int, _U], ctypes.c_int),
     "zs_adam_hparams_init": ([ctypes.c_double] * 5 + [ctypes.c_int] * 3 +
                              [_I64, ctypes.c_double, ctypes.c_double, ctypes.POINTER(AdamHParams)],
                              ctypes.c_int),

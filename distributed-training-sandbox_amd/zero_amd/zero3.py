@@ -141,6 +141,7 @@ class _GatherRuntime:
         self.n_prefetch_hits = 0
         self.gather_events = None  # optional list of (start, end, bus_bytes) per gather group
         self._tables = {}          # key -> grouped all-gather pointer table (see _table)
+        self._fp8_tables = {}      # key -> fp8 gather tables (see _fp8_plan)
         # key -> (ready, done) events, re-recorded every iteration: a wait enqueued on an event
         # keeps the record it saw, and a key's next launch comes after its materialise has
         # enqueued that wait (creating two HIP events per gather cost host time every iteration)
@@ -173,7 +174,16 @@ class _GatherRuntime:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record(side)
         hold = None
-        if plan is not None:
+        fplan = None
+        if plan is None:
+            fplan = self._fp8_tables[key] if key in self._fp8_tables else self._fp8_plan(key, managers)
+        if fplan is not None:
+            # fp8 gather: one quantise launch, ONE RCCL group, one dequantise
+            # launch into one allocation
+            hold = self._launch_fp8(fplan, side)
+            out = [(m, hold.as_strided(shape, stride, off)) for m, (shape, stride, off)
+                   in zip(managers, fplan["views"])]
+        elif plan is not None:
             # one allocation for the module's full tensors and ONE library call for its RCCL group
             # of all-gathers (zero-copy from the chunk-arena slots).  Allocated on the compute
             # stream (which reads it once the gather's event has passed); the side stream that
@@ -245,6 +255,89 @@ class _GatherRuntime:
                     views, recv, raw)
         self._tables[key] = plan
         return plan
+
+    def _fp8_plan(self, key, managers):
+        """The cached tables of a module's fp8 gather: its matrices quantised by ONE launch into
+        one send buffer of concatenated rows (+ one of row scales), ONE RCCL group of two
+        all-gathers (plus the plain all-gathers of its vectors, straight into place), then ONE
+        dequantise launch from the rank-major gathered rows into the module's full tensors (one
+        allocation, as the table path).  None: the per-parameter path (standalone managers,
+        row lengths not a multiple of 8, mixed dtypes)."""
+        plan = None
+        fp8 = [m for m in managers if m.fp8]
+        if (fp8 and all(m.send_slot is not None for m in managers)
+                and len({m.shard.dtype for m in managers}) == 1
+                and all(m.row % 8 == 0 and m.send_slot.data_ptr() % 16 == 0 for m in fp8)):
+            ws = self.ws
+            dt = managers[0].shard.dtype
+            es = managers[0].shard.element_size()
+            offs, o = [], 0
+            for m in managers:
+                offs.append(o)
+                o += -(-ws * m.S // ALIGN_ELEMS) * ALIGN_ELEMS  # every full tensor 64-element aligned
+            views = []
+            for off, m in zip(offs, managers):
+                shape = tuple(m.full_shape)
+                stride, acc = [], 1
+                for d in reversed(shape):
+                    stride.append(acc)
+                    acc *= d
+                views.append((shape, tuple(reversed(stride)), off))
+            q_off, sc_off, qo, so = [], [], 0, 0
+            for m in fp8:  # cs * row bytes each: a multiple of 8, so every matrix's rows stay 8-B aligned
+                q_off.append(qo)
+                sc_off.append(so)
+                qo += m.cs * m.row
+                so += m.cs
+            i8 = [i for i, m in enumerate(managers) if m.fp8]
+            plan = {
+                "n": len(fp8), "dtype": dt, "zdt": zs_dtype(dt), "total": max(o, 1), "views": views,
+                "qtot": max(qo, 8), "sctot": max(so, 1),
+                "src": np.array([m.send_slot.data_ptr() for m in fp8], np.uint64),
+                "rows": np.array([m.r1 - m.r0 for m in fp8], np.int64),
+                "cs": np.array([m.cs for m in fp8], np.int64),
+                "row_len": np.array([m.row for m in fp8], np.int64),
+                "q_off": np.array(q_off, np.int64), "sc_off": np.array(sc_off, np.int64),
+                "dst_off": np.array([offs[i] for i in i8], np.uint64) * np.uint64(es),
+                "plain": [(m, offs[i]) for i, m in enumerate(managers) if not m.fp8],
+                "qptr": np.zeros(len(fp8), np.uint64), "sptr": np.zeros(len(fp8), np.uint64),
+                "dst": np.zeros(len(fp8), np.uint64),
+            }
+        self._fp8_tables[key] = plan
+        return plan
+
+    def _launch_fp8(self, plan, side):
+        ws = self.ws
+        hold = torch.empty(plan["total"], dtype=plan["dtype"], device=self.device)
+        hold.record_stream(side)
+        h = stream_handle(side)
+        with torch.cuda.stream(side):  # the temporaries live and die on the side stream
+            qs = torch.empty(plan["qtot"], dtype=torch.uint8, device=self.device)
+            ss = torch.empty(plan["sctot"], dtype=torch.float32, device=self.device)
+            np.add(plan["q_off"].astype(np.uint64), np.uint64(qs.data_ptr()), out=plan["qptr"])
+            np.add(plan["sc_off"].astype(np.uint64) * np.uint64(4), np.uint64(ss.data_ptr()),
+                   out=plan["sptr"])
+            _lib.call("zs_fp8_quantize_rowset", plan["n"], plan["src"].ctypes.data,
+                      plan["qptr"].ctypes.data, plan["sptr"].ctypes.data, plan["rows"].ctypes.data,
+                      plan["cs"].ctypes.data, plan["row_len"].ctypes.data, plan["zdt"], h)
+            if ws > 1:
+                qr = torch.empty(ws * plan["qtot"], dtype=torch.uint8, device=self.device)
+                sr = torch.empty(ws * plan["sctot"], dtype=torch.float32, device=self.device)
+                with _group_ctx(self.comm):
+                    self.comm.all_gather(qs, qr, side)
+                    self.comm.all_gather(ss, sr, side)
+                    for m, off in plan["plain"]:
+                        self.comm.all_gather(m.send_slot, hold[off:off + ws * m.S], side)
+            else:
+                qr, sr = qs, ss
+                for m, off in plan["plain"]:
+                    hold[off:off + m.S].copy_(m.send_slot)
+            np.add(plan["dst_off"], np.uint64(hold.data_ptr()), out=plan["dst"])
+            _lib.call("zs_fp8_dequantize_gathered", plan["n"], qr.data_ptr(), sr.data_ptr(), ws,
+                      plan["qtot"], plan["sctot"], plan["q_off"].ctypes.data,
+                      plan["sc_off"].ctypes.data, plan["cs"].ctypes.data,
+                      plan["row_len"].ctypes.data, plan["dst"].ctypes.data, plan["zdt"], h)
+        return hold
 
     def _prefetch(self, i, cur=None):
         if 0 <= i < len(self.sequence):
@@ -487,6 +580,7 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
     for rt in runtimes:
         rt.key_managers = {}
         rt._tables = {}  # a key's managers may differ from an earlier registration
+        rt._fp8_tables = {}
         for mod in model.modules():
             ms = mod_managers[id(mod)]
             if ms:

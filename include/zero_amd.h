@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ZS_ABI_VERSION 7
+#define ZS_ABI_VERSION 8
 
 enum zs_status {
   ZS_OK = 0,
@@ -176,6 +176,26 @@ int zs_fp8_quantize_rows(const void* src, int src_dtype, void* dst, float* scale
                          int64_t row_len, uintptr_t stream);
 int zs_fp8_dequantize_rows(const void* src, const float* scales, void* dst, int dst_dtype,
                            int64_t rows, int64_t row_len, uintptr_t stream);
+
+/* A ZeRO-3 gather group's fp8 send side in one launch per 16 matrices (the per-module
+ * materialize of zero3.py:36-41 with every matrix of the module at once): matrix m's rows
+ * [0, rows[m]) of src[m] (row_len[m] elements each, src_dtype) are quantised exactly as by
+ * zs_fp8_quantize_rows into q[m] / scales[m]; rows [rows[m], cs[m]) — the dim-0 chunk's padding
+ * beyond this rank's real rows — are written as q = 0, scale = 1.  row_len[m] a multiple of 8,
+ * src 16-B and q 8-B aligned. */
+int zs_fp8_quantize_rowset(int64_t n, const uint64_t* src, const uint64_t* q, const uint64_t* scales,
+                           const int64_t* rows, const int64_t* cs, const int64_t* row_len,
+                           int src_dtype, uintptr_t stream);
+/* The group's receive side after ONE all-gather of every rank's concatenated q buffer
+ * (q_rank_bytes per rank) and ONE of its scales (sc_rank_elems per rank): full row R < ws*cs[m] of
+ * matrix m is rank k = R / cs[m]'s local row lr = R % cs[m], read from
+ * q + k*q_rank_bytes + q_off[m] + lr*row_len[m] with scale scales[k*sc_rank_elems + sc_off[m] + lr],
+ * and written, dequantised to dst_dtype, at dst[m] + R*row_len[m] (16-B aligned).  One launch per
+ * 16 matrices. */
+int zs_fp8_dequantize_gathered(int64_t n, const void* q, const float* scales, int ws,
+                               int64_t q_rank_bytes, int64_t sc_rank_elems, const int64_t* q_off,
+                               const int64_t* sc_off, const int64_t* cs, const int64_t* row_len,
+                               const uint64_t* dst, int dst_dtype, uintptr_t stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Fused Adam / AdamW.  Replaces torch.optim.Adam.step on the owned shard (zero1.py:88,          */

@@ -3,6 +3,8 @@ import ctypes
 import math
 import re
 
+import numpy as np
+
 import pytest
 
 from conftest import REPO
@@ -35,7 +37,7 @@ def test_library_is_gfx950_code_object():
 def test_abi_version_and_error_text():
     from zero_amd import _lib
 
-    assert _lib.lib.zs_abi_version() == _lib.ABI_VERSION == 7
+    assert _lib.lib.zs_abi_version() == _lib.ABI_VERSION == 8
     h = ctypes.c_void_p()
     rc = _lib.lib.zs_plan_create_ex(0, None, None, 0, 0, 0, 64, 0, 0, ctypes.byref(h))
     assert rc == _lib.ZS_ERR_INVALID
@@ -89,6 +91,26 @@ def test_new_entry_points_validate_arguments():
     assert lib.zs_fp8_dequantize_rows(None, None, None, _lib.ZS_BF16, 1, 8, 0) == _lib.ZS_ERR_INVALID
     assert b"NULL" in lib.zs_last_error()
     assert lib.zs_fp8_quantize_rows(None, _lib.ZS_BF16, None, None, 0, 8, 0) == _lib.ZS_OK
+    # the gather group's set forms: argument checks before any launch
+    assert lib.zs_fp8_quantize_rowset(0, None, None, None, None, None, None, _lib.ZS_BF16, 0) == _lib.ZS_OK
+    assert lib.zs_fp8_quantize_rowset(1, None, None, None, None, None, None, _lib.ZS_BF16, 0) \
+        == _lib.ZS_ERR_INVALID
+    assert lib.zs_fp8_quantize_rowset(1, None, None, None, None, None, None, 9, 0) == _lib.ZS_ERR_INVALID
+    ptr = np.array([4096], np.uint64)
+    for rows, cs, row_len in ((3, 2, 64), (1, 1, 12), (1, 1, 0)):  # rows > cs; row_len % 8; empty rows
+        tabs = [np.array([v], np.int64) for v in (rows, cs, row_len)]
+        assert lib.zs_fp8_quantize_rowset(1, ptr.ctypes.data, ptr.ctypes.data, ptr.ctypes.data,
+                                          *(t.ctypes.data for t in tabs), _lib.ZS_BF16, 0) \
+            == _lib.ZS_ERR_INVALID
+    assert b"zs_fp8_quantize_rowset" in lib.zs_last_error()
+    assert lib.zs_fp8_dequantize_gathered(0, None, None, 1, 0, 0, None, None, None, None, None,
+                                          _lib.ZS_BF16, 0) == _lib.ZS_OK
+    assert lib.zs_fp8_dequantize_gathered(1, None, None, 2, 8, 1, None, None, None, None, None,
+                                          _lib.ZS_BF16, 0) == _lib.ZS_ERR_INVALID
+    assert lib.zs_fp8_dequantize_gathered(1, None, None, 0, 8, 1, None, None, None, None, None,
+                                          _lib.ZS_BF16, 0) == _lib.ZS_ERR_INVALID  # ws 0
+    assert lib.zs_fp8_dequantize_gathered(1, None, None, 2, 8, 1, None, None, None, None, None,
+                                          _lib.ZS_U8, 0) == _lib.ZS_ERR_INVALID
     assert lib.zs_reduce(None, None, None, 4, _lib.ZS_F32, 0, 0) == _lib.ZS_ERR_INVALID
     assert lib.zs_broadcast(None, None, None, 4, _lib.ZS_F32, 0, 0) == _lib.ZS_ERR_INVALID
     assert lib.zs_reduce_group(None, 0, None, None, None, None, _lib.ZS_F32, 0) == _lib.ZS_ERR_INVALID

@@ -68,6 +68,69 @@ def test_fp8_rows_kernels_bit_exact(gpu, rows, row_len, dtype):
     assert torch.equal(y.cpu(), want)
 
 
+@pytest.mark.parametrize("ws", [1, 3, 8])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_fp8_rowset_and_gathered_bit_exact(gpu, ws, dtype):
+    """The gather group's fused forms: zs_fp8_quantize_rowset over several matrices of one module
+    (each rank its dim-0 chunk, padding rows past the real ones) and zs_fp8_dequantize_gathered
+    from the rank-major concatenation the all-gather produces, against the row oracle on the
+    full matrices (padding rows come back as zeros)."""
+    from zero_amd import _lib
+    from zero_amd.comm import zs_dtype
+
+    # (d0, row_len): uneven chunks, a row longer than 16384 bf16 (non-resident path), 17 matrices
+    # (> 16 per launch: two launches), short matrices
+    shapes = [(37, 64), (40, 2048), (9, 4104), (5, 16392), (3, 8)] + [(ws + 2, 24)] * 12
+    g = torch.Generator().manual_seed(ws)
+    fulls = [(torch.randn(d0, rl, generator=g) * 10.0 ** torch.randint(-3, 3, (d0, 1), generator=g)
+              ).to(dtype) for d0, rl in shapes]
+    fulls[0][4] = 0  # all-zero row: scale 1
+    cs = [-(-d0 // ws) for d0, _ in shapes]
+    n = len(shapes)
+    q_off = np.cumsum([0] + [c * rl for c, (_, rl) in zip(cs, shapes)])[:-1].astype(np.int64)
+    sc_off = np.cumsum([0] + cs)[:-1].astype(np.int64)
+    qtot = int(sum(c * rl for c, (_, rl) in zip(cs, shapes)))
+    sctot = int(sum(cs))
+    st = torch.cuda.current_stream().cuda_stream
+    qr = torch.empty(ws * qtot, dtype=torch.uint8, device=gpu)
+    sr = torch.empty(ws * sctot, dtype=torch.float32, device=gpu)
+    keep = []
+    for k in range(ws):  # every rank's send side, straight into its place in the gathered buffer
+        chunks = [f[k * c:(k + 1) * c].contiguous().to(gpu) for f, c in zip(fulls, cs)]
+        keep += chunks
+        src = np.array([t.data_ptr() for t in chunks], np.uint64)
+        qp = np.uint64(qr.data_ptr() + k * qtot) + q_off.astype(np.uint64)
+        sp = np.uint64(sr.data_ptr() + 4 * k * sctot) + (sc_off * 4).astype(np.uint64)
+        rows = np.array([t.shape[0] for t in chunks], np.int64)
+        cs_a = np.array(cs, np.int64)
+        rl = np.array([r for _, r in shapes], np.int64)
+        _lib.call("zs_fp8_quantize_rowset", n, src.ctypes.data, qp.ctypes.data, sp.ctypes.data,
+                  rows.ctypes.data, cs_a.ctypes.data, rl.ctypes.data, zs_dtype(dtype), st)
+    outs = [torch.full((ws * c, r), 7.0, dtype=dtype, device=gpu) for c, (_, r) in zip(cs, shapes)]
+    dst = np.array([o.data_ptr() for o in outs], np.uint64)
+    # (every table a named array: a temporary's .ctypes.data would point at freed memory)
+    cs_t = np.array(cs, np.int64)
+    len_t = np.array([r for _, r in shapes], np.int64)
+    _lib.call("zs_fp8_dequantize_gathered", n, qr.data_ptr(), sr.data_ptr(), ws, qtot, sctot,
+              q_off.ctypes.data, sc_off.ctypes.data, cs_t.ctypes.data, len_t.ctypes.data,
+              dst.ctypes.data, zs_dtype(dtype), st)
+    torch.cuda.synchronize()
+    qh, sh = qr.cpu().numpy(), sr.cpu().numpy()
+    for m, (f, c, o) in enumerate(zip(fulls, cs, outs)):
+        q_want, sc_want, deq_want = fp8_rows_oracle(f)
+        d0, rl = f.shape
+        for k in range(ws):  # the send side, rank by rank (padding rows: q = 0, scale = 1)
+            real = max(0, min(c, d0 - k * c))
+            qk = qh[k * qtot + q_off[m]: k * qtot + q_off[m] + c * rl].reshape(c, rl)
+            sk = sh[k * sctot + sc_off[m]: k * sctot + sc_off[m] + c]
+            assert np.array_equal(qk[:real], q_want[k * c:k * c + real]), (m, k)
+            assert np.array_equal(sk[:real], sc_want[k * c:k * c + real]), (m, k)
+            assert not qk[real:].any() and np.all(sk[real:] == 1.0), (m, k)
+        got = o.cpu()
+        assert torch.equal(got[:d0], torch.from_numpy(deq_want).to(dtype)), m
+        assert not got[d0:].float().any(), m
+
+
 def _check_materialize(rank, ws, dtype, comm=None, reshard=True):
     from zero_amd import zero3
 

@@ -98,7 +98,33 @@ def main():
           3 * elems + 4 * nrows, f"one C5 decoder layer, {elems:,} bf16 elements")
     timed("fp8_dequantize_rows_kernel<bf16> (7 launches)", dequant, 3 * elems + 4 * nrows,
           f"one C5 decoder layer, {elems:,} elements")
-    del mats, qs, scs, outs
+    # the same layer through the gather group's fused forms (round 3): one quantise launch per
+    # register class into one concatenated send buffer, one dequantise launch from it (ws = 1
+    # layout: the gathered buffer is the send buffer)
+    shp = [tuple(x.shape) for x in mats]
+    q_off = np.cumsum([0] + [r * c for r, c in shp])[:-1].astype(np.int64)
+    sc_off = np.cumsum([0] + [r for r, _ in shp])[:-1].astype(np.int64)
+    qtot, sctot = int(sum(r * c for r, c in shp)), int(sum(r for r, _ in shp))
+    qcat = torch.empty(qtot, dtype=torch.uint8, device=dev)
+    scat = torch.empty(sctot, dtype=torch.float32, device=dev)
+    src = np.array([x.data_ptr() for x in mats], np.uint64)
+    qp = np.uint64(qcat.data_ptr()) + q_off.astype(np.uint64)
+    sp = np.uint64(scat.data_ptr()) + (sc_off * 4).astype(np.uint64)
+    rows_a = np.array([r for r, _ in shp], np.int64)
+    len_a = np.array([c for _, c in shp], np.int64)
+    dst = np.array([y.data_ptr() for y in outs], np.uint64)
+    timed(f"fp8_quantize_rowset_kernel<bf16> ({len(mats)} matrices, one launch per register class)",
+          lambda: _lib.call("zs_fp8_quantize_rowset", len(mats), src.ctypes.data, qp.ctypes.data,
+                            sp.ctypes.data, rows_a.ctypes.data, rows_a.ctypes.data,
+                            len_a.ctypes.data, _lib.ZS_BF16, stream_handle(st)),
+          3 * elems + 4 * nrows, f"one C5 decoder layer, {elems:,} bf16 elements")
+    timed(f"fp8_dequantize_gathered_kernel<bf16> ({len(mats)} matrices, one launch)",
+          lambda: _lib.call("zs_fp8_dequantize_gathered", len(mats), qcat.data_ptr(),
+                            scat.data_ptr(), 1, qtot, sctot, q_off.ctypes.data, sc_off.ctypes.data,
+                            rows_a.ctypes.data, len_a.ctypes.data, dst.ctypes.data, _lib.ZS_BF16,
+                            stream_handle(st)),
+          3 * elems + 4 * nrows, f"one C5 decoder layer, {elems:,} elements")
+    del mats, qs, scs, outs, qcat, scat
     torch.cuda.empty_cache()
 
     # DDP scale, in place: a 256 MiB bucket (fits the 256 MB MALL, so repeated launches partly hit
