@@ -47,18 +47,39 @@ def _ptr(t: torch.Tensor | None) -> int:
     return 0 if t is None else int(t.data_ptr())
 
 
-def launch_groups(K: int, small_last: bool = False):
-    """Buckets 0..K-1 cut into runs of doubling length — 1, 1, 2, 4, 8, ... — each moved by ONE
-    copy launch: a launch's ramp and tail are paid log2(K) times instead of K times, and the first
-    bucket still reaches its collective after one bucket's copy.  ``small_last``: the mirror image
+LAUNCH_GROWTH = 8
+
+
+def launch_growth() -> int:
+    """Growth factor of the copy launch groups: 8 (``ZERO_AMD_LAUNCH_GROWTH`` overrides it, for
+    A/B runs).  Packing a bucket moves 2 x its bytes at ~6 TB/s; its reduce-scatter at ws = 8 moves
+    7/8 of them over xGMI at <= 1.07 TB/s aggregate, so a group 8x the size of everything before it
+    is packed about as fast as the collectives of what came before run — the comm stream waits at
+    most once, for tens of microseconds — while 24 C4 buckets take 3 launches instead of 6:
+    pack 0.70 -> 0.755 of 8 TB/s at the simulated ws=8 C4 layout (profiles/r03_launch_growth_ab.txt;
+    growth 4: 0.70)."""
+    try:
+        g = int(os.environ.get("ZERO_AMD_LAUNCH_GROWTH", str(LAUNCH_GROWTH)))
+    except ValueError:
+        g = LAUNCH_GROWTH
+    return max(g, 2)
+
+
+def launch_groups(K: int, small_last: bool = False, growth: int | None = None):
+    """Buckets 0..K-1 cut into runs whose cumulative length grows by ``growth`` — 1, 1, 2, 4, 8, …
+    at 2 (1, 3, 12, … at 4) — each moved by ONE copy launch: a launch's ramp and tail are paid
+    log_growth(K) times instead of K times, and the first bucket still reaches its collective after
+    one bucket's copy (a group's copy overlaps the previous groups' collectives while growth stays
+    below the collective : copy time ratio of a bucket).  ``small_last``: the mirror image
     (…, 4, 2, 1, 1), for the unpack after the all-gathers, so only the last bucket's copy is exposed
     after the last gather."""
-    sizes, left, size = [], K, 1
+    g = launch_growth() if growth is None else max(int(growth), 2)
+    sizes, left, done = [], K, 0
     while left > 0:
-        sizes.append(min(size, left))
+        n = 1 if done == 0 else min(done * (g - 1), left)
+        sizes.append(min(n, left))
         left -= sizes[-1]
-        if len(sizes) > 1:
-            size *= 2
+        done += sizes[-1]
     if small_last:
         sizes = sizes[::-1]
     out, k = [], 0

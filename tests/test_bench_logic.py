@@ -41,19 +41,23 @@ def test_bf16_sum_tolerance_grows_with_ranks():
 
 def test_copy_launch_groups_cover_buckets_in_order():
     """Pack / unpack launch groups (zero_amd/engine.py launch_groups): every bucket exactly once,
-    in order; doubling runs (pack: the first bucket alone, unpack: the last bucket alone)."""
+    in order; growing runs (pack: the first bucket alone, unpack: the last bucket alone)."""
     import sys
 
     sys.path.insert(0, str(bench.REPO / "distributed-training-sandbox_amd"))
     from zero_amd.engine import launch_groups
 
-    for K in range(1, 70):
-        for small_last in (False, True):
-            g = launch_groups(K, small_last=small_last)
-            assert [k for grp in g for k in grp] == list(range(K))
-            assert len(g) <= 2 + int(np.log2(K)) if K > 1 else len(g) == 1
-            assert len(g[-1 if small_last else 0]) == 1
-    assert [len(x) for x in launch_groups(24)] == [1, 1, 2, 4, 8, 8]
+    for growth in (2, 4, 8):
+        for K in range(1, 70):
+            for small_last in (False, True):
+                g = launch_groups(K, small_last=small_last, growth=growth)
+                assert [k for grp in g for k in grp] == list(range(K))
+                assert len(g) <= 2 + int(np.log(K) / np.log(growth)) if K > 1 else len(g) == 1
+                assert len(g[-1 if small_last else 0]) == 1
+    assert [len(x) for x in launch_groups(24, growth=2)] == [1, 1, 2, 4, 8, 8]
+    assert [len(x) for x in launch_groups(24, growth=8)] == [1, 7, 16]
+    assert [len(x) for x in launch_groups(24)] == [1, 7, 16]  # the default growth
+    assert [len(x) for x in launch_groups(24, small_last=True)] == [16, 7, 1]
 
 
 def test_traffic_matcher_needs_equal_algorithmic_bytes(tmp_path):
