@@ -471,7 +471,7 @@ def _zero3_report(args, opt, world, rank, red_dev, el, total, workload, extra):
                       else "fp32"),
             "data": "synthetic",
             "config": dict(workload=workload, params=int(total), param_dtype=args.dtype, zero=3,
-                           update="real ZeRO-3 (update=True)", bucket_mb=args.bucket_mb or 128.0,
+                           update="real ZeRO-3 (update=True)", bucket_mb=args.bucket_mb or 512.0,
                            gather_dtype=args.gather or args.dtype, parallelism=f"dp{world}",
                            gathers=("none at N=1: every shard is its whole parameter, no hooks "
                                     "are registered (zero3.register_zero3_hooks), so this is an "
@@ -876,7 +876,7 @@ def bench_zero3(args, world, rank, dev, use_nccl):
     kw = {} if comm is None else {"comm": comm}
     ref = [p.detach().clone() for p in model.parameters()] if world > 1 and not args.gather else None
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
-                                 sync=False, gather_dtype=args.gather, bucket_mb=args.bucket_mb or 128.0, **kw)
+                                 sync=False, gather_dtype=args.gather, bucket_mb=args.bucket_mb or 512.0, **kw)
     zero3.register_zero3_hooks(model, opt.param_managers)
 
     def step():
@@ -944,7 +944,7 @@ def bench_zero3_paramset(args, world, rank, dev, use_nccl):
             if what in ("ws", "rank") else real_get(what, dm)
     kw = {} if comm is None else {"comm": comm}
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
-                                 sync=False, gather_dtype=args.gather, bucket_mb=args.bucket_mb or 128.0, **kw)
+                                 sync=False, gather_dtype=args.gather, bucket_mb=args.bucket_mb or 512.0, **kw)
     zero3.register_zero3_hooks(model, opt.param_managers)
     gather_check = None
     if world > 1:
@@ -1032,7 +1032,7 @@ def bench_train_smollm3(args, world, rank, dev, use_nccl):
         comm, _ = _zero3_comm(args, world, rank, dev)
         kw = {} if comm is None else {"comm": comm}
         opt = zero3.ShardedOptimizer(torch.optim.AdamW(model.parameters(), lr=1e-5), update=True,
-                                     sync=False, bucket_mb=args.bucket_mb or 128.0, **kw)
+                                     sync=False, bucket_mb=args.bucket_mb or 512.0, **kw)
         # one gather group per decoder layer (FSDP2 fully_shard per block, train_fsdp.py:90-97)
         zero3.register_zero3_hooks(model, opt.param_managers, units=list(model.model.layers),
                                    reshard_after_forward=not args.no_reshard)
@@ -1145,7 +1145,7 @@ def main(argv=None):
                          "by --zero 3 on C4/C5); flat = balanced 1/N slices (ablation)")
     ap.add_argument("--bucket-mb", type=float, default=None,
                     help="MiB per bucket / flat round (default: the optimizer's own — 1024 for the "
-                         "flat arena, 256 for the bucket arena, 128 for ZeRO-3 reduce buckets)")
+                         "flat arena, 256 for the bucket arena, 512 for ZeRO-3 reduce buckets)")
     ap.add_argument("--arena", default="auto", choices=["auto", "flat", "buckets"],
                     help="ZeRO-1/2 exchange at N>1: flat = params and grads are views of one "
                          "owner-major arena, grouped reduce / broadcast rounds, no pack / unpack; "
