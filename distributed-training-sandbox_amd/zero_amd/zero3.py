@@ -497,9 +497,10 @@ class Zero3ParamManager:
         """zero3.py:43-52: back to the local shard; shrink a full-size grad to its local rows
         (reference mode) or leave it to the reduce-scatter hook (update mode)."""
         self.param.data = self.shard
-        g = self.param.grad
-        if g is not None and g.shape != self.shard.shape and not self.keep_full_grad:
-            self.param.grad.data = g.data.reshape(self.full_shape)[self.r0:self.r1].clone()
+        if not self.keep_full_grad:  # update mode keeps it for the reduce-scatter: no grad lookup
+            g = self.param.grad
+            if g is not None and g.shape != self.shard.shape:
+                self.param.grad.data = g.data.reshape(self.full_shape)[self.r0:self.r1].clone()
         self.full_data = None
 
 
