@@ -128,11 +128,15 @@ def main():
     torch.cuda.empty_cache()
 
     # DDP scale, in place: a 256 MiB bucket (fits the 256 MB MALL, so repeated launches partly hit
-    # it — the figure is not an HBM rate) and a 4 GiB buffer (HBM-bound)
+    # it — the figure is not an HBM rate) and a 4 GiB buffer (HBM-bound, placed by the probe)
     for mib in (64, 256, 4096):
         for dt, code, es in ((torch.bfloat16, _lib.ZS_BF16, 2), (torch.float32, _lib.ZS_F32, 4)):
             m = (mib << 20) // es
-            b = torch.randn(m, device=dev).to(dt)
+            if mib >= 1024:  # placed like the other rows' HBM-sized buffers (engine.probed_zeros)
+                b, _ = probed_zeros(m, dt, dev)
+                b.normal_()
+            else:
+                b = torch.randn(m, device=dev).to(dt)
             timed(f"scale_kernel<{'bf16' if es == 2 else 'f32'}> (/3, in place, {mib} MiB)",
                   lambda b=b, code=code: _lib.call("zs_scale", b.data_ptr(), b.numel(), code, 3.0,
                                                    stream_handle(st)),
