@@ -56,7 +56,7 @@ def _zero12_cases(ws):
            3: [(1, "distinct", "buckets")],
            4: [(1, "ref", None), (2, "distinct", None), (2, "distinct", "buckets")],
            8: [(2, "distinct", None), (1, "distinct", None), (2, "distinct", "buckets"),
-               (1, "distinct", "buckets")]}[ws]
+               (1, "distinct", "buckets"), (1, "ref", None), (2, "ref", None)]}[ws]
     cases = [(_mr_worker, (v, f"traj_z{v}_ws{ws}_d16_{m}.npz", "ragged", a)) for v, m, a in inj]
     if ws == 2:
         from test_gpu_checkpoint import _ckpt_worker
@@ -104,7 +104,7 @@ def _zero3_cases(ws):
              # ws = 8: the exchanges the first 8-GPU run executes — table gathers from the module
              # hooks in forward and backward, backward reduce-scatters, the shard all-reduce
              8: [("_ref_mode", "traj_z3_ws8_d16_distinct.npz"), ("_ref_injected", "traj_z3_ws8_d16_ref.npz"),
-                 ("_update_hooks", "traj_z2_ws8_d16_ref.npz"),
+                 ("_update_hooks", "traj_z2_ws8_d16_ref.npz"), ("_update_hooks", "traj_z2_ws8_d16_distinct.npz"),
                  ("_update_injected", "traj_z2_ws8_d16_distinct.npz")]}[ws]
     cases = [(_mr, c) for c in cases]
     if ws == 2:  # SmolLM3 ZeRO-3 AdamW bit-exact against the C oracle; fp8 gathers; checkpoint
