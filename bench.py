@@ -409,6 +409,26 @@ class _NoComm:
     def reduce_scatter_group(self, send, recv, count, dtype, stream):
         pass
 
+    # the ordered forms keep the product's host path (events and stream waits in one library
+    # call) with the collective left out: zs_*_group_ordered with no communicator and n = 0
+    def all_gather_group_ordered_bound(self, send, recv, count, dtype):
+        return self._ordered("zs_all_gather_group_ordered", dtype)
+
+    def reduce_scatter_group_ordered_bound(self, send, recv, count, dtype):
+        return self._ordered("zs_reduce_scatter_group_ordered", dtype)
+
+    @staticmethod
+    def _ordered(name, dtype):
+        from zero_amd import _lib
+
+        fn, dt = getattr(_lib.lib, name), int(dtype)
+
+        def run(after, ready, stream, done):
+            rc = fn(None, 0, None, None, None, dt, after, ready, stream, done)
+            if rc:
+                _lib.check(rc, name)
+        return run
+
 
 def _zero3_comm_summary(opt, steps, world, red_dev):
     """Per-step time and bus bandwidth of the ZeRO-3 collectives (gathers and gradient

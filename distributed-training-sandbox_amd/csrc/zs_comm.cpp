@@ -269,6 +269,53 @@ int zs_reduce_scatter_group(zs_comm* c, int64_t n, const uint64_t* send, const u
   return ZS_OK;
 }
 
+// Ordering around a group in the same call: record `ready` where the inputs were produced, make
+// the collective stream wait for it, issue the group, record `done` after it.
+static int ordered_prologue(uintptr_t after_stream, uint64_t ready_event, uintptr_t stream) {
+  if (ready_event) {
+    hipEvent_t ev = reinterpret_cast<hipEvent_t>(ready_event);
+    ZS_HIP(hipEventRecord(ev, reinterpret_cast<hipStream_t>(after_stream)));
+    ZS_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ev, 0));
+  }
+  return ZS_OK;
+}
+
+static int ordered_epilogue(uintptr_t stream, uint64_t done_event) {
+  if (done_event)
+    ZS_HIP(hipEventRecord(reinterpret_cast<hipEvent_t>(done_event),
+                          reinterpret_cast<hipStream_t>(stream)));
+  return ZS_OK;
+}
+
+int zs_all_gather_group_ordered(zs_comm* c, int64_t n, const uint64_t* send, const uint64_t* recv,
+                                const int64_t* send_count, int dtype, uintptr_t after_stream,
+                                uint64_t ready_event, uintptr_t stream, uint64_t done_event) {
+  ZS_REQUIRE(n == 0 || (c && c->comm), "zs_all_gather_group_ordered: NULL communicator");
+  int rc = ordered_prologue(after_stream, ready_event, stream);
+  if (rc == ZS_OK && n > 0) rc = zs_all_gather_group(c, n, send, recv, send_count, dtype, stream);
+  if (rc == ZS_OK) rc = ordered_epilogue(stream, done_event);
+  return rc;
+}
+
+int zs_reduce_scatter_group_ordered(zs_comm* c, int64_t n, const uint64_t* send,
+                                    const uint64_t* recv, const int64_t* recv_count, int dtype,
+                                    uintptr_t after_stream, uint64_t ready_event, uintptr_t stream,
+                                    uint64_t done_event) {
+  ZS_REQUIRE(n == 0 || (c && c->comm), "zs_reduce_scatter_group_ordered: NULL communicator");
+  int rc = ordered_prologue(after_stream, ready_event, stream);
+  if (rc == ZS_OK && n > 0)
+    rc = zs_reduce_scatter_group(c, n, send, recv, recv_count, dtype, stream);
+  if (rc == ZS_OK) rc = ordered_epilogue(stream, done_event);
+  return rc;
+}
+
+int zs_stream_wait_event(uintptr_t stream, uint64_t event) {
+  ZS_REQUIRE(event != 0, "zs_stream_wait_event: NULL event");
+  ZS_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream),
+                            reinterpret_cast<hipEvent_t>(event), 0));
+  return ZS_OK;
+}
+
 int zs_group_start(void) {
   ZS_NCCL(ncclGroupStart());
   return ZS_OK;

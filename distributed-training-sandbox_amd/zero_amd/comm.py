@@ -185,6 +185,31 @@ class RcclComm:
             _lib.check(fn(h, n, sp, rp, cp, dt, stream_handle(stream)), "zs_reduce_scatter_group")
         return run
 
+    def all_gather_group_ordered_bound(self, send, recv, count, dtype: int):
+        """all_gather_group_bound with the stream ordering in the same library call
+        (zs_all_gather_group_ordered): returns ``run(after_stream, ready_event, stream,
+        done_event)`` on raw handles — record ``ready_event`` on ``after_stream``, make ``stream``
+        wait for it, the group, record ``done_event`` on ``stream``: one foreign call where the
+        torch event / stream API takes four."""
+        return self._ordered(_lib.lib.zs_all_gather_group_ordered, send, recv, count, dtype)
+
+    def reduce_scatter_group_ordered_bound(self, send, recv, count, dtype: int):
+        """reduce_scatter_group_bound with the ordering in the same call (see
+        all_gather_group_ordered_bound)."""
+        return self._ordered(_lib.lib.zs_reduce_scatter_group_ordered, send, recv, count, dtype)
+
+    def _ordered(self, fn, send, recv, count, dtype):
+        n = len(count)
+        sp, rp, cp = send.ctypes.data_as(_PU64), recv.ctypes.data_as(_PU64), count.ctypes.data_as(_PI64)
+        h, dt = self._h, int(dtype)
+        keep = (send, recv, count)
+
+        def run(after, ready, stream, done, _keep=keep):
+            rc = fn(h, n, sp, rp, cp, dt, after, ready, stream, done)
+            if rc:
+                _lib.check(rc, fn.__name__)
+        return run
+
     def reduce_scatter_group(self, send, recv, count, dtype: int, stream) -> None:
         """One RCCL group of SUM reduce-scatters (a ZeRO-3 gradient bucket): entry i reduces
         ``ws * count[i]`` elements at ``send[i]`` and leaves this rank's ``count[i]`` at

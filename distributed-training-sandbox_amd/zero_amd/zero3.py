@@ -132,6 +132,7 @@ class _GatherRuntime:
     def __init__(self, ws, rank, comm, device):
         self.ws, self.rank, self.comm, self.device = ws, rank, comm, device
         self.stream = comm_stream(device)
+        self._side_h = self.stream.cuda_stream
         self.pending = {}      # key -> (list[(manager, full_tensor)], event, holding tensor)
         self.sequence = []     # learned order of group keys
         self.pos = 0
@@ -150,7 +151,10 @@ class _GatherRuntime:
     def _key_events(self, key):
         ev = self._events.get(key)
         if ev is None:
-            ev = self._events[key] = (torch.cuda.Event(), torch.cuda.Event())
+            a, b = torch.cuda.Event(), torch.cuda.Event()
+            a.record(self.stream)  # torch creates the HIP event at its first record: the raw
+            b.record(self.stream)  # handles below are what the ordered library calls record
+            ev = self._events[key] = (a, b, a.cuda_event, b.cuda_event)
         return ev
 
     def launch(self, key, managers, cur=None):
@@ -162,13 +166,26 @@ class _GatherRuntime:
             self.pending[key] = ([(m, m._gather_prepare(None)[1]) for m in managers], None, None)
             self.n_gathers += 1
             return
-        ev_ready, ev = self._key_events(key)
+        ev_ready, ev, ready_h, ev_h = self._key_events(key)
         if cur is None:
             cur = torch.cuda.current_stream(self.device)
-        ev_ready.record(cur)  # shards may just have been updated
         timed = self.gather_events is not None and self.ws > 1
         plan = self._tables[key] if key in self._tables else self._table(key, managers)
         side = self.stream
+        if plan is not None and plan[-1] is not None and not timed:
+            # one allocation for the module's full tensors and ONE library call: ready event on
+            # the compute stream (the shards may just have been updated), the side stream's wait,
+            # the RCCL group of all-gathers (zero-copy from the chunk-arena slots), the done event
+            send, count, offs, total, dt, es, views, recv, raw, ordered = plan
+            hold = torch.empty(total, dtype=managers[0].shard.dtype, device=self.device)
+            hold.record_stream(side)
+            np.add(offs, np.uint64(hold.data_ptr()), out=recv)
+            ordered(cur.cuda_stream, ready_h, self._side_h, ev_h)
+            self.pending[key] = ([(m, hold.as_strided(shape, stride, off)) for m, (shape, stride, off)
+                                  in zip(managers, views)], ev, hold)
+            self.n_gathers += 1
+            return
+        ev_ready.record(cur)  # shards may just have been updated
         side.wait_event(ev_ready)
         if timed:
             e0 = torch.cuda.Event(enable_timing=True)
@@ -189,7 +206,7 @@ class _GatherRuntime:
             # stream (which reads it once the gather's event has passed); the side stream that
             # writes it is recorded on it, so a prefetch dropped unconsumed keeps its memory until
             # the gather has finished
-            send, count, offs, total, dt, es, views, recv, raw = plan
+            send, count, offs, total, dt, es, views, recv, raw, _ = plan
             hold = torch.empty(total, dtype=managers[0].shard.dtype, device=self.device)
             hold.record_stream(side)
             np.add(offs, np.uint64(hold.data_ptr()), out=recv)
@@ -247,12 +264,15 @@ class _GatherRuntime:
             count = np.array([m.S for m in managers], np.int64)
             recv = np.zeros(len(managers), np.uint64)  # refilled per gather (allocation + offs)
             dt = zs_dtype(managers[0].shard.dtype)
-            raw = None
+            raw = ordered = None
             bind = getattr(self.comm, "all_gather_group_bound", None)
             if bind is not None:
                 raw = bind(send, recv, count, dt)
+            bind = getattr(self.comm, "all_gather_group_ordered_bound", None)
+            if bind is not None:
+                ordered = bind(send, recv, count, dt)
             plan = (send, count, np.array(offs, np.uint64) * np.uint64(es), max(o, 1), dt, es,
-                    views, recv, raw)
+                    views, recv, raw, ordered)
         self._tables[key] = plan
         return plan
 
@@ -362,7 +382,9 @@ class _GatherRuntime:
             for m, full in out:
                 m._install_full(full)
             return
-        cur.wait_event(ev)
+        rc = _lib.lib.zs_stream_wait_event(cur.cuda_stream, self._events[key][3])
+        if rc:
+            _lib.check(rc, "zs_stream_wait_event")
         if hold is not None:  # one allocation (on this stream) behind all of the module's full
             for m, full in out:  # tensors, whose views already have the full shapes
                 m.full_data = full
@@ -783,6 +805,13 @@ class _GradReducer:
         self._shard_grad = [None] * n  # cached grad-arena views handed out as shard grads
         self.ev_done = [torch.cuda.Event() for _ in range(self.K)]
         self.ev_ready = [torch.cuda.Event() for _ in range(self.K)]
+        cs = opt.runtime.stream if opt.world_size > 1 else None
+        if cs is not None:  # torch creates a HIP event at its first record: the raw handles are
+            for e in self.ev_done + self.ev_ready:  # what the ordered library calls record
+                e.record(cs)
+            self._done_h = [e.cuda_event for e in self.ev_done]
+            self._ready_h = [e.cuda_event for e in self.ev_ready]
+            self._cs_h = cs.cuda_stream
         self.timing = None  # optional list of (start, end, bus_bytes) per launched bucket
         self._rs_tables = {}
         self.reset()
@@ -865,7 +894,9 @@ class _GradReducer:
             send = np.zeros(len(idx), np.uint64)  # refilled per launch with the grads' addresses
             bind = getattr(opt.comm, "reduce_scatter_group_bound", None)
             raw = bind(send, recv, count, zs_dtype(G.dtype)) if bind is not None else None
-            t = (recv, count, zs_dtype(G.dtype), send, raw)
+            bind = getattr(opt.comm, "reduce_scatter_group_ordered_bound", None)
+            ordered = bind(send, recv, count, zs_dtype(G.dtype)) if bind is not None else None
+            t = (recv, count, zs_dtype(G.dtype), send, raw, ordered)
             self._rs_tables[k] = t
         return t
 
@@ -911,15 +942,27 @@ class _GradReducer:
                     send = torch.zeros(ws * S, dtype=wdt, device=dev)
                     send[:N].copy_(flat)
             sends.append((i, send))
+        cs = opt.runtime.stream
+        tab = self._rs_table(k) if hasattr(opt.comm, "reduce_scatter_group") else None
+        if tab is not None and tab[5] is not None and self.timing is None:
+            # ONE library call: ready event on the stream that produced the grads, the side
+            # stream's wait, the bucket's RCCL group of reduce-scatters, the done event
+            recv, count, dt, sp, raw, ordered = tab
+            for j, (_, t) in enumerate(sends):
+                sp[j] = t.data_ptr()
+            ordered(cur.cuda_stream, self._ready_h[k], self._cs_h, self._done_h[k])
+            for i, send in sends:
+                send.record_stream(cs)
+                opt.params[i].grad = None
+            return
         ready = self.ev_ready[k]
         ready.record(cur)
-        cs = opt.runtime.stream
         cs.wait_event(ready)
         if self.timing is not None:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record(cs)
-        if hasattr(opt.comm, "reduce_scatter_group"):  # the bucket's RCCL group: ONE call
-            recv, count, dt, sp, raw = self._rs_table(k)
+        if tab is not None:  # the bucket's RCCL group: ONE call
+            recv, count, dt, sp, raw, _ = tab
             for j, (_, t) in enumerate(sends):
                 sp[j] = t.data_ptr()
             if raw is not None:  # tables bound once (comm.reduce_scatter_group_bound)

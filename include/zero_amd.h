@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ZS_ABI_VERSION 8
+#define ZS_ABI_VERSION 9
 
 enum zs_status {
   ZS_OK = 0,
@@ -322,6 +322,21 @@ int zs_all_gather_group(zs_comm* comm, int64_t n, const uint64_t* send, const ui
                         const int64_t* send_count, int dtype, uintptr_t stream);
 int zs_reduce_scatter_group(zs_comm* comm, int64_t n, const uint64_t* send, const uint64_t* recv,
                             const int64_t* recv_count, int dtype, uintptr_t stream);
+/* The same two groups with their stream ordering in the same call (a ZeRO-3 module gather or a
+ * gradient bucket is otherwise four runtime calls from Python around one library call):
+ * ready_event != 0: record it on after_stream (where the inputs were produced) and make `stream`
+ * wait for it; then the group (comm may be NULL when n == 0: ordering only); done_event != 0:
+ * record it on `stream` after the group.  Events are HIP events (hipEvent_t as uint64_t). */
+int zs_all_gather_group_ordered(zs_comm* comm, int64_t n, const uint64_t* send,
+                                const uint64_t* recv, const int64_t* send_count, int dtype,
+                                uintptr_t after_stream, uint64_t ready_event, uintptr_t stream,
+                                uint64_t done_event);
+int zs_reduce_scatter_group_ordered(zs_comm* comm, int64_t n, const uint64_t* send,
+                                    const uint64_t* recv, const int64_t* recv_count, int dtype,
+                                    uintptr_t after_stream, uint64_t ready_event, uintptr_t stream,
+                                    uint64_t done_event);
+/* hipStreamWaitEvent(stream, event): the consumer side of the ordered groups. */
+int zs_stream_wait_event(uintptr_t stream, uint64_t event);
 int zs_group_start(void);
 int zs_group_end(void);
 /* RCCL version the library is bound to at run time (e.g. 22606). */

@@ -37,7 +37,7 @@ def test_library_is_gfx950_code_object():
 def test_abi_version_and_error_text():
     from zero_amd import _lib
 
-    assert _lib.lib.zs_abi_version() == _lib.ABI_VERSION == 8
+    assert _lib.lib.zs_abi_version() == _lib.ABI_VERSION == 9
     h = ctypes.c_void_p()
     rc = _lib.lib.zs_plan_create_ex(0, None, None, 0, 0, 0, 64, 0, 0, ctypes.byref(h))
     assert rc == _lib.ZS_ERR_INVALID
@@ -117,7 +117,15 @@ def test_new_entry_points_validate_arguments():
     assert lib.zs_broadcast_group(None, 0, None, None, None, _lib.ZS_F32, 0) == _lib.ZS_ERR_INVALID
     assert lib.zs_all_gather_group(None, 0, None, None, None, _lib.ZS_F32, 0) == _lib.ZS_ERR_INVALID
     assert lib.zs_reduce_scatter_group(None, 0, None, None, None, _lib.ZS_F32, 0) == _lib.ZS_ERR_INVALID
+    # the ordered forms: a group needs a communicator; n == 0 without events is a no-op
+    assert lib.zs_all_gather_group_ordered(None, 1, None, None, None, _lib.ZS_BF16, 0, 0, 0, 0) \
+        == _lib.ZS_ERR_INVALID
+    assert lib.zs_reduce_scatter_group_ordered(None, 1, None, None, None, _lib.ZS_BF16, 0, 0, 0, 0) \
+        == _lib.ZS_ERR_INVALID
+    assert lib.zs_all_gather_group_ordered(None, 0, None, None, None, _lib.ZS_BF16, 0, 0, 0, 0) == _lib.ZS_OK
     assert b"NULL communicator" in lib.zs_last_error()
+    assert lib.zs_stream_wait_event(0, 0) == _lib.ZS_ERR_INVALID
+    assert b"NULL event" in lib.zs_last_error()
     from zero_amd.plan import Plan
 
     plan = Plan([100, 300, 5], 2, 0, window_elems=64)
