@@ -199,6 +199,78 @@ __global__ __launch_bounds__(256) void adam_split8(const unsigned short* __restr
   }
 }
 
+// 16 B per lane for the three 2-byte streams (8 consecutive elements per lane: 1 KiB per wave
+// instruction) AND dense float4 accesses for m / v: the fp32 streams are loaded lane-contiguous
+// (lane l: elements 4l.. of each 256-element half of the wave's 512-element span) and transposed
+// through a wave-private LDS area to 8 consecutive elements per lane, and back before the stores.
+template <int G>
+__global__ __launch_bounds__(256) void adam_split8t(const unsigned short* __restrict__ g,
+                                                    unsigned short* __restrict__ hi,
+                                                    unsigned short* __restrict__ lo,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    long n, HP hp) {
+  __shared__ f4 lds[4][2][128];  // per wave: m and v, 512 floats each
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  f4* lm = lds[wv][0];
+  f4* lv = lds[wv][1];
+  const long chunk = 256L * 8 * G;
+  const long nchunks = n / chunk;
+  for (long c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    u4 gg[G], hh[G], ll[G];
+    f4 ma[G], mb[G], va[G], vb[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {  // every load first
+      const long base = c * chunk + long(u * 4 + wv) * 512;
+      gg[u] = ld16(g + base + 8 * lane);
+      hh[u] = ld16(hi + base + 8 * lane);
+      ll[u] = ld16(lo + base + 8 * lane);
+      ma[u] = ld4(m + base + 4 * lane);
+      mb[u] = ld4(m + base + 256 + 4 * lane);
+      va[u] = ld4(v + base + 4 * lane);
+      vb[u] = ld4(v + base + 256 + 4 * lane);
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const long base = c * chunk + long(u * 4 + wv) * 512;
+      lm[lane] = ma[u];
+      lm[64 + lane] = mb[u];
+      lv[lane] = va[u];
+      lv[64 + lane] = vb[u];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      f4 m0 = lm[2 * lane], m1 = lm[2 * lane + 1], v0 = lv[2 * lane], v1 = lv[2 * lane + 1];
+      f4 g0 = unbf(u2{gg[u].x, gg[u].y}), g1 = unbf(u2{gg[u].z, gg[u].w});
+      f4 p0 = join(u2{hh[u].x, hh[u].y}, u2{ll[u].x, ll[u].y});
+      f4 p1 = join(u2{hh[u].z, hh[u].w}, u2{ll[u].z, ll[u].w});
+      elem4(g0, p0, m0, v0, hp);
+      elem4(g1, p1, m1, v1, hp);
+      u2 h0, l0, h1, l1;
+      split(p0, h0, l0);
+      split(p1, h1, l1);
+      st16(hi + base + 8 * lane, u4{h0.x, h0.y, h1.x, h1.y});
+      st16(lo + base + 8 * lane, u4{l0.x, l0.y, l1.x, l1.y});
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      lm[2 * lane] = m0;
+      lm[2 * lane + 1] = m1;
+      lv[2 * lane] = v0;
+      lv[2 * lane + 1] = v1;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      st4(m + base + 4 * lane, lm[lane]);
+      st4(m + base + 256 + 4 * lane, lm[64 + lane]);
+      st4(v + base + 4 * lane, lv[lane]);
+      st4(v + base + 256 + 4 * lane, lv[64 + lane]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void copy_nt(const float* __restrict__ a, float* __restrict__ b,
                                                long n) {
   for (long i = (long(blockIdx.x) * 256 + threadIdx.x) * 4; i < n; i += long(gridDim.x) * 256 * 4)
@@ -264,6 +336,12 @@ int main(int argc, char** argv) {
              26.0 * n / ms / 1e6, n / ms * 1e3);
       ms = time_ms([&] { adam_split8<2><<<grid, 256>>>(g, po, lo, m, v, n, hp); }, 5);
       printf("alloc %d round %d adam split8 G=2   26 B %8.3f ms %7.1f GB/s %.4g elem/s\n", a, r, ms,
+             26.0 * n / ms / 1e6, n / ms * 1e3);
+      ms = time_ms([&] { adam_split8t<1><<<grid, 256>>>(g, po, lo, m, v, n, hp); }, 5);
+      printf("alloc %d round %d adam split8t G=1  26 B %8.3f ms %7.1f GB/s %.4g elem/s\n", a, r, ms,
+             26.0 * n / ms / 1e6, n / ms * 1e3);
+      ms = time_ms([&] { adam_split8t<2><<<grid, 256>>>(g, po, lo, m, v, n, hp); }, 5);
+      printf("alloc %d round %d adam split8t G=2  26 B %8.3f ms %7.1f GB/s %.4g elem/s\n", a, r, ms,
              26.0 * n / ms / 1e6, n / ms * 1e3);
       ms = time_ms([&] { copy_nt<<<grid, 256>>>(m, v, n); }, 5);
       printf("alloc %d round %d copy_nt           8 B %8.3f ms %7.1f GB/s\n", a, r, ms,
