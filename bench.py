@@ -8,7 +8,11 @@ already resident in HBM: pack → RCCL reduce-scatter → fused Adam → RCCL al
 (N=1: one fused Adam launch).  value = params/s = 3,075,098,624 / step time (whole job; total work
 is fixed as N grows → "strong" scaling).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]  (N>1 under torch.distributed.run)
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+N>1 runs one rank per GPU: under torch.distributed.run (WORLD_SIZE must equal N, else exit 2), or,
+with no launcher, bench.py starts ``torch.distributed.run --nproc-per-node N`` itself as a child
+process and relays rank 0's line.  A product communicator that cannot be created or fails its
+self-check ends the run (exit 5); ``--comm c10d`` times torch.distributed's instead.
 Prints ONE JSON line on rank 0 (plus diagnostics on stderr).
 """
 from __future__ import annotations
@@ -41,24 +45,53 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _cpu_sample(shapes, sample_elems: int, per_layer: int = 9, min_tensors: int = 30):
+    """Indices of the tensors the CPU baseline steps: for a decoder set (C4 / C5), whole decoder
+    layers from the first one (9 tensors each: q, k, v, o, gate, up, down, 2 norms) until at least
+    ``min_tensors`` tensors and ``sample_elems`` parameters — the embedding is skipped, so the
+    sample keeps the set's tensor-size mix and the reference's per-tensor collective count (12
+    blocking calls per tensor per step, zero2.py:94-133) is represented; for the MLP sets, the
+    leading tensors up to ``sample_elems``."""
+    import numpy as np
+
+    sizes = [int(np.prod(s)) for s in shapes]
+    if len(shapes) > 2 * per_layer and len(shapes[1]) == 2:  # decoder set: [embed, layers..., tail]
+        n_layers = (len(shapes) - 2) // per_layer
+        sel, n = [], 0
+        for layer in range(n_layers):
+            idx = list(range(1 + layer * per_layer, 1 + (layer + 1) * per_layer))
+            sel += idx
+            n += sum(sizes[i] for i in idx)
+            if len(sel) >= min_tensors and n >= sample_elems:
+                break
+        return sel, f"decoder layers 0-{layer} ({layer + 1} of {n_layers}; embedding skipped)"
+    sel, n = [], 0
+    for i, k in enumerate(sizes):
+        if n + k > sample_elems and sel:
+            break
+        n += k
+        sel.append(i)
+    return sel, f"the {len(sel)} leading tensors"
+
+
 def cpu_baseline(shapes, sample_elems: int, variant: int = 2, min_seconds: float = 10.0):
     """SURVEY.md §8(d) CPU baseline (2): the reference's own ZeRO step algorithm restated on the
     host cores — per-tensor flatten / cat x ws / gloo reduce_scatter_tensor, /ws on the owner,
     torch.optim.Adam on CPU (single-tensor path, fp32 as the reference), per-tensor broadcast
     (oracle/zero_cpu_step.py, checked against the reference's trajectories by
-    tests/test_oracle.py) — on a bounded sample: the leading tensors of the set, fp32."""
+    tests/test_oracle.py) — on a bounded sample of whole decoder layers (``_cpu_sample``), fp32.
+    The reported rate is sampled params / step time; the full-set step is extrapolated at the
+    same rate per parameter AND per tensor (the sample's tensor density is the set's, minus the
+    embedding), stated in the result."""
     import numpy as np
     import torch
 
     from oracle.zero_cpu_step import ReferenceStepCPU
 
-    sel, n = [], 0
-    for s in shapes:
-        k = int(np.prod(s))
-        if n + k > sample_elems and sel:
-            break
-        n += k
-        sel.append(s)
+    idx, what = _cpu_sample(shapes, sample_elems)
+    sel = [shapes[i] for i in idx]
+    n = int(sum(int(np.prod(s)) for s in sel))
+    total = int(sum(int(np.prod(s)) for s in shapes))
     g = torch.Generator().manual_seed(0)
     ps = [torch.nn.Parameter(torch.randn(s, generator=g) * 0.02) for s in sel]
     grads = [torch.randn(s, generator=g) * 1e-3 for s in sel]
@@ -78,10 +111,18 @@ def cpu_baseline(shapes, sample_elems: int, variant: int = 2, min_seconds: float
         opt.step()
         el += time.perf_counter() - t0
         steps += 1
-    return dict(value=n * steps / el, unit="params/s", cores=torch.get_num_threads(), kind="port",
-                sample=f"first {n:,} params ({len(sel)} leading tensors of the set, fp32), "
-                       f"{steps} steps of the reference's ZeRO-{variant if variant in (1, 2) else 2} "
-                       f"step restated on CPU (per-tensor gloo collectives + torch.optim.Adam, "
+    rate = n * steps / el
+    return dict(value=rate, unit="params/s", cores=torch.get_num_threads(), kind="port",
+                tensors_sampled=len(sel), params_sampled=n, tensors_total=len(shapes),
+                params_total=total, step_s_sampled=el / steps,
+                extrapolated_full_step_s=total / rate,
+                extrapolation=(f"full-set step ~ {total:,} params / {rate:.3g} params/s: the "
+                               f"sampled layers' rate applied to the whole set ({len(shapes)} "
+                               "tensors); the embedding / lm_head are single large tensors, so "
+                               "per-tensor overheads weigh slightly less there"),
+                sample=f"{what}: {len(sel)} tensors, {n:,} params (fp32), {steps} steps of the "
+                       f"reference's ZeRO-{variant if variant in (1, 2) else 2} step restated on "
+                       f"CPU (per-tensor gloo collectives + torch.optim.Adam, "
                        f"oracle/zero_cpu_step.py), {el:.1f} s of step(); torch {torch.__version__}")
 
 
@@ -303,34 +344,124 @@ def _teardown_engine(opt):
 
 
 def _checked_comm(kw, world, rank, dev):
-    """Run comm_selfcheck on kw["comm"] (AND-ed over ranks) before anything is measured.  If the
-    library's own communicator gets any closed-form result wrong on any rank, every rank switches
-    to the same RCCL through torch.distributed (C10dComm) — a wrong exchange is never timed — and
-    the check is repeated there.  Returns the report (incl. "comm_used" when it switched)."""
+    """Run comm_selfcheck on kw["comm"] (AND-ed over ranks) before anything is measured.  A
+    communicator that gets any closed-form result wrong on any rank ends the run (exit 5): a wrong
+    exchange is never timed, and the run never swaps in another communicator behind the caller's
+    back (``--comm c10d`` asks for torch's explicitly)."""
     import torch
     import torch.distributed as dist
 
-    from zero_amd.comm import C10dComm, RcclComm
-
-    def check(comm):
-        out = comm_selfcheck(comm, world, rank, dev)
-        ok = torch.tensor([1.0 if out["ok"] else 0.0], device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        out["all_ranks_ok"] = bool(ok.item() == 1.0)
-        return out
-
-    out = check(kw["comm"])
-    if not out["all_ranks_ok"] and isinstance(kw["comm"], RcclComm):
-        log(f"rank {rank}: RcclComm self-check FAILED ({out}); measuring through C10dComm")
-        kw["comm"].close()
-        kw["comm"] = C10dComm()
-        failed = out
-        out = check(kw["comm"])
-        out["rccl_comm_failed"] = failed
-        out["comm_used"] = "c10d (RcclComm failed its self-check)"
-    elif not out["all_ranks_ok"]:
-        log(f"rank {rank}: communicator self-check FAILED: {out}")
+    out = comm_selfcheck(kw["comm"], world, rank, dev)
+    ok = torch.tensor([1.0 if out["ok"] else 0.0], device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    out["all_ranks_ok"] = bool(ok.item() == 1.0)
+    if not out["all_ranks_ok"]:
+        _fail_comm(rank, f"{type(kw['comm']).__name__} failed the closed-form self-check: {out}")
     return out
+
+
+class CommFailed(RuntimeError):
+    pass
+
+
+def _fail_comm(rank: int, detail) -> None:
+    """The product communicator is unusable at N>1: end the run loudly (exit 5) instead of timing
+    something else.  In a test process: raise."""
+    log(f"[bench] COMMUNICATOR FAILED on rank {rank}: {detail}")
+    if _IN_PROCESS[0]:
+        raise CommFailed(f"rank {rank}: {detail}")
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(5)
+
+
+def _product_comm(rank: int):
+    """The library's own RCCL communicator (zero_amd.comm.RcclComm); failing to create it ends
+    the run (exit 5) unless the caller asked for ``--comm c10d``."""
+    from zero_amd.comm import RcclComm
+
+    try:
+        return RcclComm()
+    except Exception as e:  # noqa: BLE001 — reported and fatal
+        _fail_comm(rank, f"RcclComm() raised {type(e).__name__}: {e} (use --comm c10d to time "
+                         "torch.distributed's communicator instead)")
+
+
+def _free_port() -> int:
+    """A free TCP port below the ephemeral range (32768+), so no outgoing connection (gloo's pair
+    sockets) can take it between this check and the rendezvous bind."""
+    import random
+    import socket
+
+    rng = random.Random()
+    for _ in range(200):
+        p = rng.randrange(20000, 32000)
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            try:
+                s.bind(("127.0.0.1", p))
+                return p
+            except OSError:
+                continue
+    raise RuntimeError("no free port in 20000-32000")
+
+
+def _self_launch_cmd(argv, n: int, port: int):
+    """The command ``python bench.py --gpus N`` runs when no launcher started it: N ranks, one
+    process per GPU, through torch.distributed.run on 127.0.0.1 (the driver's own form)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port),
+            str(REPO / "bench.py"), *argv]
+
+
+def _launch_ranks(argv, n: int, cmd=None) -> int:
+    """Run the N ranks as ONE child process (torch.distributed.run), relay rank 0's JSON line to
+    stdout and everything else to stderr, and return the child's exit code.  Called before any
+    GPU or torch import in this process; SIGTERM / SIGINT are forwarded to the child."""
+    import signal
+    import subprocess
+
+    cmd = cmd or _self_launch_cmd(argv, n, _free_port())
+    log(f"[bench] no WORLD_SIZE in the environment and --gpus {n}: launching {n} ranks: "
+        + " ".join(cmd))
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    prev = {}
+
+    def forward(sig, _frame):
+        if proc.poll() is None:
+            proc.send_signal(sig)
+
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        try:
+            prev[sig] = signal.signal(sig, forward)
+        except ValueError:  # not the main thread (a test): no forwarding
+            pass
+    lines = 0
+    try:
+        for line in proc.stdout:
+            s = line.strip()
+            obj = None
+            if s.startswith("{"):
+                try:
+                    obj = json.loads(s)
+                except ValueError:
+                    obj = None
+            if isinstance(obj, dict):
+                print(s, flush=True)
+                lines += 1
+            else:
+                sys.stderr.write(line)
+                sys.stderr.flush()
+        rc = proc.wait()
+    finally:
+        for sig, h in prev.items():
+            signal.signal(sig, h)
+        if proc.poll() is None:
+            proc.kill()
+            proc.wait()
+    if rc == 0 and lines != 1:
+        log(f"[bench] the {n}-rank child exited 0 but printed {lines} JSON lines (expected 1)")
+        return 6
+    return rc
 
 
 def comm_sweep(comm, arena, world, red_dev, sizes_mb=(4, 16, 64, 256), iters=5):
@@ -548,9 +679,9 @@ def _zero3_comm(args, world, rank, dev):
 
         return GlooStagedComm(), None
     if world > 1:
-        from zero_amd.comm import C10dComm, RcclComm
+        from zero_amd.comm import C10dComm
 
-        kw["comm"] = C10dComm() if args.comm == "c10d" else RcclComm()
+        kw["comm"] = C10dComm() if args.comm == "c10d" else _product_comm(rank)
         _phase("communicator self-check")
         chk = _checked_comm(kw, world, rank, dev)
         return kw["comm"], chk
@@ -641,7 +772,7 @@ def zero3_gather_check(opt, model, shapes, full_copies, dev, world, rank, red_de
     idx = model.groups[1]
     ms = [opt.param_managers[getattr(layer, f"p{k}")] for k in range(layer.n)]
     rt.launch(("exchange-check",), ms)
-    out, ev, _hold = rt.pending.pop(("exchange-check",))
+    out, ev, _hold, _ = rt.pending.pop(("exchange-check",))
     torch.cuda.current_stream(dev).wait_event(ev)
     torch.cuda.synchronize()
     bits = lambda t: t.reshape(-1).view(torch.int16 if t.element_size() == 2 else torch.int32)  # noqa: E731
@@ -1206,6 +1337,21 @@ def main(argv=None):
                     help="end the process (exit 3) with a diagnostic if the run has not finished "
                          "after this many seconds (a collective that never completes)")
     args = ap.parse_args(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # `python bench.py --gpus N` without a launcher: start the N ranks here, one process per
+        # GPU, the way the reference always launches (modal_utils.py:115-120, torchrun) — before
+        # anything touches the GPU, as a child process (never an exec)
+        rc = _launch_ranks(sys.argv[1:] if argv is None else list(argv), args.gpus)
+        if _IN_PROCESS[0]:
+            return rc
+        sys.exit(rc)
+    if env_world is not None and int(env_world) != args.gpus:
+        log(f"[bench] WORLD_SIZE={env_world} but --gpus {args.gpus}: refusing to time a job whose "
+            "rank count is not the one asked for")
+        if _IN_PROCESS[0]:
+            raise SystemExit(2)
+        sys.exit(2)
     if args.steps is None:
         args.steps = 4 if args.train else (1500 if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 300)
     if args.warmup is None:
@@ -1224,8 +1370,6 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE")
     if args.comm == "gloo-staged":  # test-only: every rank shares the box's GPUs round-robin
         local = local % torch.cuda.device_count()
     if args.share_gpu and world > 1:
@@ -1290,11 +1434,7 @@ def main(argv=None):
         if args.comm == "c10d":
             kw["comm"], comm_used = C10dComm(), "c10d"
         else:
-            try:
-                kw["comm"], comm_used = RcclComm(), "rccl"
-            except Exception as e:  # keep measuring on the same RCCL, through torch's communicator
-                log(f"rank {rank}: RcclComm failed ({e}); falling back to C10dComm")
-                kw["comm"], comm_used = C10dComm(), f"c10d (RcclComm failed: {e})"
+            kw["comm"], comm_used = _product_comm(rank), "rccl"
     if args.simulate_ws > 1:
         assert world == 1, "--simulate-ws is a single-GPU diagnostic"
         kw["comm"] = _NoComm(args.simulate_ws)
@@ -1348,7 +1488,7 @@ def main(argv=None):
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item()) / n * 1e3
 
-    exchange_check, arena_ab = {}, {}
+    exchange_check, arena_ab, arena_cal = {}, {}, {}
     opt = step = None
     for arena in arenas:
         if opt is not None:
@@ -1366,7 +1506,19 @@ def main(argv=None):
             _phase(f"arena calibration ({kind})")
             for _ in range(args.warmup):
                 step()
-            arena_ab[kind] = timed(step, max(3, min(args.steps, 5)))
+            n_cal = max(3, min(args.steps, 5))
+            opt.engine.comm_events = [] if world > 1 else None
+            arena_ab[kind] = timed(step, n_cal)
+            cal_ev, opt.engine.comm_events = opt.engine.comm_events, None
+            # what the exchange itself moved, per arena (HIP events on the comm stream): the first
+            # multi-GPU line says WHY one arena won, not only which step was shorter
+            arena_cal[kind] = {"ms_per_step": arena_ab[kind], "steps": n_cal}
+            if world > 1:
+                cs = collective_summary(cal_ev, n_cal, world, red_dev)
+                arena_cal[kind].update(
+                    busbw_gbs=cs["busbw_gbs"], frac_of_peer_links=cs["frac_of_peer_links"],
+                    frac_of_aggregate=cs["frac_of_aggregate"], comm_ms_per_step=cs["ms_per_step"],
+                    collectives={k: v for k, v in cs.items() if isinstance(v, dict)})
     if len(arenas) > 1:
         if not arena_ab:
             _fail_check("ZeRO step exchange", rank, "every arena failed its exchange check")
@@ -1536,6 +1688,7 @@ def main(argv=None):
             out["exchange_check_all_arenas"] = exchange_check
         if arena_ab:
             out["arena_calibration_ms_per_step"] = arena_ab
+            out["arena_calibration"] = arena_cal
         out["host_enqueue_ms_per_step"] = host_ms  # rank 0's Python + launch time per step
         if collectives is not None:
             out["collectives"] = collectives

@@ -646,98 +646,120 @@ __global__ __launch_bounds__(kThreads) void fp8_quantize_rowset_kernel(const QSe
   }
 }
 
-// Dequantise: work items are (row, segment) pairs — a segment is kDqU wave accesses of E elements
-// per lane (E = 8 for bf16 output: an 8-B fp8 load and a 16-B store per lane; E = 4 for fp32:
-// 4 B -> 16 B), so every store instruction covers one contiguous 1 KiB and a short matrix (1024
-// rows of a k/v projection) still spreads over every SIMD.  All kDqU loads are issued before the
-// first store; the row's scale is loaded once per item.
-constexpr int kDqU = 4;
+// Dequantise (round 4): one wave walks whole rows.  The rows of a set of matrices are numbered
+// over the set (a single matrix for zs_fp8_dequantize_rows; every matrix of a gather group, rank by
+// rank, for zs_fp8_dequantize_gathered), and each wave takes rows g, g + nwaves, ... — so the matrix
+// index only grows (uniform forward scan) and the row's rank, local row, scale and source /
+// destination pointers are worked out ONCE per row, in scalar registers (one 32-bit division per
+// row, none per access).  The wave then walks the row in batches of kDqU accesses per lane: 8-B fp8
+// loads (512 B per wave instruction, dense) and 16-B bf16 stores (1 KiB, dense) for bf16 output,
+// 4 B -> 16 B for fp32.  The loads of the NEXT batch — in the same row or the wave's next row — are
+// issued before the stores of the current one, so on gfx950, whose vmcnt counts loads and stores
+// together, waiting for a batch's data never waits for the previous batch's stores: each wave keeps
+// one batch of loads and one of stores in flight throughout.
+constexpr int kDqU = 8;
 
-template <typename T>
-__device__ __forceinline__ void fp8_dequantize_segment(const unsigned char* __restrict__ q_row,
-                                                       float sc, T* __restrict__ y_row,
-                                                       int64_t row_len, int64_t s0, int lane) {
-#pragma clang fp contract(off)
-  constexpr int E = sizeof(T) == 2 ? 8 : 4;
-  const gptr<const unsigned char> q = glob(q_row);
-  const gptr<T> y = glob(y_row);
-  uint2 raw[kDqU];
-#pragma unroll
-  for (int u = 0; u < kDqU; ++u) {
-    const int64_t i = s0 + (int64_t(u) * 64 + lane) * E;
-    raw[u] = make_uint2(0, 0);
-    if (i < row_len) {
-      if constexpr (E == 8) raw[u] = nt_ld8(q + i);
-      else raw[u].x = __builtin_nontemporal_load(reinterpret_cast<gptr<const uint32_t>>(q + i));
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < kDqU; ++u) {
-    const int64_t i = s0 + (int64_t(u) * 64 + lane) * E;
-    if (i >= row_len) continue;
-    const int lo = int(raw[u].x), hi = int(raw[u].y);
-    const float a0 = __builtin_amdgcn_cvt_f32_fp8(lo, 0) * sc, a1 = __builtin_amdgcn_cvt_f32_fp8(lo, 1) * sc;
-    const float a2 = __builtin_amdgcn_cvt_f32_fp8(lo, 2) * sc, a3 = __builtin_amdgcn_cvt_f32_fp8(lo, 3) * sc;
-    if constexpr (E == 8) {
-      const float b0 = __builtin_amdgcn_cvt_f32_fp8(hi, 0) * sc, b1 = __builtin_amdgcn_cvt_f32_fp8(hi, 1) * sc;
-      const float b2 = __builtin_amdgcn_cvt_f32_fp8(hi, 2) * sc, b3 = __builtin_amdgcn_cvt_f32_fp8(hi, 3) * sc;
-      auto pk = [](float a, float b) { return uint32_t(f32_to_bf16(a)) | (uint32_t(f32_to_bf16(b)) << 16); };
-      nt_st16(y + i, make_uint4(pk(a0, a1), pk(a2, a3), pk(b0, b1), pk(b2, b3)));
-    } else {
-      st4(reinterpret_cast<float*>(y_row + i), 0, make_float4(a0, a1, a2, a3));
-    }
-  }
-}
-
-template <typename T>
-__global__ __launch_bounds__(kThreads) void fp8_dequantize_rows_wave_kernel(
-    const unsigned char* __restrict__ src, const float* __restrict__ scales, T* __restrict__ dst,
-    int64_t rows, int64_t row_len) {
-  constexpr int64_t SEG = int64_t(64) * (sizeof(T) == 2 ? 8 : 4) * kDqU;
-  const int lane = threadIdx.x & 63;
-  const int64_t per_row = (row_len + SEG - 1) / SEG;
-  const int64_t items = rows * per_row;
-  const int64_t nwaves = int64_t(gridDim.x) * (kThreads / 64);
-  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
-  for (int64_t it = int64_t(blockIdx.x) * (kThreads / 64) + wave; it < items; it += nwaves) {
-    const int64_t r = it / per_row;
-    fp8_dequantize_segment<T>(src + r * row_len, glob(scales)[r], dst + r * row_len, row_len,
-                              (it - r * per_row) * SEG, lane);
-  }
-}
-
-// The receive side of a gather group (zs_fp8_dequantize_gathered): after one all-gather of every
-// rank's concatenated q (q_rank bytes each) and one of its scales (sc_rank each), full row R of
-// matrix m is rank R / cs[m]'s local row R % cs[m]; items as above, numbered over the matrices.
 struct DqSet {
   const unsigned char* q;
   const float* sc;
-  int64_t q_rank, sc_rank;
-  int64_t q_off[kSetMax], sc_off[kSetMax], cs[kSetMax], row_len[kSetMax], per_row[kSetMax];
-  int64_t prefix[kSetMax + 1];  // prefix over ws * cs[m] * per_row[m] items
+  int64_t q_rank, sc_rank;  // per-rank strides of the gathered q (bytes) and scales (elements)
+  int64_t q_off[kSetMax], sc_off[kSetMax], cs[kSetMax], row_len[kSetMax];
+  int64_t prefix[kSetMax + 1];  // prefix over ws * cs[m] full rows
   void* dst[kSetMax];
   int n;
 };
 
 template <typename T>
+struct DqRow {
+  const unsigned char* q;
+  T* y;
+  float sc;
+  int64_t len;
+};
+
+template <typename T>
+__device__ __forceinline__ void fp8_dq_load(const DqRow<T>& r, int64_t b0, int lane, uint2* raw) {
+  constexpr int E = sizeof(T) == 2 ? 8 : 4;
+  const gptr<const unsigned char> q = glob(r.q);
+#pragma unroll
+  for (int u = 0; u < kDqU; ++u) {
+    const int64_t i = b0 + (int64_t(u) * 64 + lane) * E;
+    raw[u] = make_uint2(0, 0);
+    if (i < r.len) {
+      if constexpr (E == 8) raw[u] = nt_ld8(q + i);
+      else raw[u].x = __builtin_nontemporal_load(reinterpret_cast<gptr<const uint32_t>>(q + i));
+    }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void fp8_dq_store(const DqRow<T>& r, int64_t b0, int lane,
+                                             const uint2* raw) {
+#pragma clang fp contract(off)
+  constexpr int E = sizeof(T) == 2 ? 8 : 4;
+  const gptr<T> y = glob(r.y);
+  const float sc = r.sc;
+#pragma unroll
+  for (int u = 0; u < kDqU; ++u) {
+    const int64_t i = b0 + (int64_t(u) * 64 + lane) * E;
+    if (i >= r.len) continue;
+    const int lo = int(raw[u].x), hi = int(raw[u].y);
+    const float a0 = __builtin_amdgcn_cvt_f32_fp8(lo, 0) * sc, a1 = __builtin_amdgcn_cvt_f32_fp8(lo, 1) * sc;
+    const float a2 = __builtin_amdgcn_cvt_f32_fp8(lo, 2) * sc, a3 = __builtin_amdgcn_cvt_f32_fp8(lo, 3) * sc;
+    if constexpr (E == 8) {
+      const float b0_ = __builtin_amdgcn_cvt_f32_fp8(hi, 0) * sc, b1 = __builtin_amdgcn_cvt_f32_fp8(hi, 1) * sc;
+      const float b2 = __builtin_amdgcn_cvt_f32_fp8(hi, 2) * sc, b3 = __builtin_amdgcn_cvt_f32_fp8(hi, 3) * sc;
+      auto pk = [](float a, float b) { return uint32_t(f32_to_bf16(a)) | (uint32_t(f32_to_bf16(b)) << 16); };
+      nt_st16(y + i, make_uint4(pk(a0, a1), pk(a2, a3), pk(b0_, b1), pk(b2, b3)));
+    } else {
+      st4(reinterpret_cast<float*>(r.y + i), 0, make_float4(a0, a1, a2, a3));
+    }
+  }
+}
+
+template <typename T>
 __global__ __launch_bounds__(kThreads) void fp8_dequantize_gathered_kernel(const DqSet set) {
-  constexpr int64_t SEG = int64_t(64) * (sizeof(T) == 2 ? 8 : 4) * kDqU;
+  constexpr int64_t B = int64_t(64) * (sizeof(T) == 2 ? 8 : 4) * kDqU;  // elements per batch
   const int lane = threadIdx.x & 63;
   const int64_t total = set.prefix[set.n];
   const int64_t nwaves = int64_t(gridDim.x) * (kThreads / 64);
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));  // uniform: scalar math
   int m = 0;
-  for (int64_t it = int64_t(blockIdx.x) * (kThreads / 64) + wave; it < total; it += nwaves) {
-    while (set.prefix[m + 1] <= it) ++m;
-    // 32-bit (scalar) divisions: the host checks every matrix has < 2^31 items and rows
-    const uint32_t j = uint32_t(it - set.prefix[m]), pr = uint32_t(set.per_row[m]);
-    const int64_t len = set.row_len[m];
-    const uint32_t R = j / pr, cs = uint32_t(set.cs[m]);
+  // row g of the set -> its pointers and scale (uniform; the host checks ws * cs[m] < 2^31)
+  auto row_at = [&](int64_t g, DqRow<T>& r) {
+    while (set.prefix[m + 1] <= g) ++m;
+    const uint32_t R = uint32_t(g - set.prefix[m]), cs = uint32_t(set.cs[m]);
     const uint32_t rk = R / cs, lr = R - rk * cs;
-    const float sc = glob(set.sc)[int64_t(rk) * set.sc_rank + set.sc_off[m] + lr];
-    fp8_dequantize_segment<T>(set.q + int64_t(rk) * set.q_rank + set.q_off[m] + lr * len, sc,
-                              static_cast<T*>(set.dst[m]) + R * len, len, int64_t(j - R * pr) * SEG,
-                              lane);
+    r.len = set.row_len[m];
+    r.sc = glob(set.sc)[int64_t(rk) * set.sc_rank + set.sc_off[m] + lr];
+    r.q = set.q + int64_t(rk) * set.q_rank + set.q_off[m] + int64_t(lr) * r.len;
+    r.y = static_cast<T*>(set.dst[m]) + int64_t(R) * r.len;
+  };
+  int64_t g = int64_t(blockIdx.x) * (kThreads / 64) + wave;
+  if (g >= total) return;
+  DqRow<T> cur;
+  row_at(g, cur);
+  int64_t b0 = 0;
+  uint2 raw[kDqU];
+  fp8_dq_load<T>(cur, b0, lane, raw);
+  while (true) {
+    DqRow<T> nxt = cur;
+    int64_t nb0 = b0 + B;
+    bool more = true;
+    if (nb0 >= cur.len) {  // the wave's next row
+      g += nwaves;
+      more = g < total;
+      if (more) row_at(g, nxt);
+      nb0 = 0;
+    }
+    uint2 nraw[kDqU];
+    if (more) fp8_dq_load<T>(nxt, nb0, lane, nraw);  // next batch's loads before this one's stores
+    fp8_dq_store<T>(cur, b0, lane, raw);
+    if (!more) break;
+    cur = nxt;
+    b0 = nb0;
+#pragma unroll
+    for (int u = 0; u < kDqU; ++u) raw[u] = nraw[u];
   }
 }
 
@@ -757,6 +779,20 @@ __global__ __launch_bounds__(kThreads) void fp8_dequantize_rows_kernel(
 }
 
 inline bool aligned(uint64_t p, uint64_t a) { return p % a == 0; }
+
+// Dequantise grid: one wave per row (4 rows per workgroup) up to the usual cap; with
+// ZERO_AMD_DQ_WG_PER_CU=k (diagnostic A/B) at most k workgroups per CU, each wave walking several
+// rows with the next row's loads issued before the current row's stores.
+int dq_grid(int64_t rows) {
+  static int per_cu = -1;
+  if (per_cu < 0) {
+    const char* e = std::getenv("ZERO_AMD_DQ_WG_PER_CU");
+    per_cu = e ? std::max(0, std::atoi(e)) : 0;
+  }
+  int64_t cap = grid_cap();
+  if (per_cu > 0) cap = std::max<int64_t>(1, cap / 128 * per_cu);
+  return int(std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, cap)));
+}
 
 }  // namespace
 
@@ -1049,14 +1085,23 @@ int zs_fp8_dequantize_rows(const void* src, const float* scales, void* dst, int 
   const bool vec = row_len % 8 == 0 && aligned(uint64_t(src), 8) && aligned(uint64_t(dst), 16);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const unsigned char* q = static_cast<const unsigned char*>(src);
-  if (vec) {  // one wave per (row, segment) item, 4 per workgroup
-    const int64_t seg = int64_t(64) * kDqU * (dst_dtype == ZS_F32 ? 4 : 8);
-    const int64_t items = rows * ((row_len + seg - 1) / seg);
-    const int grid = int(std::min<int64_t>((items + 3) / 4, grid_cap()));
+  if (vec) {  // the gathered kernel over one matrix of one rank: one wave per row
+    ZS_REQUIRE(rows < (int64_t(1) << 31), "zs_fp8_dequantize_rows: %lld rows (max 2^31 - 1)",
+               (long long)rows);
+    DqSet set{};
+    set.q = q;
+    set.sc = scales;
+    set.n = 1;
+    set.cs[0] = rows;
+    set.row_len[0] = row_len;
+    set.dst[0] = dst;
+    set.prefix[0] = 0;
+    for (int k = 1; k <= kSetMax; ++k) set.prefix[k] = rows;
+    const int grid = dq_grid(rows);
     if (dst_dtype == ZS_F32)
-      hipLaunchKernelGGL((fp8_dequantize_rows_wave_kernel<float>), dim3(grid), dim3(kThreads), 0, st, q, scales, static_cast<float*>(dst), rows, row_len);
+      hipLaunchKernelGGL((fp8_dequantize_gathered_kernel<float>), dim3(grid), dim3(kThreads), 0, st, set);
     else
-      hipLaunchKernelGGL((fp8_dequantize_rows_wave_kernel<unsigned short>), dim3(grid), dim3(kThreads), 0, st, q, scales, static_cast<unsigned short*>(dst), rows, row_len);
+      hipLaunchKernelGGL((fp8_dequantize_gathered_kernel<unsigned short>), dim3(grid), dim3(kThreads), 0, st, set);
   } else {
     const int grid = int(std::min<int64_t>(std::max<int64_t>(1, (n + kThreads - 1) / kThreads), grid_cap()));
     if (dst_dtype == ZS_F32)
@@ -1140,20 +1185,16 @@ int zs_fp8_dequantize_gathered(int64_t n, const void* q, const float* scales, in
   ZS_REQUIRE(aligned(uint64_t(q), 8) && aligned(uint64_t(scales), 4) && q_rank_bytes % 8 == 0 &&
                  q_rank_bytes >= 0 && sc_rank_elems >= 0,
              "zs_fp8_dequantize_gathered: q must be 8-B aligned with an 8-B multiple rank stride");
-  const int es = dst_dtype == ZS_F32 ? 4 : 2;
-  const int64_t seg = int64_t(64) * kDqU * (dst_dtype == ZS_F32 ? 4 : 8);
   for (int64_t m = 0; m < n; ++m)
     ZS_REQUIRE(cs[m] >= 0 && row_len[m] > 0 && row_len[m] % 8 == 0 && q_off[m] % 8 == 0 &&
                    q_off[m] >= 0 && sc_off[m] >= 0 && (cs[m] == 0 || (dst[m] && aligned(dst[m], 16))),
                "zs_fp8_dequantize_gathered: matrix %lld: cs %lld, row_len %lld, q_off %lld (needs "
                "row_len and q_off multiples of 8, dst 16-B aligned)", (long long)m,
                (long long)cs[m], (long long)row_len[m], (long long)q_off[m]);
-  for (int64_t m = 0; m < n; ++m)  // the kernel's item and row arithmetic is 32-bit
-    ZS_REQUIRE(cs[m] <= (int64_t(1) << 31) / ws &&
-                   int64_t(ws) * cs[m] * ((row_len[m] + seg - 1) / seg) < (int64_t(1) << 31),
+  for (int64_t m = 0; m < n; ++m)  // the kernel's row arithmetic is 32-bit
+    ZS_REQUIRE(int64_t(ws) * cs[m] < (int64_t(1) << 31),
                "zs_fp8_dequantize_gathered: matrix %lld too large (%lld rows x %d ranks)",
                (long long)m, (long long)cs[m], ws);
-  (void)es;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   for (int64_t m0 = 0; m0 < n; m0 += kSetMax) {
     DqSet set{};
@@ -1169,14 +1210,13 @@ int zs_fp8_dequantize_gathered(int64_t n, const void* q, const float* scales, in
       set.sc_off[k] = sc_off[m];
       set.cs[k] = cs[m];
       set.row_len[k] = row_len[m];
-      set.per_row[k] = (row_len[m] + seg - 1) / seg;
       set.dst[k] = reinterpret_cast<void*>(dst[m]);
-      set.prefix[k + 1] = set.prefix[k] + int64_t(ws) * cs[m] * set.per_row[k];
+      set.prefix[k + 1] = set.prefix[k] + int64_t(ws) * cs[m];
     }
     for (int k = set.n; k < kSetMax; ++k) set.prefix[k + 1] = set.prefix[set.n];
     const int64_t total = set.prefix[set.n];
     if (total == 0) continue;
-    const int grid = int(std::min<int64_t>((total + 3) / 4, grid_cap()));
+    const int grid = dq_grid(total);
     if (dst_dtype == ZS_F32)
       hipLaunchKernelGGL((fp8_dequantize_gathered_kernel<float>), dim3(grid), dim3(kThreads), 0, st, set);
     else
@@ -1401,13 +1441,13 @@ int zs_adam_step_ex(float* p, uint16_t* p_bf16, const void* g, int g_dtype, floa
 // rewritten (A_{t-1} -> A_t) although the reference signature spells it const.
 int zs_adam_step(float* p, uint16_t* p_bf16, const void* g, int g_dtype, float* m, float* v,
                  int64_t n, float lr, float b1, float b2, float eps, float wd, int decoupled,
-                 int64_t step, float grad_scale, const float* carry, float carry_scale,
+                 int64_t step, float grad_scale, float* carry, float carry_scale,
                  uintptr_t stream) {
   ZS_REQUIRE(grad_scale > 0.0f && std::isfinite(grad_scale), "zs_adam_step: grad_scale must be > 0");
   const double r = 1.0 / double(grad_scale), k = std::nearbyint(r);
   const double div = (k >= 1.0 && std::fabs(r - k) <= 1e-6 * k) ? k : r;
   return zs_adam_step_ex(p, p_bf16, g, g_dtype, m, v, n, lr, b1, b2, eps, wd, decoupled, step, div,
-                         const_cast<float*>(carry), carry_scale, stream);
+                         carry, carry_scale, stream);
 }
 
 int zs_adamset_destroy(zs_adamset* as) {
@@ -1424,6 +1464,28 @@ int zs_adamset_stats(const zs_adamset* as, int64_t* elems, int64_t* bytes) {
   ZS_REQUIRE(as && elems && bytes, "zs_adamset_stats: NULL argument");
   *elems = as->elems;
   *bytes = as->bytes;
+  return ZS_OK;
+}
+
+int zs_device_alloc(int64_t bytes, void** out) {
+  ZS_REQUIRE(out != nullptr, "zs_device_alloc: out is NULL");
+  ZS_REQUIRE(bytes > 0, "zs_device_alloc: bytes must be > 0 (got %lld)", (long long)bytes);
+  *out = nullptr;
+  void* p = nullptr;
+  const hipError_t e = hipMalloc(&p, size_t(bytes));
+  if (e == hipErrorOutOfMemory) {
+    (void)hipGetLastError();  // clear the sticky-looking error state of the runtime
+    return zs::fail(ZS_ERR_NOMEM, "zs_device_alloc: %lld bytes: out of device memory",
+                    (long long)bytes);
+  }
+  ZS_HIP(e);
+  *out = p;
+  return ZS_OK;
+}
+
+int zs_device_free(void* p) {
+  if (p == nullptr) return ZS_OK;
+  ZS_HIP(hipFree(p));
   return ZS_OK;
 }
 

@@ -20,7 +20,7 @@ ZS_OK, ZS_ERR_INVALID, ZS_ERR_HIP, ZS_ERR_RCCL, ZS_ERR_NOMEM = 0, 1, 2, 3, 4
 ZS_F32, ZS_BF16, ZS_U8, ZS_BF16_SPLIT = 0, 1, 2, 3
 ZS_LAYOUT_R, ZS_LAYOUT_Z, ZS_LAYOUT_F = 0, 1, 2
 ZS_BUCKETS_RAGGED, ZS_BUCKETS_PADDED = 0, 1
-ABI_VERSION = 9
+ABI_VERSION = 10
 ZS_UNIQUE_ID_BYTES = 128
 
 # Every symbol include/zero_amd.h declares (tests check the library exports all of them).
@@ -38,6 +38,7 @@ EXPORTED = (
     "zs_comm_unique_id", "zs_comm_init", "zs_comm_destroy", "zs_reduce_scatter", "zs_all_gather",
     "zs_all_reduce", "zs_reduce", "zs_broadcast", "zs_reduce_group", "zs_broadcast_group", "zs_all_gather_group", "zs_reduce_scatter_group",
     "zs_all_gather_group_ordered", "zs_reduce_scatter_group_ordered", "zs_stream_wait_event", "zs_group_start", "zs_group_end", "zs_rccl_version",
+    "zs_device_alloc", "zs_device_free",
 )
 
 
@@ -139,6 +140,8 @@ _SIGS = {
     "zs_group_start": ([], ctypes.c_int),
     "zs_group_end": ([], ctypes.c_int),
     "zs_rccl_version": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "zs_device_alloc": ([_I64, ctypes.POINTER(_P)], ctypes.c_int),
+    "zs_device_free": ([_P], ctypes.c_int),
 }
 
 

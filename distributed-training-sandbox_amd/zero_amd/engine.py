@@ -96,11 +96,64 @@ PROBE_MIN_BYTES = 1 << 30
 PROBE_ACCEPT_GBS = 5950.0
 
 
-def _stream_gbs(buf: torch.Tensor, stream) -> float:
-    """In-place streaming GB/s of ``buf`` (read + write of every byte, gfx950 copy kernel; one warm
-    pass first, which also touches every page)."""
-    nbytes = buf.numel() * buf.element_size()
-    probe = CopySet([buf.data_ptr()], [buf.data_ptr()], [nbytes])  # unchanged contents
+_PLACED = {"bytes": 0, "buffers": 0}  # device memory held by placed buffers (outside torch's cache)
+
+
+def placed_bytes() -> int:
+    """Bytes of device memory currently held by placed buffers (``probed_zeros``).  They are
+    hipMalloc allocations outside torch's caching allocator, so ``torch.cuda.memory_allocated``
+    does not count them; the harness memory report adds them (training_utils/memory.py)."""
+    return _PLACED["bytes"]
+
+
+class _DeviceBuffer:
+    """``nbytes`` of device memory from ``zs_device_alloc`` (hipMalloc), freed with
+    ``zs_device_free`` when the last tensor viewing it is released (torch keeps this object alive
+    through ``__cuda_array_interface__``).  Nothing here touches torch's caching allocator."""
+
+    def __init__(self, nbytes: int, device):
+        import ctypes
+
+        self.nbytes, self.device = int(nbytes), torch.device(device)
+        ptr = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.call("zs_device_alloc", self.nbytes, ctypes.byref(ptr))
+        self.ptr = int(ptr.value)
+        _PLACED["bytes"] += self.nbytes
+        _PLACED["buffers"] += 1
+
+    @property
+    def __cuda_array_interface__(self):
+        return {"shape": (self.nbytes,), "typestr": "|u1", "data": (self.ptr, False),
+                "version": 2}
+
+    def tensor(self, n: int, dtype) -> torch.Tensor:
+        """The first ``n`` elements of the buffer as a 1-D ``dtype`` tensor on its device."""
+        with torch.cuda.device(self.device):
+            raw = torch.as_tensor(self, device=self.device)
+        if raw.data_ptr() != self.ptr or raw.device != self.device:
+            raise RuntimeError("zero_amd: torch did not wrap the placed buffer in place "
+                               f"({raw.device}, {raw.data_ptr():#x} != {self.ptr:#x})")
+        es = torch.empty((), dtype=dtype).element_size()
+        return raw[:n * es].view(dtype)
+
+    def free(self):
+        if self.ptr:
+            ptr, self.ptr = self.ptr, 0
+            _PLACED["bytes"] -= self.nbytes
+            _PLACED["buffers"] -= 1
+            try:
+                _lib.lib.zs_device_free(ptr)
+            except Exception:  # noqa: BLE001 — interpreter shutdown: the runtime may be gone
+                pass
+
+    __del__ = free
+
+
+def _stream_gbs(ptr: int, nbytes: int, stream) -> float:
+    """In-place streaming GB/s of ``nbytes`` at ``ptr`` (read + write of every byte, gfx950 copy
+    kernel; one warm pass first, which also touches every page)."""
+    probe = CopySet([ptr], [ptr], [nbytes])  # unchanged contents
     probe.run(stream)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
@@ -123,8 +176,13 @@ def probed_zeros(n: int, dtype, device, tries: int = 8, accept_gbs: float = PROB
     kernel; the first at ``accept_gbs`` or above is kept at once, otherwise the fastest of
     ``tries``.  At most THREE candidates are held at once (the best so far, the newest, and the
     last rejected one, so the next allocation cannot be handed the memory just rejected): peak
-    transient memory is 3x the buffer.  Rejected candidates go back to the device.  Skipped when
-    free memory is short — then the single plain allocation is still measured.
+    transient memory is 3x the buffer.
+
+    Candidates are device allocations of their own (``zs_device_alloc``, outside torch's caching
+    allocator — round 4): a rejected one goes straight back to the device, and the caller's cached
+    blocks are never touched (no ``torch.cuda.empty_cache()``).  The kept buffer is freed when its
+    last tensor is; ``placed_bytes()`` counts what is held.  Skipped when free memory is short —
+    then the single plain allocation is still measured.
     Returns (buffer, info dict): ``gbs`` every candidate's GB/s in allocation order,
     ``unprobed_gbs`` the first (what a plain allocation would have given), ``chosen``."""
     nbytes = n * torch.empty((), dtype=dtype).element_size()
@@ -137,42 +195,44 @@ def probed_zeros(n: int, dtype, device, tries: int = 8, accept_gbs: float = PROB
         accept_gbs = float(env)
     if nbytes < PROBE_MIN_BYTES:
         return torch.zeros(n, dtype=dtype, device=device), info
+    device = torch.device(device)
     stream = torch.cuda.current_stream(device)
     free, total = torch.cuda.mem_get_info(device)
     # three candidates are held at once: keep a quarter of the device (and 2 GiB) out of it
     room = (free - max(total // 4, 2 << 30)) // nbytes
     if tries <= 1 or room < 3:
         buf = torch.zeros(n, dtype=dtype, device=device)
-        g = round(_stream_gbs(buf, stream), 1)
+        g = round(_stream_gbs(buf.data_ptr(), nbytes, stream), 1)
         info.update(gbs=[g], unprobed_gbs=g, chosen=0,
                     probe="off" if tries <= 1 else "skipped: free memory short")
         return buf, info
     best = newest_rejected = None
     for k in range(tries):
-        buf = torch.zeros(n, dtype=dtype, device=device)
-        g = _stream_gbs(buf, stream)
+        cand = _DeviceBuffer(nbytes, device)
+        g = _stream_gbs(cand.ptr, nbytes, stream)
         info["gbs"].append(round(g, 1))
         if best is None or g > best[0]:
-            rejected, best = best, (g, k, buf)
+            rejected, best = best, (g, k, cand)
         else:
-            rejected = (g, k, buf)
-        del buf
+            rejected = (g, k, cand)
+        del cand
         if newest_rejected is not None and rejected is not None:
-            # release the older blocker to the device, not to torch's cache (which would hand the
-            # same block straight back as the next candidate)
+            # the older blocker goes back to the device now; the newest stays held so the next
+            # allocation cannot be handed the memory just rejected
+            newest_rejected[2].free()
             newest_rejected = None
-            torch.cuda.empty_cache()
         newest_rejected = rejected if rejected is not None else newest_rejected
         rejected = None
         if best[0] >= accept_gbs:
             break
-    out, chosen = best[2], best[1]
-    del best, newest_rejected
-    # hand the rejected candidates back to the device (not just to torch's cache), so later
-    # allocations outside torch (RCCL buffers, segment tables) and mem_get_info see them
-    torch.cuda.empty_cache()
+    if newest_rejected is not None:
+        newest_rejected[2].free()
+    keep, chosen = best[2], best[1]
+    out = keep.tensor(n, dtype)
+    out.zero_()
+    del best, newest_rejected, keep
     info.update(tries=len(info["gbs"]), chosen=chosen, accept_gbs=accept_gbs,
-                unprobed_gbs=info["gbs"][0], held_max=3)
+                unprobed_gbs=info["gbs"][0], held_max=3, allocator="zs_device_alloc (hipMalloc)")
     return out, info
 
 

@@ -6,6 +6,9 @@ logical (numel Ã— element size, in MiB) â€” the quantity the reference reports â
 physical: the distinct storages behind those tensors.  The two differ for the drop-ins on purpose:
 ``optimizer.optimizer.state[p]`` holds *views* of one flat fp32 shard buffer, and ZeRO-3 parameters
 are views of one flat chunk arena, so the physical column shows what is really resident.
+"Total allocated" / "Max allocated" are torch's allocator figures plus the placed buffers of 1 GiB
+or more (optimizer state, parameter / gradient arenas: ``engine.probed_zeros``), which are device
+allocations of their own outside torch's cache.
 """
 from __future__ import annotations
 
@@ -64,8 +67,11 @@ def memory_report(model, optimizer, device) -> MemoryReport:
     g_l, g_p = _walk(p.grad for p in params)
     o_l, o_p = _walk(_state_tensors(optimizer))
     on_gpu = torch.cuda.is_available() and torch.device(device).type == "cuda"
-    alloc = torch.cuda.memory_allocated(device) / _MIB if on_gpu else 0.0
-    peak = torch.cuda.max_memory_allocated(device) / _MIB if on_gpu else 0.0
+    from ..engine import placed_bytes
+
+    placed = placed_bytes() / _MIB if on_gpu else 0.0
+    alloc = torch.cuda.memory_allocated(device) / _MIB + placed if on_gpu else 0.0
+    peak = torch.cuda.max_memory_allocated(device) / _MIB + placed if on_gpu else 0.0
     return MemoryReport(p_l, g_l, o_l, p_p, g_p, o_p, alloc, peak)
 
 

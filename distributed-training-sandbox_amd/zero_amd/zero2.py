@@ -6,11 +6,25 @@ zero2.py:99-107), the owner averages it (zero2.py:111) and steps Adam on its ind
 (zero2.py:120), then each param is broadcast from its owner (zero2.py:122-133).  The result is
 exactly data-parallel Adam.
 
-Here: grads are packed into buckets laid out owner-major (Layout R), one in-place RCCL
-reduce-scatter per bucket delivers each owner the summed grads of exactly the params it owns,
-the fused HIP Adam divides by ws and updates them, and one in-place all-gather per bucket
-replaces the per-param broadcasts.  Ownership, and therefore optimizer-state placement, is
-bit-identical to the reference.
+Here:
+  * default ``arena="flat"``: every parameter is a view of one owner-major *flat parameter
+    arena* (rank r's owned parameters, Layout R, are the contiguous stretch [base_r, base_r+L_r)),
+    and after ``zero_grad()`` every ``p.grad`` is a view of a flat gradient arena of the same
+    layout, so backward accumulates straight into it.  A step is a few *rounds* (window j of every
+    owner's stretch): ONE RCCL group of per-owner ``ncclReduce`` — each owner's window of the
+    gradient arena summed into its reduced buffer, the reduce-scatter-v of zero2.py:94-113 —, the
+    fused HIP Adam on the own window (``/ws`` folded in) writing the updated parameters straight
+    into the arena, and ONE RCCL group of in-place ``ncclBroadcast`` of every owner's window, the
+    all-gather-v of zero2.py:122-133.  No pack, no unpack: the parameters are the arena.  After
+    the step ``p.grad`` is still the arena view holding this rank's local gradient (the reduce is
+    out of place); ``zero_grad()`` zeroes it.  ``overlap=True`` launches each round's reduces from
+    backward hooks as buckets complete.
+  * ``arena="buckets"``: parameters and grads stay where the caller put them; grads are packed
+    into rank-major buckets, one in-place RCCL reduce-scatter per even bucket (grouped per-owner
+    reduce / broadcast for the ragged tail) delivers each owner its summed grads, Adam updates
+    them, an in-place all-gather per bucket replaces the per-param broadcasts, then unpack; grads
+    are released after the step.
+Ownership, and therefore optimizer-state placement, is bit-identical to the reference on both.
 """
 from __future__ import annotations
 

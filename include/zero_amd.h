@@ -24,7 +24,12 @@
 extern "C" {
 #endif
 
-#define ZS_ABI_VERSION 9
+/* Callers check zs_abi_version() == ZS_ABI_VERSION before any other call: version 7 kept the
+ * names zs_plan_create / zs_adam_step but changed their argument lists (the version-6 forms are
+ * the *_ex entry points), so a caller built against an older header links and then passes the
+ * wrong arguments.  The Python binding (zero_amd/_lib.py) and tests/c/abi_host.c refuse a
+ * mismatch. */
+#define ZS_ABI_VERSION 10
 
 enum zs_status {
   ZS_OK = 0,
@@ -260,7 +265,8 @@ int zs_adamset_stats(const zs_adamset* as, int64_t* elems, int64_t* bytes);
  * table to build.  p: fp32 master/param, updated in place; p_bf16: optional bf16 copy of the
  * result (NULL = none); g: reduced gradient sum (g_dtype ZS_F32 or ZS_BF16; NULL = zero); m, v:
  * fp32 exp_avg / exp_avg_sq, in place; carry: ZeRO-1's A_{t-1}, READ AND REWRITTEN with A_t
- * (NULL = none) although spelled const here; carry_scale: ws-1.  grad_scale = 1/ws: the update
+ * (NULL = none; SURVEY.md §8(b) spells it const, but the kernel writes it, so it is declared
+ * writable — same C calling convention); carry_scale: ws-1.  grad_scale = 1/ws: the update
  * divides by the float nearest to 1/grad_scale (the world size), as zero1.py:84 `p.grad /= ws`.
  * The float scalars are widened to double before torch's bias-correction arithmetic; torch
  * derives them from Python doubles (adam.py:508-515), so for torch's bits with hyper-parameters
@@ -269,7 +275,7 @@ int zs_adamset_stats(const zs_adamset* as, int64_t* elems, int64_t* bytes);
  * Asynchronous on `stream`; its two-entry table is a stream-ordered allocation. */
 int zs_adam_step(float* p, uint16_t* p_bf16, const void* g, int g_dtype, float* m, float* v,
                  int64_t n, float lr, float b1, float b2, float eps, float wd, int decoupled,
-                 int64_t step, float grad_scale, const float* carry, float carry_scale,
+                 int64_t step, float grad_scale, float* carry, float carry_scale,
                  uintptr_t stream);
 /* The same with torch's double scalars and the divisor itself (grad_div = ws; for a
  * non-power-of-two ws dividing is not multiplying by 1/ws): bit-exact with torch's arithmetic. */
@@ -277,6 +283,18 @@ int zs_adam_step_ex(float* p, uint16_t* p_bf16, const void* g, int g_dtype, floa
                     int64_t n, double lr, double beta1, double beta2, double eps,
                     double weight_decay, int decoupled, int64_t step, double grad_div, float* carry,
                     double carry_mul, uintptr_t stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Device buffers outside the caller's caching allocator (ABI v10).  The placement probe          */
+/* (zero_amd/engine.py probed_zeros) streams candidate allocations of a long-lived, bandwidth-    */
+/* bound buffer and keeps the fastest; candidates come from here so a rejected one goes straight */
+/* back to the device without emptying torch's cache (the caller's cached blocks stay).          */
+/* ------------------------------------------------------------------------------------------ */
+/* hipMalloc of `bytes` (> 0) into *out; ZS_ERR_NOMEM when the device is full. */
+int zs_device_alloc(int64_t bytes, void** out);
+/* hipFree (NULL is a no-op).  Synchronises the device as hipFree does: only for buffers no queued
+ * work still uses. */
+int zs_device_free(void* p);
 
 /* ------------------------------------------------------------------------------------------ */
 /* RCCL over xGMI.  Replaces the per-tensor dist.all_reduce (zero1.py:83, zero3.py:146),        */

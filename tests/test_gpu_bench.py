@@ -34,7 +34,8 @@ def test_bench_json_line_n1(gpu):
                 "--warmup", "1", "--no-cpu-baseline"])
     assert KEYS <= set(out) and out["n_gpus"] == 1 and out["value"] > 0
     rf = out["roofline"]
-    assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1.2 and rf["achieved"] > 0
+    # above 1 the timed kernel would not be doing its algorithmic work: fail
+    assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1.0 and rf["achieved"] > 0
     assert "fp32_master" not in out  # fp32 parameters: the master is the parameter
 
 

@@ -1,0 +1,62 @@
+"""Placement probe side effects (engine.probed_zeros): the candidates are
+device allocations of their own (zs_device_alloc), so building an optimizer never releases the
+CALLER's cached blocks (no torch.cuda.empty_cache() inside the constructor), the kept buffer is a
+placed allocation counted by placed_bytes(), and it is returned to the device with its tensors."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _segments():
+    return {s["address"] for s in torch.cuda.memory_snapshot()}
+
+
+@pytest.fixture
+def pg1():
+    import torch.distributed as dist
+
+    from _zero_run import init_pg
+    from conftest import free_port
+
+    init_pg(0, 1, free_port())
+    yield
+    dist.destroy_process_group()
+
+
+def test_probe_keeps_callers_cached_block(gpu, pg1):
+    from zero_amd import engine, zero2
+    from zero_amd.shapes import mlp_shapes
+
+    dev = gpu
+    torch.cuda.synchronize()
+    params = [torch.nn.Parameter(torch.zeros(s, device=dev)) for s in mlp_shapes(12800)]  # C3, fp32
+    blk = torch.empty(1 << 30, dtype=torch.uint8, device=dev)  # the caller's own 1 GiB block ...
+    addr = blk.data_ptr()
+    del blk  # ... now cached by torch, not in use
+    assert addr in _segments()
+    before = engine.placed_bytes()
+    opt = zero2.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), sync=True)
+    for p in params:
+        p.grad = torch.full_like(p, 1e-3)
+    opt.step()  # builds the engine: state (7.9 GB fp32) placed by the probe
+    torch.cuda.synchronize()
+    assert addr in _segments(), "the caller's cached 1 GiB block was released by the probe"
+    pl = opt.engine.placement
+    assert pl.get("allocator", "").startswith("zs_device_alloc") and pl["tries"] >= 1, pl
+    assert 0 <= pl["chosen"] < pl["tries"] == len(pl["gbs"]) and pl["unprobed_gbs"] == pl["gbs"][0]
+    held = engine.placed_bytes() - before
+    assert held >= 2 * sum(p.numel() for p in params) * 4, held  # exp_avg + exp_avg_sq at least
+    # the state is outside torch's allocator: none of its storages is a torch segment
+    st = opt.engine.state
+    assert st.untyped_storage().data_ptr() not in _segments()
+    # Adam's first step on a constant grad: every parameter moved by -lr (bias-corrected)
+    assert torch.allclose(params[0][:2, :4], torch.full((2, 4), -1e-3, device=dev), rtol=1e-4)
+    free0 = torch.cuda.mem_get_info(dev)[0]
+    del opt, st
+    import gc
+
+    gc.collect()
+    torch.cuda.synchronize()
+    assert engine.placed_bytes() == before  # placed buffers went back with their tensors
+    assert torch.cuda.mem_get_info(dev)[0] > free0 + held // 2

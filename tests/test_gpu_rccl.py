@@ -131,12 +131,16 @@ def test_rccl_zero3(gpu, rccl_env, ws):
 
 
 # --- bench.py at N = 2 on the shared GPU ------------------------------------------------
-def _bench2(args, timeout=300):
+def _bench2(args, timeout=300, launcher=True):
+    """bench.py at N = 2 on the shared GPU, under torch.distributed.run (the driver's SCALE form)
+    or, with ``launcher=False``, as plain ``python bench.py --gpus 2`` (bench.py starts the two
+    ranks itself)."""
     env = dict(os.environ, **CHILD_ENV)
-    env.pop("ZS_TEST_COMM", None)
-    env.pop("NCCL_HOSTID", None)  # bench --share-gpu sets it per rank
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2",
+    for k in ("ZS_TEST_COMM", "NCCL_HOSTID", "WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)  # (bench --share-gpu sets NCCL_HOSTID per rank)
+    launch = ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+              "127.0.0.1", "--master-port", str(free_port())] if launcher else []
+    cmd = [sys.executable, *launch, "bench.py", "--gpus", "2",
            "--share-gpu", "--no-cpu-baseline", "--watchdog-s", str(timeout - 30)] + args
     r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
@@ -149,10 +153,14 @@ def _bench2(args, timeout=300):
 def test_bench_share_gpu_exchange_check(gpu, zero):
     """The N>1 bench path against real RCCL: communicator self-check, the exchange check of BOTH
     arenas (one real engine step on the bf16 arena vs the exact fp32 sum and a PyTorch Adam
-    restatement; bit-identical parameters on every rank), calibration, timed steps."""
+    restatement; bit-identical parameters on every rank), calibration, timed steps.  ZeRO-2 runs
+    as plain ``python bench.py --gpus 2`` (no launcher: bench.py starts the two ranks itself)."""
     out = _bench2(["--config", "C2", "--dtype", "bf16", "--zero", str(zero), "--steps", "3",
-                   "--warmup", "1", "--no-comm-sweep"])
+                   "--warmup", "1", "--no-comm-sweep"], launcher=zero == 1)
     assert out["n_gpus"] == 2 and out["rccl_selfcheck"]["all_ranks_ok"]
+    assert out["config"]["parallelism"] == "dp2"
+    for kind in ("flat", "buckets"):
+        assert out["arena_calibration"][kind]["busbw_gbs"] > 0, out["arena_calibration"]
     assert out["config"]["comm"] == "rccl", out["config"]["comm"]
     assert out["rehearsal"].startswith("share-gpu")
     checks = out["exchange_check_all_arenas"]
@@ -233,6 +241,10 @@ def _bench_rank(rank, ws, port, argv):
             assert c["reduce_max_err_over_bound"] <= 1.0 and c["adam_max_bf16_ulp"] <= 1, (kind, c)
             assert c["params_identical_across_ranks"], (kind, c)
         assert set(out["arena_calibration_ms_per_step"]) == {"flat", "buckets"}
+        cal = out["arena_calibration"]
+        for kind in ("flat", "buckets"):  # each exchange's own bus bandwidth, not only its step
+            assert cal[kind]["busbw_gbs"] > 0 and cal[kind]["frac_of_peer_links"] > 0, cal
+            assert cal[kind]["ms_per_step"] == out["arena_calibration_ms_per_step"][kind]
         assert out["rccl_selfcheck"]["all_ranks_ok"] and out["config"]["comm"] == "rccl"
 
 

@@ -1,3 +1,5 @@
+# Round-3 snapshot of zero_amd/zero3.py (git HEAD at the start of round 4): the A/B baseline of
+# tools/z3_host_ab.py --baseline r03.  Not part of the product.
 """ZeRO-3 drop-in: ``Zero3ParamManager``, ``register_zero3_hooks`` and ``ShardedOptimizer`` of
 reference zero/zero3.py:25-168, MI355X-native.
 
@@ -147,7 +149,6 @@ class _GatherRuntime:
         # keeps the record it saw, and a key's next launch comes after its materialise has
         # enqueued that wait (creating two HIP events per gather cost host time every iteration)
         self._events = {}
-        self.iteration_callbacks = []  # called by end_iteration (hook bookkeeping resets)
 
     def _key_events(self, key):
         ev = self._events.get(key)
@@ -164,7 +165,7 @@ class _GatherRuntime:
             return
         if self.ws == 1 and not any(m.fp8 for m in managers):
             # the shard is the whole parameter: nothing to gather, no stream to synchronise with
-            self.pending[key] = ([(m, m._gather_prepare(None)[1]) for m in managers], None, None, None)
+            self.pending[key] = ([(m, m._gather_prepare(None)[1]) for m in managers], None, None)
             self.n_gathers += 1
             return
         ev_ready, ev, ready_h, ev_h = self._key_events(key)
@@ -183,7 +184,7 @@ class _GatherRuntime:
             np.add(offs, np.uint64(hold.data_ptr()), out=recv)
             ordered(cur.cuda_stream, ready_h, self._side_h, ev_h)
             self.pending[key] = ([(m, hold.as_strided(shape, stride, off)) for m, (shape, stride, off)
-                                  in zip(managers, views)], ev, hold, cur)
+                                  in zip(managers, views)], ev, hold)
             self.n_gathers += 1
             return
         ev_ready.record(cur)  # shards may just have been updated
@@ -232,7 +233,7 @@ class _GatherRuntime:
         if timed:  # ring all-gather bus bytes: (ws-1)/ws of the gathered tensor, per rank
             bus = sum(m.gather_bytes() for m in managers) * (self.ws - 1)
             self.gather_events.append((e0, _timed_after(side), bus))
-        self.pending[key] = (out, ev, hold, cur)
+        self.pending[key] = (out, ev, hold)
         self.n_gathers += 1
 
     def _table(self, key, managers):
@@ -378,7 +379,7 @@ class _GatherRuntime:
         if key in self.pending:
             self.n_prefetch_hits += 1
         self.launch(key, managers, cur)
-        out, ev, hold, alloc_stream = self.pending.pop(key)
+        out, ev, hold = self.pending.pop(key)
         if ev is None:  # ws == 1
             for m, full in out:
                 m._install_full(full)
@@ -386,10 +387,6 @@ class _GatherRuntime:
         rc = _lib.lib.zs_stream_wait_event(cur.cuda_stream, self._events[key][3])
         if rc:
             _lib.check(rc, "zs_stream_wait_event")
-        if hold is not None and alloc_stream is not None and alloc_stream != cur:
-            # prefetched under another current stream (a user stream in forward, autograd's in
-            # backward): the allocator must not reuse the block while THIS stream reads it
-            hold.record_stream(cur)
         if hold is not None:  # one allocation (on this stream) behind all of the module's full
             for m, full in out:  # tensors, whose views already have the full shapes
                 m.full_data = full
@@ -400,8 +397,6 @@ class _GatherRuntime:
             m._install_full(full)
 
     def end_iteration(self):
-        for fn in self.iteration_callbacks:
-            fn()
         if self.sequence:
             self.recording = False
         self.pending.clear()
@@ -512,7 +507,7 @@ class Zero3ParamManager:
         rt = self._runtime()
         key = ("param", id(self))
         rt.launch(key, [self])
-        out, ev, hold, _ = rt.pending.pop(key)
+        out, ev, hold = rt.pending.pop(key)
         cur = torch.cuda.current_stream(self.shard.device)
         if ev is not None:
             cur.wait_event(ev)
@@ -659,40 +654,17 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
 
     # backward_hooks == "tensor"
     pre_bwd = make_pre("bwd")
-    pre_fwd = make_pre("fwd")
     post_fwd = make_post("fwd")
     hooked = [m for m in model.modules() if mod_managers[id(m)]]
-    managed = [mg for m in hooked for mg in mod_managers[id(m)]]
-    # per backward: how many of a module's parameters will count in (trainable ones), and which
-    # modules each trainable parameter counts in; re-derived at the first backward gather of a
-    # backward whenever requires_grad changed since (gradual unfreezing, frozen layers)
-    n_req, param_mods, hooked_params = {}, {}, set()
-    trainable_sig = [None]
-
-    def recount():
-        sig = tuple(mg.param.requires_grad for mg in managed)
-        if sig == trainable_sig[0]:
-            return
-        trainable_sig[0] = sig
-        n_req.clear()
-        param_mods.clear()
-        for m in hooked:
-            n_req[id(m)] = sum(1 for mg in mod_managers[id(m)] if mg.param.requires_grad)
-            for mg in mod_managers[id(m)]:
-                if mg.param.requires_grad:
-                    param_mods.setdefault(id(mg.param), []).append(id(m))
-        for mg in managed:
-            p = mg.param
-            if p.requires_grad and id(p) not in hooked_params:
-                # newly trainable: its post-accumulate hook from now on (keyed by id, so the hook
-                # the parameter holds keeps no reference to it)
-                hooked_params.add(id(p))
-                handles.append(_add_post_accumulate_hook(p, functools.partial(grad_ready, id(p))))
-
+    n_req = {id(m): sum(1 for mg in mod_managers[id(m)] if mg.param.requires_grad) for m in hooked}
+    param_mods = {}
+    for m in hooked:
+        for mg in mod_managers[id(m)]:
+            if mg.param.requires_grad:
+                param_mods.setdefault(mg.param, []).append(id(m))
     open_ = {}     # id(module) -> managers gathered for its backward, not released yet
     pending = {}   # id(module) -> parameter gradients still to come this backward
     queued = [False]
-    warned = set()
 
     def end_backward():
         queued[0] = False
@@ -700,28 +672,19 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
             for mg in ms:
                 mg.release()
         open_.clear()
-        pending.clear()
-
-    def reset_stale():
-        """A backward that raised before its end-of-backward callback ran leaves modules open and
-        the callback flag set; the next forward (outside any backward) releases them and resets."""
-        if queued[0] and torch._C._current_graph_task_id() == -1:
-            end_backward()
 
     def backward_pre(module):
         mid = id(module)
         if not queued[0]:
             queued[0] = True
-            recount()
             torch.autograd.Variable._execution_engine.queue_callback(end_backward)
         pre_bwd(module)
-        open_[mid] = mod_managers[mid]
-        # nothing will count in: released at the end of backward
-        pending[mid] = n_req.get(mid, 0) or -1
-
-    def forward_pre(module, *args):
-        reset_stale()
-        return pre_fwd(module, *args)
+        if n_req[mid]:
+            open_[mid] = mod_managers[mid]
+            pending[mid] = n_req[mid]
+        else:  # nothing will count in: released at the end of backward
+            open_[mid] = mod_managers[mid]
+            pending[mid] = -1
 
     def forward_post(module, args, output):
         post_fwd(module)
@@ -732,20 +695,10 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
             elif ts:
                 torch.autograd.graph.register_multi_grad_hook(
                     ts, lambda _g, module=module: backward_pre(module), mode="any")
-            elif id(module) not in warned and any(mg.param.requires_grad
-                                                   for mg in mod_managers[id(module)]):
-                warned.add(id(module))
-                import warnings
-
-                warnings.warn(
-                    f"zero_amd ZeRO-3: {type(module).__name__}'s output holds no tensor that "
-                    "requires grad, so its parameters get no backward gather from the tensor-style "
-                    "hooks; use register_zero3_hooks(..., backward_hooks='module') for such modules",
-                    RuntimeWarning, stacklevel=2)
         return None
 
-    def grad_ready(pid, _p):
-        for mid in param_mods.get(pid, ()):
+    def grad_ready(mids, _p):
+        for mid in mids:
             if mid in open_:
                 pending[mid] -= 1
                 if pending[mid] == 0:
@@ -753,11 +706,11 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
                         mg.release()
 
     for m in hooked:
-        handles.append(m.register_forward_pre_hook(forward_pre))
+        handles.append(m.register_forward_pre_hook(make_pre("fwd")))
         handles.append(m.register_forward_hook(forward_post))
-    recount()
-    for rt in runtimes:  # the end of every step() also clears what a failed backward left
-        rt.iteration_callbacks.append(reset_stale)
+    for p, mids in param_mods.items():
+        # the modules each parameter counts in, bound once (no tensor hashing per backward)
+        handles.append(_add_post_accumulate_hook(p, functools.partial(grad_ready, tuple(mids))))
     return handles
 
 
@@ -1354,10 +1307,7 @@ class ShardedOptimizer:
         so the list stays a step or two long and the counter trails by as much."""
         keep = []
         for e0, e1 in self._comm_spans:
-            # both ends must have completed: e0 sits on the compute stream, which can still hold
-            # queued work after every reduce-scatter on the side stream (e1) has finished, and
-            # hipEventElapsedTime on an incomplete event fails
-            if completed_only and not (e1.query() and e0.query()):
+            if completed_only and not e1.query():
                 keep.append((e0, e1))
                 continue
             self.communication_time += max(0.0, e0.elapsed_time(e1) / 1e3)

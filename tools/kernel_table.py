@@ -47,7 +47,7 @@ def main():
     st = torch.cuda.current_stream(dev)
     rows = []
 
-    def timed(name, launch, alg_bytes, note):
+    def timed(name, launch, alg_bytes, note, rocprof=None, per_call=1):
         launch()  # warm
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -59,7 +59,9 @@ def main():
         ms = e0.elapsed_time(e1) / args.iters
         gbs = alg_bytes / (ms / 1e3) / 1e9
         row = {"kernel": name, "avg_launch_ms": ms, "alg_bytes_per_launch": int(alg_bytes),
-               "achieved_gbs": gbs, "frac": gbs / HBM_PEAK_GBS, "workload": note}
+               "achieved_gbs": gbs, "frac": gbs / HBM_PEAK_GBS, "workload": note,
+               # for tools/kernel_pmc.py: the rocprof kernel-name prefix and dispatches per call
+               "rocprof_kernel": rocprof, "dispatches_per_call": per_call}
         rows.append(row)
         print(json.dumps(row), flush=True)
 
@@ -69,20 +71,36 @@ def main():
     dst, _ = probed_zeros(n, torch.bfloat16, dev)
     src.normal_()
     timed("convert_kernel<true> (fp32->bf16)", lambda: convert(src, dst, st), 6 * n,
-          f"C3 gradient, {n:,} elements (grad_comm='bf16')")
+          f"C3 gradient, {n:,} elements (grad_comm='bf16')", "convert_kernel<true>")
     timed("convert_kernel<false> (bf16->fp32)", lambda: convert(dst, src, st), 6 * n,
-          f"C3 gradient, {n:,} elements")
+          f"C3 gradient, {n:,} elements", "convert_kernel<false>")
     del src, dst
     torch.cuda.empty_cache()
 
-    # fp8 row quantise / dequantise: one C5 decoder layer's matrices (bf16)
+    # fp8 row quantise / dequantise: one C5 decoder layer's matrices (bf16), in placed buffers
+    # (engine.probed_zeros, as every HBM-sized buffer of the product path) so the kernels are
+    # measured on the same kind of memory as Adam; the in-place copy rows at the end give the
+    # streaming rate of these very buffers (the ceiling the kernels can reach here)
     layer = [s for s in decoder_shapes("C5", 1)[1:10] if len(s) == 2]
-    mats = [torch.randn(s, device=dev).to(torch.bfloat16) for s in layer]
-    qs = [torch.empty(s, dtype=torch.uint8, device=dev) for s in layer]
-    scs = [torch.empty(s[0], dtype=torch.float32, device=dev) for s in layer]
-    outs = [torch.empty(s, dtype=torch.bfloat16, device=dev) for s in layer]
     elems = sum(int(np.prod(s)) for s in layer)
     nrows = sum(s[0] for s in layer)
+    gib = 1 << 30
+    src_buf, _ = probed_zeros(max(elems, gib // 2), torch.bfloat16, dev)
+    q_buf, _ = probed_zeros(max(elems + 64 * len(layer), gib), torch.uint8, dev)
+    out_buf, _ = probed_zeros(max(elems, gib // 2), torch.bfloat16, dev)
+    sc_buf = torch.empty(nrows + 64 * len(layer), dtype=torch.float32, device=dev)
+    mats, qs, scs, outs, o = [], [], [], [], 0
+    so = 0
+    for s_ in layer:
+        k = int(np.prod(s_))
+        mats.append(src_buf[o:o + k].view(s_))
+        qs.append(q_buf[o:o + k].view(s_))
+        outs.append(out_buf[o:o + k].view(s_))
+        scs.append(sc_buf[so:so + s_[0]])
+        o += k
+        so += s_[0]
+    for x in mats:
+        x.normal_()
 
     def quant():
         for x, q, sc in zip(mats, qs, scs):
@@ -95,37 +113,39 @@ def main():
                       _lib.ZS_BF16, q.shape[0], q.shape[1], stream_handle(st))
 
     timed("fp8_quantize_rows_kernel<bf16> (7 launches, one per matrix)", quant,
-          3 * elems + 4 * nrows, f"one C5 decoder layer, {elems:,} bf16 elements")
-    timed("fp8_dequantize_rows_kernel<bf16> (7 launches)", dequant, 3 * elems + 4 * nrows,
-          f"one C5 decoder layer, {elems:,} elements")
-    # the same layer through the gather group's fused forms (round 3): one quantise launch per
-    # register class into one concatenated send buffer, one dequantise launch from it (ws = 1
-    # layout: the gathered buffer is the send buffer)
+          3 * elems + 4 * nrows, f"one C5 decoder layer, {elems:,} bf16 elements",
+          "fp8_quantize_rows_wave_kernel<unsigned short,", len(layer))
+    timed("fp8_dequantize_rows (7 launches, one per matrix; the gathered kernel at ws = 1)", dequant,
+          3 * elems + 4 * nrows, f"one C5 decoder layer, {elems:,} elements",
+          "fp8_dequantize_gathered_kernel<unsigned short>", len(layer))
+    # the same layer through the gather group's fused forms: one quantise launch per register
+    # class into one concatenated send buffer, one dequantise launch from it (ws = 1 layout: the
+    # gathered buffer is the send buffer)
     shp = [tuple(x.shape) for x in mats]
     q_off = np.cumsum([0] + [r * c for r, c in shp])[:-1].astype(np.int64)
     sc_off = np.cumsum([0] + [r for r, _ in shp])[:-1].astype(np.int64)
     qtot, sctot = int(sum(r * c for r, c in shp)), int(sum(r for r, _ in shp))
-    qcat = torch.empty(qtot, dtype=torch.uint8, device=dev)
-    scat = torch.empty(sctot, dtype=torch.float32, device=dev)
     src = np.array([x.data_ptr() for x in mats], np.uint64)
-    qp = np.uint64(qcat.data_ptr()) + q_off.astype(np.uint64)
-    sp = np.uint64(scat.data_ptr()) + (sc_off * 4).astype(np.uint64)
+    qp = np.uint64(q_buf.data_ptr()) + q_off.astype(np.uint64)
+    sp = np.uint64(sc_buf.data_ptr()) + (sc_off * 4).astype(np.uint64)
     rows_a = np.array([r for r, _ in shp], np.int64)
     len_a = np.array([c for _, c in shp], np.int64)
     dst = np.array([y.data_ptr() for y in outs], np.uint64)
+    nreg = sorted({8 if c <= 4096 else 16 if c <= 8192 else 32 for c in len_a})
     timed(f"fp8_quantize_rowset_kernel<bf16> ({len(mats)} matrices, one launch per register class)",
           lambda: _lib.call("zs_fp8_quantize_rowset", len(mats), src.ctypes.data, qp.ctypes.data,
                             sp.ctypes.data, rows_a.ctypes.data, rows_a.ctypes.data,
                             len_a.ctypes.data, _lib.ZS_BF16, stream_handle(st)),
-          3 * elems + 4 * nrows, f"one C5 decoder layer, {elems:,} bf16 elements")
+          3 * elems + 4 * nrows, f"one C5 decoder layer, {elems:,} bf16 elements",
+          "fp8_quantize_rowset_kernel<unsigned short,", len(nreg))
     timed(f"fp8_dequantize_gathered_kernel<bf16> ({len(mats)} matrices, one launch)",
-          lambda: _lib.call("zs_fp8_dequantize_gathered", len(mats), qcat.data_ptr(),
-                            scat.data_ptr(), 1, qtot, sctot, q_off.ctypes.data, sc_off.ctypes.data,
+          lambda: _lib.call("zs_fp8_dequantize_gathered", len(mats), q_buf.data_ptr(),
+                            sc_buf.data_ptr(), 1, qtot, sctot, q_off.ctypes.data, sc_off.ctypes.data,
                             rows_a.ctypes.data, len_a.ctypes.data, dst.ctypes.data, _lib.ZS_BF16,
                             stream_handle(st)),
-          3 * elems + 4 * nrows, f"one C5 decoder layer, {elems:,} elements")
-    del mats, qs, scs, outs, qcat, scat
-    torch.cuda.empty_cache()
+          3 * elems + 4 * nrows, f"one C5 decoder layer, {elems:,} elements",
+          "fp8_dequantize_gathered_kernel<unsigned short>", 1)
+    # (the in-place copies over these buffers run at the very end: see below)
 
     # DDP scale, in place: a 256 MiB bucket (fits the 256 MB MALL, so repeated launches partly hit
     # it — the figure is not an HBM rate) and a 4 GiB buffer (HBM-bound, placed by the probe)
@@ -140,7 +160,8 @@ def main():
             timed(f"scale_kernel<{'bf16' if es == 2 else 'f32'}> (/3, in place, {mib} MiB)",
                   lambda b=b, code=code: _lib.call("zs_scale", b.data_ptr(), b.numel(), code, 3.0,
                                                    stream_handle(st)),
-                  2 * es * m, f"DDP bucket, {mib} MiB {dt}" + (" (MALL-resident)" if mib <= 256 else ""))
+                  2 * es * m, f"DDP bucket, {mib} MiB {dt}" + (" (MALL-resident)" if mib <= 256 else ""),
+                  f"scale_kernel<{'unsigned short' if es == 2 else 'float'}>")
             del b
             torch.cuda.empty_cache()
 
@@ -159,7 +180,15 @@ def main():
         a += -(-k // 64) * 64
     cs = CopySet(src, dst, nb)
     timed("copy_segments_kernel (pack, 326 segments)", lambda: cs.run(st), 2 * cs.nbytes,
-          f"C4 bf16 grads, {total:,} elements, one launch")
+          f"C4 bf16 grads, {total:,} elements, one launch", "copy_segments_kernel<")
+    del grads, arena, cs
+    # the streaming rate of the fp8 rows' own buffers (in-place float4 copy, read + write): the
+    # ceiling those kernels can reach on this memory
+    for nm, buf in (("fp8 layer output buffer", out_buf), ("fp8 layer q buffer", q_buf)):
+        nb = buf.numel() * buf.element_size()
+        cp = CopySet([buf.data_ptr()], [buf.data_ptr()], [nb])
+        timed(f"copy_segments_kernel (in place, {nm})", lambda cp=cp: cp.run(st), 2 * nb,
+              f"{nb:,} B, the buffer the fp8 rows use", "copy_segments_kernel<")
     if args.out:
         Path(args.out).write_text(json.dumps({"iters": args.iters, "peak_gbs": HBM_PEAK_GBS,
                                               "rows": rows}, indent=1))

@@ -6,7 +6,8 @@ host time).  Wall time per iteration and process CPU time (all threads: the back
 autograd's device thread) per block — the box's host speed drifts by 30 % over minutes, so only
 the interleaved comparison means anything.
 
-Usage: python tools/z3_host_ab.py [--config C5] [--ws 8] [--iters 20] [--blocks 6]
+Usage: python tools/z3_host_ab.py [--config C5] [--ws 8] [--iters 20] [--blocks 6] [--baseline r02|r03]
+(--baseline r03: tools/_zero3_r03.py, the round-3 runtime, against the current one)
 """
 from __future__ import annotations
 
@@ -30,6 +31,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--baseline", default="r02", choices=["r02", "r03"])
+    ap.add_argument("--out", default=None)
     args = ap.parse_args()
 
     import torch
@@ -41,14 +44,16 @@ def main():
     from zero_amd.paramset import ParamSetModel, decoder_layer_groups
     from zero_amd.shapes import CONFIGS
 
-    spec = importlib.util.spec_from_file_location("zero_amd._zero3_r02", REPO / "tools" / "_zero3_r02.py")
+    base = "round2" if args.baseline == "r02" else "round3"
+    spec = importlib.util.spec_from_file_location(f"zero_amd._zero3_{args.baseline}",
+                                                  REPO / "tools" / f"_zero3_{args.baseline}.py")
     z3_old = importlib.util.module_from_spec(spec)
     sys.modules[spec.name] = z3_old
     spec.loader.exec_module(z3_old)
     assert z3_old.__package__ == zero_amd.__name__
 
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29563")
+    os.environ.setdefault("MASTER_PORT", str(bench._free_port()))
     dist.init_process_group("gloo", rank=0, world_size=1)
     dev = torch.device("cuda:0")
     shapes = CONFIGS[args.config][1]()
@@ -76,14 +81,14 @@ def main():
             opt.step()
         return step
 
-    variants = {"round2": build(z3_old, 0), "current": build(z3_new, 0)}
+    variants = {base: build(z3_old, 0), "current": build(z3_new, 0)}
     for st in variants.values():
         for _ in range(args.warmup):
             st()
     torch.cuda.synchronize()
     rows = []
     for b in range(args.blocks):
-        for name in (("round2", "current") if b % 2 == 0 else ("current", "round2")):
+        for name in ((base, "current") if b % 2 == 0 else ("current", base)):
             st = variants[name]
             torch.cuda.synchronize()
             w0, c0 = time.perf_counter(), time.process_time()
@@ -100,8 +105,11 @@ def main():
         cs_ = sorted(r["cpu_ms"] for r in rows if r["variant"] == name)
         summ[name] = {"wall_ms_median": ws_[len(ws_) // 2], "wall_ms_min": ws_[0],
                       "cpu_ms_median": cs_[len(cs_) // 2], "cpu_ms_min": cs_[0]}
-    print(json.dumps({"config": args.config, "simulated_ws": ws, "iters_per_block": args.iters,
-                      "summary": summ}), flush=True)
+    res = {"config": args.config, "simulated_ws": ws, "iters_per_block": args.iters,
+           "baseline": base, "summary": summ}
+    print(json.dumps(res), flush=True)
+    if args.out:
+        Path(args.out).write_text(json.dumps(dict(res, blocks=rows), indent=1) + "\n")
     dist.destroy_process_group()
 
 

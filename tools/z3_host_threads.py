@@ -1,0 +1,118 @@
+"""Where the host CPU of the hooked ZeRO-3 iteration goes, per thread.
+
+Rank 0 of a simulated ws-rank job on the configs[4] parameter set (C5: 34 layer modules, 291
+tensors; collectives no-ops, so the GPU runs only Adam): wall time and process CPU time per
+iteration, split by thread — the main thread (forward hooks, step), autograd's device thread
+(backward hooks: gathers, releases, reduce-scatter bucket launches) and every other thread of the
+process (HIP runtime) — from psutil's per-thread CPU times around blocks of iterations.  Blocks
+alternate nothing: this is a breakdown, not an A/B (tools/z3_host_ab.py is the A/B).
+
+Usage: python tools/z3_host_threads.py [--config C5] [--ws 8] [--iters 20] [--blocks 5]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO / "distributed-training-sandbox_amd"))
+sys.path.insert(0, str(REPO))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C5")
+    ap.add_argument("--ws", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--blocks", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+
+    import psutil
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    from zero_amd import zero3
+    from zero_amd.paramset import ParamSetModel, decoder_layer_groups
+    from zero_amd.shapes import CONFIGS
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(bench._free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    dev = torch.device("cuda:0")
+    shapes = CONFIGS[args.config][1]()
+    ws = args.ws
+    gen = torch.Generator(device=dev).manual_seed(0)
+    params = [torch.nn.Parameter(torch.empty(s, device=dev, dtype=torch.bfloat16).normal_(
+        0.0, 0.02, generator=gen)) for s in shapes]
+    grads = [torch.empty(s, device=dev, dtype=torch.bfloat16).normal_(0.0, 1e-3, generator=gen)
+             for s in shapes]
+    model = ParamSetModel(params, decoder_layer_groups(len(shapes)))
+    model.set_grad_source(grads)
+    real_get = zero3.get
+    zero3.get = lambda what, dm=None: {"ws": ws, "rank": 0}.get(what) if what in ("ws", "rank") \
+        else real_get(what, dm)
+    opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
+                                 sync=False, comm=bench._NoComm(ws))
+    zero3.register_zero3_hooks(model, opt.param_managers)
+    x = torch.zeros(1, device=dev, requires_grad=True)
+    bwd_tid = set()
+    params[0].register_post_accumulate_grad_hook(lambda p: bwd_tid.add(threading.get_native_id()))
+
+    def step():
+        opt.zero_grad()
+        model(x).sum().backward()
+        opt.step()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    proc = psutil.Process()
+    main_tid = threading.get_native_id()
+
+    def snap():
+        return {t.id: t.user_time + t.system_time for t in proc.threads()}
+
+    rows = []
+    for b in range(args.blocks):
+        torch.cuda.synchronize()
+        s0, w0, c0 = snap(), time.perf_counter(), time.process_time()
+        for _ in range(args.iters):
+            step()
+        torch.cuda.synchronize()
+        w, c, s1 = time.perf_counter() - w0, time.process_time() - c0, snap()
+        d = {tid: s1[tid] - s0.get(tid, 0.0) for tid in s1}
+        n = args.iters
+        main = d.get(main_tid, 0.0)
+        bwd = sum(d.get(t, 0.0) for t in bwd_tid if t != main_tid)
+        other = sum(v for t, v in d.items() if t != main_tid and t not in bwd_tid)
+        busy = sorted(((round(v / n * 1e3, 3), t) for t, v in d.items()
+                       if t != main_tid and t not in bwd_tid and v > 0), reverse=True)[:4]
+        rows.append({"block": b, "wall_ms": round(w / n * 1e3, 3), "cpu_ms": round(c / n * 1e3, 3),
+                     "main_thread_ms": round(main / n * 1e3, 3),
+                     "autograd_thread_ms": round(bwd / n * 1e3, 3),
+                     "other_threads_ms": round(other / n * 1e3, 3),
+                     "busiest_other_threads_ms": [v for v, _ in busy]})
+        print(json.dumps(rows[-1]), flush=True)
+    med = lambda k: sorted(r[k] for r in rows)[len(rows) // 2]  # noqa: E731
+    summ = {"config": args.config, "simulated_ws": ws, "iters_per_block": args.iters,
+            "autograd_thread_is_main": bool(bwd_tid and bwd_tid <= {main_tid}),
+            "median": {k: med(k) for k in ("wall_ms", "cpu_ms", "main_thread_ms",
+                                           "autograd_thread_ms", "other_threads_ms")},
+            "gathers_per_iteration": 2 * len(model.layers), "reduce_buckets": opt._reducer.K,
+            "blocks": rows}
+    print(json.dumps({k: v for k, v in summ.items() if k != "blocks"}), flush=True)
+    if args.out:
+        Path(args.out).write_text(json.dumps(summ, indent=1) + "\n")
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
