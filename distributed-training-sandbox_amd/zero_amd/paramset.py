@@ -6,7 +6,8 @@ reference's ZeRO-3 machinery (zero3.py:56-77: gather in the forward / backward p
 in the post-hooks, reduce the gradients) each decoder layer's tensors become one ``nn.Module``
 whose forward is a custom autograd function: forward passes a tiny activation through, backward
 hands every parameter its gradient from a *gradient source* (by default fixed synthetic tensors
-resident in HBM, returned as fresh views so autograd's AccumulateGrad adopts them without a copy).
+resident in HBM, returned as fresh aliases — ``detach()``: a new tensor on the same storage — so
+autograd's AccumulateGrad adopts them without a copy).
 The gathered weights are not multiplied with anything: an iteration is exactly ZeRO-3's
 communication and update — all-gather per layer in forward, again in backward, reduce-scatter of
 the gradients, fused Adam on the chunks.
@@ -65,10 +66,11 @@ class ParamSetModel(nn.Module):
         self.groups = [list(g) for g in groups]
 
     def set_grad_source(self, grads):
-        """Every backward hands parameter i the tensor grads[i] (as a fresh view, no copy)."""
+        """Every backward hands parameter i the tensor grads[i] (as a fresh alias, no copy: the
+        alias is referenced only by autograd, so AccumulateGrad adopts it instead of cloning)."""
         for layer, g in zip(self.layers, self.groups):
             srcs = [grads[i] for i in g]
-            layer.grad_source = lambda srcs=srcs: [t.view(t.shape) for t in srcs]
+            layer.grad_source = lambda srcs=srcs: [t.detach() for t in srcs]
 
     def forward(self, x):
         for layer in self.layers:

@@ -133,6 +133,9 @@ class _GatherRuntime:
         self.ws, self.rank, self.comm, self.device = ws, rank, comm, device
         self.stream = comm_stream(device)
         self._side_h = self.stream.cuda_stream
+        # the current stream as a raw handle (torch.cuda.current_stream builds a Stream object per
+        # call; the hot path only needs the handle for the library's ordered calls)
+        self._dev_idx = device.index if device.index is not None else torch.cuda.current_device()
         self.pending = {}      # key -> (list[(manager, full_tensor)], event, holding tensor)
         self.sequence = []     # learned order of group keys
         self.pos = 0
@@ -158,8 +161,13 @@ class _GatherRuntime:
             ev = self._events[key] = (a, b, a.cuda_event, b.cuda_event)
         return ev
 
-    def launch(self, key, managers, cur=None):
-        """Enqueue the all-gather of ``managers`` on the side stream; returns immediately."""
+    def _cur_h(self) -> int:
+        return torch._C._cuda_getCurrentRawStream(self._dev_idx)
+
+    def launch(self, key, managers, cur_h=None):
+        """Enqueue the all-gather of ``managers`` on the side stream; returns immediately.
+        ``cur_h``: the raw handle of the stream the gathered tensors will be read on (default:
+        the current stream)."""
         if key in self.pending or not managers:
             return
         if self.ws == 1 and not any(m.fp8 for m in managers):
@@ -168,8 +176,8 @@ class _GatherRuntime:
             self.n_gathers += 1
             return
         ev_ready, ev, ready_h, ev_h = self._key_events(key)
-        if cur is None:
-            cur = torch.cuda.current_stream(self.device)
+        if cur_h is None:
+            cur_h = self._cur_h()
         timed = self.gather_events is not None and self.ws > 1
         plan = self._tables[key] if key in self._tables else self._table(key, managers)
         side = self.stream
@@ -181,11 +189,12 @@ class _GatherRuntime:
             hold = torch.empty(total, dtype=managers[0].shard.dtype, device=self.device)
             hold.record_stream(side)
             np.add(offs, np.uint64(hold.data_ptr()), out=recv)
-            ordered(cur.cuda_stream, ready_h, self._side_h, ev_h)
+            ordered(cur_h, ready_h, self._side_h, ev_h)
             self.pending[key] = ([(m, hold.as_strided(shape, stride, off)) for m, (shape, stride, off)
-                                  in zip(managers, views)], ev, hold, cur)
+                                  in zip(managers, views)], ev, hold, cur_h)
             self.n_gathers += 1
             return
+        cur = torch.cuda.current_stream(self.device)
         ev_ready.record(cur)  # shards may just have been updated
         side.wait_event(ev_ready)
         if timed:
@@ -232,7 +241,7 @@ class _GatherRuntime:
         if timed:  # ring all-gather bus bytes: (ws-1)/ws of the gathered tensor, per rank
             bus = sum(m.gather_bytes() for m in managers) * (self.ws - 1)
             self.gather_events.append((e0, _timed_after(side), bus))
-        self.pending[key] = (out, ev, hold, cur)
+        self.pending[key] = (out, ev, hold, cur_h)
         self.n_gathers += 1
 
     def _table(self, key, managers):
@@ -360,13 +369,13 @@ class _GatherRuntime:
                       plan["row_len"].ctypes.data, plan["dst"].ctypes.data, plan["zdt"], h)
         return hold
 
-    def _prefetch(self, i, cur=None):
+    def _prefetch(self, i, cur_h=None):
         if 0 <= i < len(self.sequence):
             key = self.sequence[i]
-            self.launch(key, self.key_managers.get(key), cur)
+            self.launch(key, self.key_managers.get(key), cur_h)
 
     def materialize(self, key, managers):
-        cur = torch.cuda.current_stream(self.device)
+        cur_h = self._cur_h()
         if self.recording:
             self.sequence.append(key)
         else:
@@ -374,27 +383,28 @@ class _GatherRuntime:
                 self.pos += 1
             elif key in self.sequence[self.pos:]:
                 self.pos = self.sequence.index(key, self.pos) + 1
-            self._prefetch(self.pos, cur)  # the next group, while this one computes
+            self._prefetch(self.pos, cur_h)  # the next group, while this one computes
         if key in self.pending:
             self.n_prefetch_hits += 1
-        self.launch(key, managers, cur)
-        out, ev, hold, alloc_stream = self.pending.pop(key)
+        self.launch(key, managers, cur_h)
+        out, ev, hold, alloc_h = self.pending.pop(key)
         if ev is None:  # ws == 1
             for m, full in out:
                 m._install_full(full)
             return
-        rc = _lib.lib.zs_stream_wait_event(cur.cuda_stream, self._events[key][3])
+        rc = _lib.lib.zs_stream_wait_event(cur_h, self._events[key][3])
         if rc:
             _lib.check(rc, "zs_stream_wait_event")
-        if hold is not None and alloc_stream is not None and alloc_stream != cur:
+        if hold is not None and alloc_h is not None and alloc_h != cur_h:
             # prefetched under another current stream (a user stream in forward, autograd's in
             # backward): the allocator must not reuse the block while THIS stream reads it
-            hold.record_stream(cur)
+            hold.record_stream(torch.cuda.current_stream(self.device))
         if hold is not None:  # one allocation (on this stream) behind all of the module's full
             for m, full in out:  # tensors, whose views already have the full shapes
                 m.full_data = full
                 m.param.data = full
             return
+        cur = torch.cuda.current_stream(self.device)
         for m, full in out:
             full.record_stream(cur)
             m._install_full(full)
@@ -963,7 +973,8 @@ class _GradReducer:
                     self.local_grads[i] = g
             return
         dev = ar.device
-        cur = torch.cuda.current_stream(dev)
+        cur_h = opt.runtime._cur_h()
+        cur = None  # the Stream object, built only on the paths that need it
         wdt = opt._G.dtype  # on the wire: the param dtype, or bf16 for grad_comm="bf16"
         sends = []  # (param index, send buffer): alive until the RCCL group has been enqueued
         S_l, N_l = self._S_l, self._N_l
@@ -978,18 +989,23 @@ class _GradReducer:
                     raise ValueError("zero_amd ZeRO-3 update mode needs the full-size gradient "
                                      "(param %d: got %s)" % (i, tuple(g.shape)))
                 self.had_grad[i] = True
-                flat = g.reshape(-1) if g.is_contiguous() else g.contiguous().reshape(-1)
-                if wdt != ar.dtype:  # bf16 exchange: gfx950 RNE conversion into the send buffer
-                    from .kernels import convert
+                if wdt == ar.dtype and N == ws * S and g.is_contiguous():
+                    send = g  # zero-copy: rows of torch.chunk are contiguous
+                else:
+                    flat = g.reshape(-1) if g.is_contiguous() else g.contiguous().reshape(-1)
+                    if wdt != ar.dtype:  # bf16 exchange: gfx950 RNE conversion into the send buffer
+                        from .kernels import convert
 
-                    send = torch.empty(ws * S, dtype=wdt, device=dev) if N == ws * S else \
-                        torch.zeros(ws * S, dtype=wdt, device=dev)
-                    convert(flat, send[:N], cur)
-                elif N == ws * S:
-                    send = flat  # zero-copy: rows of torch.chunk are contiguous
-                else:  # uneven chunks: every rank sends ws*S elements
-                    send = torch.zeros(ws * S, dtype=wdt, device=dev)
-                    send[:N].copy_(flat)
+                        if cur is None:
+                            cur = torch.cuda.current_stream(dev)
+                        send = torch.empty(ws * S, dtype=wdt, device=dev) if N == ws * S else \
+                            torch.zeros(ws * S, dtype=wdt, device=dev)
+                        convert(flat, send[:N], cur)
+                    elif N == ws * S:
+                        send = flat
+                    else:  # uneven chunks: every rank sends ws*S elements
+                        send = torch.zeros(ws * S, dtype=wdt, device=dev)
+                        send[:N].copy_(flat)
             sends.append((i, send))
         cs = opt.runtime.stream
         tab = self._rs_table(k) if hasattr(opt.comm, "reduce_scatter_group") else None
@@ -999,11 +1015,13 @@ class _GradReducer:
             recv, count, dt, sp, raw, ordered = tab
             for j, (_, t) in enumerate(sends):
                 sp[j] = t.data_ptr()
-            ordered(cur.cuda_stream, self._ready_h[k], self._cs_h, self._done_h[k])
+            ordered(cur_h, self._ready_h[k], self._cs_h, self._done_h[k])
             for i, send in sends:
                 send.record_stream(cs)
                 opt.params[i].grad = None
             return
+        if cur is None:
+            cur = torch.cuda.current_stream(dev)
         ready = self.ev_ready[k]
         ready.record(cur)
         cs.wait_event(ready)

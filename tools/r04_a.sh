@@ -18,4 +18,6 @@ grep -h '"frac"' "$O/kernels_table.log" | python3 -c "import sys,json; [print(f\
 echo "--- dq8"; grep -h 'dequant' "$O/kernels_table_dq8.log" | python3 -c "import sys,json; [print(f\"{json.loads(l)['kernel'][:80]:80s} {json.loads(l)['frac']:.3f}\") for l in sys.stdin]"
 timeout -k 10 300 python3 tools/z3_host_threads.py --out "$O/z3_threads.json" > "$O/z3_threads.log" 2>&1 || { tail -20 "$O/z3_threads.log"; exit 1; }
 tail -1 "$O/z3_threads.log"
+timeout -k 10 400 python3 tools/z3_host_ab.py --baseline r03 --blocks 4 --out "$O/z3_ab.json" > "$O/z3_ab.log" 2>&1 || { tail -20 "$O/z3_ab.log"; exit 1; }
+tail -1 "$O/z3_ab.log"
 echo "[r04a] done"
