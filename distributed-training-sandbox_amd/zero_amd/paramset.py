@@ -35,7 +35,7 @@ class _PassThrough(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, layer, *params):
         ctx.layer = layer
-        return x.clone()
+        return x.view_as(x)  # an alias: no kernel launch, just an autograd node per layer
 
     @staticmethod
     def backward(ctx, gx):

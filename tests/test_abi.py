@@ -252,3 +252,17 @@ def test_plain_c_client(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
     assert out.returncode == 0, out.stderr
     assert out.stdout.startswith("c-abi ok")
+
+
+def test_device_alloc_validates_without_gpu():
+    """ABI v10's zs_device_alloc / zs_device_free (the placement probe's private allocations):
+    bad arguments are rejected before the runtime is touched; freeing NULL is a no-op."""
+    from zero_amd import _lib
+
+    lib = _lib.lib
+    out = ctypes.c_void_p(123)
+    assert lib.zs_device_alloc(0, ctypes.byref(out)) == _lib.ZS_ERR_INVALID
+    assert b"bytes must be > 0" in lib.zs_last_error()
+    assert lib.zs_device_alloc(-5, ctypes.byref(out)) == _lib.ZS_ERR_INVALID
+    assert lib.zs_device_alloc(64, None) == _lib.ZS_ERR_INVALID
+    assert lib.zs_device_free(None) == _lib.ZS_OK
