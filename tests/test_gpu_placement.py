@@ -53,7 +53,9 @@ def test_probe_keeps_callers_cached_block(gpu, pg1):
     # Adam's first step on a constant grad: every parameter moved by -lr (bias-corrected)
     assert torch.allclose(params[0][:2, :4], torch.full((2, 4), -1e-3, device=dev), rtol=1e-4)
     free0 = torch.cuda.mem_get_info(dev)[0]
-    del opt, st
+    # the parameters are views of the flat arena and their grads views of the grad arena (and
+    # their hooks reach the engine): everything goes when the model and the optimizer go
+    del opt, st, params, p
     import gc
 
     gc.collect()

@@ -6,8 +6,11 @@ R="${GRAFT_REPO_ROOT:-$(pwd)}"; O="$R/gpurun_out/r04a"; mkdir -p "$O"
 export TMPDIR=/tmp
 cd "$R" || exit 2
 timeout -k 10 500 python -u -m pytest tests/test_gpu_placement.py tests/test_gpu_fp8.py tests/test_gpu_kernels.py \
-  "tests/test_gpu_rccl.py::test_bench_share_gpu_exchange_check" -x -v --timeout 240 --timeout-method thread > "$O/pytest.log" 2>&1 || { tail -60 "$O/pytest.log"; exit 1; }
-tail -3 "$O/pytest.log"
+  "tests/test_gpu_rccl.py::test_bench_share_gpu_exchange_check" -v --timeout 240 --timeout-method thread > "$O/pytest.log" 2>&1
+rc=$?
+tail -3 "$O/pytest.log"; grep -E "^(FAILED|ERROR)" "$O/pytest.log" | head -20
+# a test failure is read afterwards; a crash / kill / time limit ends the call here
+case $rc in 124|134|137|139) echo "pytest rc=$rc: stopping"; exit 1;; esac
 timeout -k 10 240 python3 tools/kernel_table.py --out "$O/kernels_table.json" > "$O/kernels_table.log" 2>&1 || { tail -20 "$O/kernels_table.log"; exit 1; }
 ZERO_AMD_DQ_WG_PER_CU=8 timeout -k 10 240 python3 tools/kernel_table.py --out "$O/kernels_table_dq8.json" > "$O/kernels_table_dq8.log" 2>&1 || exit 1
 ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o run -- python3 "$R/tools/kernel_table.py" --iters 10 --out "$O/kernels_table_kt.json" ) > "$O/kt.log" 2>&1 || exit 1

@@ -32,6 +32,10 @@ def main():
     ap.add_argument("--blocks", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--no-events", action="store_true",
+                    help="DIAGNOSTIC: the ordered library calls and the consumer's stream wait "
+                         "become no-ops (no HIP event record / wait at all): how much of the "
+                         "runtime threads' CPU the stream ordering costs")
     args = ap.parse_args()
 
     import psutil
@@ -59,8 +63,14 @@ def main():
     real_get = zero3.get
     zero3.get = lambda what, dm=None: {"ws": ws, "rank": 0}.get(what) if what in ("ws", "rank") \
         else real_get(what, dm)
+    comm = bench._NoComm(ws)
+    if args.no_events:
+        from zero_amd import _lib
+
+        comm._ordered = staticmethod(lambda name, dtype: (lambda after, ready, stream, done: None))
+        _lib.lib.zs_stream_wait_event = lambda *a: 0
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
-                                 sync=False, comm=bench._NoComm(ws))
+                                 sync=False, comm=comm)
     zero3.register_zero3_hooks(model, opt.param_managers)
     x = torch.zeros(1, device=dev, requires_grad=True)
     bwd_tid = set()
@@ -95,14 +105,21 @@ def main():
         other = sum(v for t, v in d.items() if t != main_tid and t not in bwd_tid)
         busy = sorted(((round(v / n * 1e3, 3), t) for t, v in d.items()
                        if t != main_tid and t not in bwd_tid and v > 0), reverse=True)[:4]
+        names = {}
+        for t in d:
+            try:
+                names[t] = Path(f"/proc/self/task/{t}/comm").read_text().strip()
+            except OSError:
+                names[t] = "?"
         rows.append({"block": b, "wall_ms": round(w / n * 1e3, 3), "cpu_ms": round(c / n * 1e3, 3),
                      "main_thread_ms": round(main / n * 1e3, 3),
                      "autograd_thread_ms": round(bwd / n * 1e3, 3),
                      "other_threads_ms": round(other / n * 1e3, 3),
-                     "busiest_other_threads_ms": [v for v, _ in busy]})
+                     "busiest_other_threads_ms": {f"{names.get(t, '?')}[{t}]": v for v, t in busy}})
         print(json.dumps(rows[-1]), flush=True)
     med = lambda k: sorted(r[k] for r in rows)[len(rows) // 2]  # noqa: E731
     summ = {"config": args.config, "simulated_ws": ws, "iters_per_block": args.iters,
+            "no_events": args.no_events,
             "autograd_thread_is_main": bool(bwd_tid and bwd_tid <= {main_tid}),
             "median": {k: med(k) for k in ("wall_ms", "cpu_ms", "main_thread_ms",
                                            "autograd_thread_ms", "other_threads_ms")},
