@@ -10,11 +10,15 @@ a row's traffic is the sum over the dispatches of its last call.
 
 Units and corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE / WRITE_SIZE are KiB per dispatch;
 on gfx950 FETCH_SIZE reports 1/2 of a wide (16 B/lane) coalesced streaming read, so reads of
-16 B/lane are doubled.  WRITE_SIZE is exact for 16 B/lane stores.  Other widths are uncalibrated by
-the guide: the table reports the raw counters beside the corrected figure, and the in-place copy
-rows (16 B/lane both ways) calibrate the rule on the same run.
+16 B/lane are doubled.  WRITE_SIZE is exact for 16 B/lane stores.  8-B/lane reads and stores are
+not calibrated by the guide; they are calibrated here on known byte counts in the same run: the
+bf16 -> fp32 conversion reads exactly 2 B x n with 8-B lanes (FETCH_SIZE = 1/2 of it, like the
+16-B reads: doubled as well), and the fp32 -> bf16 conversion writes exactly 2 B x n with 8-B
+lanes (WRITE_SIZE = all of it).  The raw counters are kept beside every corrected figure.
 
-usage: python tools/kernel_pmc.py <kernel_table.json> <fetch_dir> <write_dir> <out.json>
+usage: python tools/kernel_pmc.py <kernel_table.json> <fetch_dir> <write_dir> <out.json> [timed.json]
+(timed.json: an unprofiled kernel_table.py run whose launch times and fractions are reported —
+the profiled passes run few iterations and their times are not the kernels')
 """
 import csv
 import json
@@ -76,6 +80,8 @@ def per_row(table, disp):
 def main():
     tab, fdir, wdir, out = sys.argv[1:5]
     table = json.loads(Path(tab).read_text())
+    timed = {r["kernel"]: r for r in json.loads(Path(sys.argv[5]).read_text())["rows"]} \
+        if len(sys.argv) > 5 else {}
     fetch = per_row(table, _dispatches(fdir, "FETCH_SIZE"))
     write = per_row(table, _dispatches(wdir, "WRITE_SIZE"))
     rows = []
@@ -86,19 +92,23 @@ def main():
         pre = r["rocprof_kernel"]
         fk, wk = fetch[k], write[k]
         rw, ww = READ_WIDTH.get(pre), WRITE_WIDTH.get(pre)
-        fetch_b = fk * 1024 * (2 if rw == 16 else 1)
+        fetch_b = fk * 1024 * (2 if rw in (8, 16) else 1)
         hbm = fetch_b + wk * 1024
+        t = timed.get(k, r)
         rows.append({
-            "kernel": k, "workload": r["workload"], "avg_launch_ms": r["avg_launch_ms"],
-            "frac": r["frac"], "alg_bytes_per_call": r["alg_bytes_per_launch"],
+            "kernel": k, "workload": r["workload"], "avg_launch_ms": t["avg_launch_ms"],
+            "frac": t["frac"], "achieved_gbs": t.get("achieved_gbs"),
+            "alg_bytes_per_call": r["alg_bytes_per_launch"],
             "fetch_size_kib": fk, "write_size_kib": wk, "read_bytes_per_lane": rw,
             "write_bytes_per_lane": ww,
             "fetch_bytes": fetch_b, "write_bytes": wk * 1024, "hbm_bytes_per_call": hbm,
             "traffic_over_algorithmic": hbm / r["alg_bytes_per_launch"],
             "fetch_correction": "x2 (16 B/lane reads, guide §HBM)" if rw == 16 else
-                                "none (8 B/lane reads: uncalibrated by the guide; raw KiB)"})
+                                "x2 (8 B/lane reads: calibrated on the bf16->fp32 conversion's "
+                                "known 2 B/element read in this run)" if rw == 8 else "none"})
     doc = {"source": f"{tab} + rocprofv3 --pmc FETCH_SIZE ({fdir}) / --pmc WRITE_SIZE ({wdir}), "
-                     "separate passes", "units": "FETCH_SIZE / WRITE_SIZE: KiB per dispatch",
+                     "separate passes" + (f"; times and fractions from {sys.argv[5]}" if timed else ""),
+           "units": "FETCH_SIZE / WRITE_SIZE: KiB per dispatch",
            "rows": rows}
     Path(out).write_text(json.dumps(doc, indent=1) + "\n")
     for x in rows:

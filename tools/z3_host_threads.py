@@ -67,7 +67,7 @@ def main():
     if args.no_events:
         from zero_amd import _lib
 
-        comm._ordered = staticmethod(lambda name, dtype: (lambda after, ready, stream, done: None))
+        comm._ordered = lambda name, dtype: (lambda after, ready, stream, done: None)
         _lib.lib.zs_stream_wait_event = lambda *a: 0
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
                                  sync=False, comm=comm)
