@@ -657,7 +657,7 @@ __global__ __launch_bounds__(kThreads) void fp8_quantize_rowset_kernel(const QSe
 // issued before the stores of the current one, so on gfx950, whose vmcnt counts loads and stores
 // together, waiting for a batch's data never waits for the previous batch's stores: each wave keeps
 // one batch of loads and one of stores in flight throughout.
-constexpr int kDqU = 8;
+constexpr int kDqU = 8;  // default accesses in flight per lane (zs_tune "dq_unroll": 4 / 8 / 16)
 
 struct DqSet {
   const unsigned char* q;
@@ -677,12 +677,12 @@ struct DqRow {
   int64_t len;
 };
 
-template <typename T>
+template <typename T, int U>
 __device__ __forceinline__ void fp8_dq_load(const DqRow<T>& r, int64_t b0, int lane, uint2* raw) {
   constexpr int E = sizeof(T) == 2 ? 8 : 4;
   const gptr<const unsigned char> q = glob(r.q);
 #pragma unroll
-  for (int u = 0; u < kDqU; ++u) {
+  for (int u = 0; u < U; ++u) {
     const int64_t i = b0 + (int64_t(u) * 64 + lane) * E;
     raw[u] = make_uint2(0, 0);
     if (i < r.len) {
@@ -692,7 +692,7 @@ __device__ __forceinline__ void fp8_dq_load(const DqRow<T>& r, int64_t b0, int l
   }
 }
 
-template <typename T>
+template <typename T, int U, bool NT>
 __device__ __forceinline__ void fp8_dq_store(const DqRow<T>& r, int64_t b0, int lane,
                                              const uint2* raw) {
 #pragma clang fp contract(off)
@@ -700,7 +700,7 @@ __device__ __forceinline__ void fp8_dq_store(const DqRow<T>& r, int64_t b0, int 
   const gptr<T> y = glob(r.y);
   const float sc = r.sc;
 #pragma unroll
-  for (int u = 0; u < kDqU; ++u) {
+  for (int u = 0; u < U; ++u) {
     const int64_t i = b0 + (int64_t(u) * 64 + lane) * E;
     if (i >= r.len) continue;
     const int lo = int(raw[u].x), hi = int(raw[u].y);
@@ -710,16 +710,19 @@ __device__ __forceinline__ void fp8_dq_store(const DqRow<T>& r, int64_t b0, int 
       const float b0_ = __builtin_amdgcn_cvt_f32_fp8(hi, 0) * sc, b1 = __builtin_amdgcn_cvt_f32_fp8(hi, 1) * sc;
       const float b2 = __builtin_amdgcn_cvt_f32_fp8(hi, 2) * sc, b3 = __builtin_amdgcn_cvt_f32_fp8(hi, 3) * sc;
       auto pk = [](float a, float b) { return uint32_t(f32_to_bf16(a)) | (uint32_t(f32_to_bf16(b)) << 16); };
-      nt_st16(y + i, make_uint4(pk(a0, a1), pk(a2, a3), pk(b0_, b1), pk(b2, b3)));
+      const uint4 v = make_uint4(pk(a0, a1), pk(a2, a3), pk(b0_, b1), pk(b2, b3));
+      if constexpr (NT) nt_st16(y + i, v);
+      else *reinterpret_cast<gptr<uint4>>(y + i) = v;
     } else {
-      st4(reinterpret_cast<float*>(r.y + i), 0, make_float4(a0, a1, a2, a3));
+      if constexpr (NT) st4(reinterpret_cast<float*>(r.y + i), 0, make_float4(a0, a1, a2, a3));
+      else *reinterpret_cast<gptr<float4>>(y + i) = make_float4(a0, a1, a2, a3);
     }
   }
 }
 
-template <typename T>
+template <typename T, int U, bool NT>
 __global__ __launch_bounds__(kThreads) void fp8_dequantize_gathered_kernel(const DqSet set) {
-  constexpr int64_t B = int64_t(64) * (sizeof(T) == 2 ? 8 : 4) * kDqU;  // elements per batch
+  constexpr int64_t B = int64_t(64) * (sizeof(T) == 2 ? 8 : 4) * U;  // elements per batch
   const int lane = threadIdx.x & 63;
   const int64_t total = set.prefix[set.n];
   const int64_t nwaves = int64_t(gridDim.x) * (kThreads / 64);
@@ -740,8 +743,8 @@ __global__ __launch_bounds__(kThreads) void fp8_dequantize_gathered_kernel(const
   DqRow<T> cur;
   row_at(g, cur);
   int64_t b0 = 0;
-  uint2 raw[kDqU];
-  fp8_dq_load<T>(cur, b0, lane, raw);
+  uint2 raw[U];
+  fp8_dq_load<T, U>(cur, b0, lane, raw);
   while (true) {
     DqRow<T> nxt = cur;
     int64_t nb0 = b0 + B;
@@ -752,14 +755,14 @@ __global__ __launch_bounds__(kThreads) void fp8_dequantize_gathered_kernel(const
       if (more) row_at(g, nxt);
       nb0 = 0;
     }
-    uint2 nraw[kDqU];
-    if (more) fp8_dq_load<T>(nxt, nb0, lane, nraw);  // next batch's loads before this one's stores
-    fp8_dq_store<T>(cur, b0, lane, raw);
+    uint2 nraw[U];
+    if (more) fp8_dq_load<T, U>(nxt, nb0, lane, nraw);  // next batch's loads before this one's stores
+    fp8_dq_store<T, U, NT>(cur, b0, lane, raw);
     if (!more) break;
     cur = nxt;
     b0 = nb0;
 #pragma unroll
-    for (int u = 0; u < kDqU; ++u) raw[u] = nraw[u];
+    for (int u = 0; u < U; ++u) raw[u] = nraw[u];
   }
 }
 
@@ -780,18 +783,42 @@ __global__ __launch_bounds__(kThreads) void fp8_dequantize_rows_kernel(
 
 inline bool aligned(uint64_t p, uint64_t a) { return p % a == 0; }
 
-// Dequantise grid: one wave per row (4 rows per workgroup) up to the usual cap; with
-// ZERO_AMD_DQ_WG_PER_CU=k (diagnostic A/B) at most k workgroups per CU, each wave walking several
-// rows with the next row's loads issued before the current row's stores.
+// Diagnostic tuning knobs of the dequantise kernel (zs_tune; defaults are the measured best):
+// accesses in flight per lane, non-temporal stores, and a cap of workgroups per CU (0 = one wave
+// per row up to the usual grid cap; k > 0 = at most k workgroups per CU, each wave walking several
+// rows with the next row's loads issued before the current row's stores).
+struct DqTune {
+  int unroll = kDqU;
+  int nt_store = 1;
+  int wg_per_cu = 0;
+};
+DqTune& dq_tune() {
+  static DqTune t;
+  return t;
+}
+
 int dq_grid(int64_t rows) {
-  static int per_cu = -1;
-  if (per_cu < 0) {
-    const char* e = std::getenv("ZERO_AMD_DQ_WG_PER_CU");
-    per_cu = e ? std::max(0, std::atoi(e)) : 0;
-  }
   int64_t cap = grid_cap();
+  const int per_cu = dq_tune().wg_per_cu;
   if (per_cu > 0) cap = std::max<int64_t>(1, cap / 128 * per_cu);
   return int(std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, cap)));
+}
+
+template <typename T>
+void launch_dequantize_t(const DqSet& set, int grid, hipStream_t st) {
+  const DqTune& t = dq_tune();
+#define ZS_DQ(U, NT) hipLaunchKernelGGL((fp8_dequantize_gathered_kernel<T, U, NT>), dim3(grid), dim3(kThreads), 0, st, set)
+  if (t.nt_store) {
+    switch (t.unroll) { case 4: ZS_DQ(4, true); break; case 16: ZS_DQ(16, true); break; default: ZS_DQ(8, true); }
+  } else {
+    switch (t.unroll) { case 4: ZS_DQ(4, false); break; case 16: ZS_DQ(16, false); break; default: ZS_DQ(8, false); }
+  }
+#undef ZS_DQ
+}
+
+void launch_dequantize(const DqSet& set, int dst_dtype, int grid, hipStream_t st) {
+  if (dst_dtype == ZS_F32) launch_dequantize_t<float>(set, grid, st);
+  else launch_dequantize_t<unsigned short>(set, grid, st);
 }
 
 }  // namespace
@@ -1098,10 +1125,7 @@ int zs_fp8_dequantize_rows(const void* src, const float* scales, void* dst, int 
     set.prefix[0] = 0;
     for (int k = 1; k <= kSetMax; ++k) set.prefix[k] = rows;
     const int grid = dq_grid(rows);
-    if (dst_dtype == ZS_F32)
-      hipLaunchKernelGGL((fp8_dequantize_gathered_kernel<float>), dim3(grid), dim3(kThreads), 0, st, set);
-    else
-      hipLaunchKernelGGL((fp8_dequantize_gathered_kernel<unsigned short>), dim3(grid), dim3(kThreads), 0, st, set);
+    launch_dequantize(set, dst_dtype, grid, st);
   } else {
     const int grid = int(std::min<int64_t>(std::max<int64_t>(1, (n + kThreads - 1) / kThreads), grid_cap()));
     if (dst_dtype == ZS_F32)
@@ -1217,10 +1241,7 @@ int zs_fp8_dequantize_gathered(int64_t n, const void* q, const float* scales, in
     const int64_t total = set.prefix[set.n];
     if (total == 0) continue;
     const int grid = dq_grid(total);
-    if (dst_dtype == ZS_F32)
-      hipLaunchKernelGGL((fp8_dequantize_gathered_kernel<float>), dim3(grid), dim3(kThreads), 0, st, set);
-    else
-      hipLaunchKernelGGL((fp8_dequantize_gathered_kernel<unsigned short>), dim3(grid), dim3(kThreads), 0, st, set);
+    launch_dequantize(set, dst_dtype, grid, st);
     ZS_HIP(hipGetLastError());
   }
   return ZS_OK;
@@ -1464,6 +1485,28 @@ int zs_adamset_stats(const zs_adamset* as, int64_t* elems, int64_t* bytes) {
   ZS_REQUIRE(as && elems && bytes, "zs_adamset_stats: NULL argument");
   *elems = as->elems;
   *bytes = as->bytes;
+  return ZS_OK;
+}
+
+int zs_tune(const char* key, int64_t value, int64_t* previous) {
+  ZS_REQUIRE(key != nullptr, "zs_tune: key is NULL");
+  int* slot = nullptr;
+  bool ok = false;
+  if (std::strcmp(key, "dq_unroll") == 0) {
+    slot = &dq_tune().unroll;
+    ok = value == 4 || value == 8 || value == 16;
+  } else if (std::strcmp(key, "dq_nt_store") == 0) {
+    slot = &dq_tune().nt_store;
+    ok = value == 0 || value == 1;
+  } else if (std::strcmp(key, "dq_wg_per_cu") == 0) {
+    slot = &dq_tune().wg_per_cu;
+    ok = value >= 0 && value <= 128;
+  } else {
+    return zs::fail(ZS_ERR_INVALID, "zs_tune: unknown key '%s'", key);
+  }
+  ZS_REQUIRE(ok, "zs_tune: value %lld out of range for '%s'", (long long)value, key);
+  if (previous) *previous = *slot;
+  *slot = int(value);
   return ZS_OK;
 }
 

@@ -38,7 +38,7 @@ EXPORTED = (
     "zs_comm_unique_id", "zs_comm_init", "zs_comm_destroy", "zs_reduce_scatter", "zs_all_gather",
     "zs_all_reduce", "zs_reduce", "zs_broadcast", "zs_reduce_group", "zs_broadcast_group", "zs_all_gather_group", "zs_reduce_scatter_group",
     "zs_all_gather_group_ordered", "zs_reduce_scatter_group_ordered", "zs_stream_wait_event", "zs_group_start", "zs_group_end", "zs_rccl_version",
-    "zs_device_alloc", "zs_device_free",
+    "zs_device_alloc", "zs_device_free", "zs_tune",
 )
 
 
@@ -142,6 +142,7 @@ _SIGS = {
     "zs_rccl_version": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "zs_device_alloc": ([_I64, ctypes.POINTER(_P)], ctypes.c_int),
     "zs_device_free": ([_P], ctypes.c_int),
+    "zs_tune": ([ctypes.c_char_p, _I64, _PI64], ctypes.c_int),
 }
 
 

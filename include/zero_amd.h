@@ -296,6 +296,13 @@ int zs_device_alloc(int64_t bytes, void** out);
  * work still uses. */
 int zs_device_free(void* p);
 
+/* Diagnostic A/B knobs (process-wide; the defaults are the measured best, so a product caller
+ * never needs this): "dq_unroll" (4 / 8 / 16 accesses in flight per lane of the fp8 dequantise),
+ * "dq_nt_store" (0 / 1: non-temporal stores), "dq_wg_per_cu" (0 = one wave per row; k = at most k
+ * workgroups per CU walking several rows each).  *previous (may be NULL) gets the old value;
+ * ZS_ERR_INVALID for an unknown key or value. */
+int zs_tune(const char* key, int64_t value, int64_t* previous);
+
 /* ------------------------------------------------------------------------------------------ */
 /* RCCL over xGMI.  Replaces the per-tensor dist.all_reduce (zero1.py:83, zero3.py:146),        */
 /* dist.reduce_scatter_tensor (zero2.py:107), dist.broadcast (zero1.py:102, zero2.py:133) and   */

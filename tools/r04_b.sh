@@ -15,4 +15,6 @@ timeout -k 10 300 python3 tools/z3_host_threads.py --blocks 3 --no-events --out 
 grep '^{' "$O/z3_threads_noev.log" | tail -2
 timeout -k 10 400 python3 bench.py --steps 300 > "$O/bench_n1.json" 2> "$O/bench_n1.err" || { tail -20 "$O/bench_n1.err"; exit 1; }
 python3 -c "import json; d=json.loads(open('$O/bench_n1.json').read().strip().splitlines()[-1]); print(d['ms_per_step'], d['roofline']['frac'], d['placement']['state'], d['cpu_baseline'])"
+timeout -k 10 300 python3 tools/dq_ab.py --out "$O/dq_ab.json" > "$O/dq_ab.log" 2>&1 || { tail -20 "$O/dq_ab.log"; exit 1; }
+grep "^{" "$O/dq_ab.log"
 echo "[r04b] done"
