@@ -772,7 +772,7 @@ def zero3_gather_check(opt, model, shapes, full_copies, dev, world, rank, red_de
     idx = model.groups[1]
     ms = [opt.param_managers[getattr(layer, f"p{k}")] for k in range(layer.n)]
     rt.launch(("exchange-check",), ms)
-    out, ev, _hold, _ = rt.pending.pop(("exchange-check",))
+    out, ev, _hold, _, _ = rt.pending.pop(("exchange-check",))
     torch.cuda.current_stream(dev).wait_event(ev)
     torch.cuda.synchronize()
     bits = lambda t: t.reshape(-1).view(torch.int16 if t.element_size() == 2 else torch.int32)  # noqa: E731

@@ -125,18 +125,31 @@ class _GatherRuntime:
     (and, in update mode, the gradient reduce-scatters, on the same stream).
 
     The first iteration records the order in which module groups are materialised (forward, then
-    backward); afterwards each materialise also launches the gather of the next group in that
-    order, so the all-gather overlaps the current module's compute.  ``end_iteration`` (called at
-    the end of step()) prefetches the first group of the next iteration."""
+    backward); afterwards the learned sequence is cut into *waves* of ``wave`` consecutive groups,
+    and materialising the first group of wave w launches wave w + 1, so the all-gathers overlap the
+    current wave's compute.  A wave is ordered as a unit: ONE ready event on the compute stream
+    before its first gather, ONE done event after its last, and its consumers wait once per wave —
+    a cross-stream wait on a pending HIP event costs ~10 µs of a HIP runtime thread plus ~5 µs of
+    the caller (profiles/r04_hip_event_cost.json), and at one wait pair per module those were 6 of
+    the 12 ms of host CPU of a simulated ws = 8 C5 iteration.  ``wave = 1`` is the per-module
+    ordering.  ``end_iteration`` (called at the end of step()) prefetches the first wave of the next
+    iteration."""
 
-    def __init__(self, ws, rank, comm, device):
+    def __init__(self, ws, rank, comm, device, wave: int = 2):
         self.ws, self.rank, self.comm, self.device = ws, rank, comm, device
+        if int(wave) < 1:
+            raise ValueError(f"gather wave must be >= 1 (got {wave})")
+        self.wave = int(wave)
+        self._waves_launched = set()  # wave indices launched this iteration
+        self._waited = {}             # done-event handle -> stream handle that waited on it
         self.stream = comm_stream(device)
         self._side_h = self.stream.cuda_stream
         # the current stream as a raw handle (torch.cuda.current_stream builds a Stream object per
         # call; the hot path only needs the handle for the library's ordered calls)
         self._dev_idx = device.index if device.index is not None else torch.cuda.current_device()
-        self.pending = {}      # key -> (list[(manager, full_tensor)], event, holding tensor)
+        # key -> (list[(manager, full_tensor)], done event, holding tensor, stream handle the gather
+        # was ordered after, raw handle of the done event its consumers wait on)
+        self.pending = {}
         self.sequence = []     # learned order of group keys
         self.pos = 0
         self.recording = True
@@ -172,10 +185,12 @@ class _GatherRuntime:
             return
         if self.ws == 1 and not any(m.fp8 for m in managers):
             # the shard is the whole parameter: nothing to gather, no stream to synchronise with
-            self.pending[key] = ([(m, m._gather_prepare(None)[1]) for m in managers], None, None, None)
+            self.pending[key] = ([(m, m._gather_prepare(None)[1]) for m in managers], None, None, None,
+                                 None)
             self.n_gathers += 1
             return
         ev_ready, ev, ready_h, ev_h = self._key_events(key)
+        self._waited.pop(ev_h, None)  # re-recorded below: no consumer has waited on this record
         if cur_h is None:
             cur_h = self._cur_h()
         timed = self.gather_events is not None and self.ws > 1
@@ -191,7 +206,7 @@ class _GatherRuntime:
             np.add(offs, np.uint64(hold.data_ptr()), out=recv)
             ordered(cur_h, ready_h, self._side_h, ev_h)
             self.pending[key] = ([(m, hold.as_strided(shape, stride, off)) for m, (shape, stride, off)
-                                  in zip(managers, views)], ev, hold, cur_h)
+                                  in zip(managers, views)], ev, hold, cur_h, ev_h)
             self.n_gathers += 1
             return
         cur = torch.cuda.current_stream(self.device)
@@ -241,7 +256,7 @@ class _GatherRuntime:
         if timed:  # ring all-gather bus bytes: (ws-1)/ws of the gathered tensor, per rank
             bus = sum(m.gather_bytes() for m in managers) * (self.ws - 1)
             self.gather_events.append((e0, _timed_after(side), bus))
-        self.pending[key] = (out, ev, hold, cur_h)
+        self.pending[key] = (out, ev, hold, cur_h, ev_h)
         self.n_gathers += 1
 
     def _table(self, key, managers):
@@ -369,32 +384,90 @@ class _GatherRuntime:
                       plan["row_len"].ctypes.data, plan["dst"].ctypes.data, plan["zdt"], h)
         return hold
 
+    def _fast_plan(self, key, managers):
+        """The key's ordered-call table when its gather can take the one-call fast path (a chunk-
+        arena module, ws > 1, no per-collective timing), else None."""
+        if self.ws == 1 or not managers or self.gather_events is not None:
+            return None
+        plan = self._tables[key] if key in self._tables else self._table(key, managers)
+        return plan if plan is not None and plan[-1] is not None else None
+
+    def _launch_wave(self, keys, cur_h):
+        """Launch the not-yet-pending groups of ``keys`` as one wave: the first gather records the
+        ready event on the compute stream (``cur_h``) and makes the side stream wait for it, the
+        last records the done event every member's consumer waits on.  Falls back to one launch
+        per group when any of them cannot take the fast path."""
+        todo = [(k, self.key_managers.get(k)) for k in keys if k not in self.pending]
+        todo = [(k, ms) for k, ms in todo if ms]
+        if not todo:
+            return
+        plans = [self._fast_plan(k, ms) for k, ms in todo]
+        if len(todo) == 1 or any(pl is None for pl in plans):
+            for k, ms in todo:
+                self.launch(k, ms, cur_h)
+            return
+        ready_h = self._key_events(todo[0][0])[2]
+        _, done_ev, _, done_h = self._key_events(todo[-1][0])
+        self._waited.pop(done_h, None)
+        last = len(todo) - 1
+        side, side_h = self.stream, self._side_h
+        for j, ((k, ms), plan) in enumerate(zip(todo, plans)):
+            send, count, offs, total, dt, es, views, recv, raw, ordered = plan
+            hold = torch.empty(total, dtype=ms[0].shard.dtype, device=self.device)
+            hold.record_stream(side)
+            np.add(offs, np.uint64(hold.data_ptr()), out=recv)
+            ordered(cur_h, ready_h if j == 0 else 0, side_h, done_h if j == last else 0)
+            self.pending[k] = ([(m, hold.as_strided(shape, stride, off)) for m, (shape, stride, off)
+                                in zip(ms, views)], done_ev, hold, cur_h, done_h)
+            self.n_gathers += 1
+
+    def _ensure_wave(self, w, cur_h=None):
+        """Launch wave ``w`` of the learned sequence unless it was launched this iteration."""
+        G = self.wave
+        if w in self._waves_launched or not 0 <= w * G < len(self.sequence):
+            return
+        self._waves_launched.add(w)
+        if cur_h is None:
+            cur_h = self._cur_h()
+        self._launch_wave(self.sequence[w * G:(w + 1) * G], cur_h)
+
     def _prefetch(self, i, cur_h=None):
+        """Make sure the wave holding sequence position ``i`` has been launched."""
         if 0 <= i < len(self.sequence):
-            key = self.sequence[i]
-            self.launch(key, self.key_managers.get(key), cur_h)
+            self._ensure_wave(i // self.wave, cur_h)
 
     def materialize(self, key, managers):
         cur_h = self._cur_h()
         if self.recording:
             self.sequence.append(key)
         else:
-            if self.pos < len(self.sequence) and self.sequence[self.pos] == key:
-                self.pos += 1
-            elif key in self.sequence[self.pos:]:
-                self.pos = self.sequence.index(key, self.pos) + 1
-            self._prefetch(self.pos, cur_h)  # the next group, while this one computes
+            seq = self.sequence
+            if self.pos < len(seq) and seq[self.pos] == key:
+                p = self.pos
+            elif key in seq[self.pos:]:
+                p = seq.index(key, self.pos)
+            else:
+                p = None
+            if p is not None:
+                self.pos = p + 1
+                w = p // self.wave
+                self._ensure_wave(w, cur_h)      # (normally launched as the previous prefetch)
+                self._ensure_wave(w + 1, cur_h)  # the next wave, while this one computes
+            else:
+                self._prefetch(self.pos, cur_h)
         if key in self.pending:
             self.n_prefetch_hits += 1
         self.launch(key, managers, cur_h)
-        out, ev, hold, alloc_h = self.pending.pop(key)
+        out, ev, hold, alloc_h, wait_h = self.pending.pop(key)
         if ev is None:  # ws == 1
             for m, full in out:
                 m._install_full(full)
             return
-        rc = _lib.lib.zs_stream_wait_event(cur_h, self._events[key][3])
-        if rc:
-            _lib.check(rc, "zs_stream_wait_event")
+        if self._waited.get(wait_h) != cur_h:  # once per wave and consuming stream
+            rc = _lib.lib.zs_stream_wait_event(cur_h, wait_h)
+            if rc:
+                _lib.check(rc, "zs_stream_wait_event")
+            self._waited[wait_h] = cur_h
         if hold is not None and alloc_h is not None and alloc_h != cur_h:
             # prefetched under another current stream (a user stream in forward, autograd's in
             # backward): the allocator must not reuse the block while THIS stream reads it
@@ -415,6 +488,8 @@ class _GatherRuntime:
         if self.sequence:
             self.recording = False
         self.pending.clear()
+        self._waves_launched.clear()
+        self._waited.clear()
         self.pos = 0
         self._prefetch(0)
 
@@ -522,7 +597,7 @@ class Zero3ParamManager:
         rt = self._runtime()
         key = ("param", id(self))
         rt.launch(key, [self])
-        out, ev, hold, _ = rt.pending.pop(key)
+        out, ev, hold, _, _ = rt.pending.pop(key)
         cur = torch.cuda.current_stream(self.shard.device)
         if ev is not None:
             cur.wait_event(ev)
@@ -888,13 +963,11 @@ class _GradReducer:
         self.launched_in_backward = 0
 
     def register_hooks(self):
-        return [_add_post_accumulate_hook(p, functools.partial(self._on_grad_hook, i))
+        return [_add_post_accumulate_hook(p, functools.partial(self.on_grad_ready, i))
                 for i, p in enumerate(self.opt.params) if p.requires_grad]
 
-    def _on_grad_hook(self, i: int, _param):
-        self.on_grad_ready(i)
-
-    def on_grad_ready(self, i: int):
+    def on_grad_ready(self, i: int, _param=None):
+        """Parameter i's gradient is complete (its post-accumulate-grad hook, or by hand)."""
         if self.marked[i]:
             raise RuntimeError(
                 "zero_amd ZeRO-3: gradient of parameter %d accumulated twice before step(); "
@@ -1058,13 +1131,19 @@ class _GradReducer:
 # CPU 16.0 -> 13.3 ms, profiles/r03_z3_bucket_ab.json), at the price of up to 512 MB of full
 # gradients waiting for their collective — nothing against 288 GB of HBM.
 RS_BUCKET_MB = 512.0
+# Module gathers ordered (and prefetched) as waves of this many consecutive groups: one ready and
+# one done event, and one consumer wait, per wave (see _GatherRuntime).  2 halves the cross-stream
+# waits of the per-module ordering; the compute of a wave's first module waits for the whole wave
+# (both gathers were launched one wave earlier, while the previous wave computed).
+GATHER_WAVE = 2
 
 
 class ShardedOptimizer:
     """zero3.py:81-168 with ``update`` selecting reference (no-op) or real ZeRO-3 updates."""
 
     def __init__(self, optimizer: Optimizer, *, update: bool = False, comm=None, sync: bool = True,
-                 gather_dtype=None, bucket_mb: float = RS_BUCKET_MB, grad_comm: str | None = None):
+                 gather_dtype=None, bucket_mb: float = RS_BUCKET_MB, grad_comm: str | None = None,
+                 gather_wave: int = GATHER_WAVE):
         if not isinstance(optimizer, torch.optim.Adam):
             raise TypeError("zero_amd ShardedOptimizer wraps torch.optim.Adam / AdamW")
         self.optimizer = optimizer
@@ -1102,7 +1181,7 @@ class ShardedOptimizer:
         if comm is None:
             comm = RcclComm()
         self.comm = comm
-        self.runtime = _GatherRuntime(world_size, rank, comm, dev)
+        self.runtime = _GatherRuntime(world_size, rank, comm, dev, wave=gather_wave)
         # zero3.py:104-110: every param becomes its dim-0 chunk — here a view of the chunk arena
         # (the full tensor is released); one manager per param
         self._arena = _ChunkArena(self.params, world_size, rank)

@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--blocks", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--wave", type=int, default=None, help="gather wave (default: the library's)")
+    ap.add_argument("--bucket-mb", type=float, default=None, help="reduce-scatter bucket MB")
     ap.add_argument("--no-events", action="store_true",
                     help="DIAGNOSTIC: the ordered library calls and the consumer's stream wait "
                          "become no-ops (no HIP event record / wait at all): how much of the "
@@ -69,8 +71,13 @@ def main():
 
         comm._ordered = lambda name, dtype: (lambda after, ready, stream, done: None)
         _lib.lib.zs_stream_wait_event = lambda *a: 0
+    kw = {}
+    if args.wave is not None:
+        kw["gather_wave"] = args.wave
+    if args.bucket_mb is not None:
+        kw["bucket_mb"] = args.bucket_mb
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
-                                 sync=False, comm=comm)
+                                 sync=False, comm=comm, **kw)
     zero3.register_zero3_hooks(model, opt.param_managers)
     x = torch.zeros(1, device=dev, requires_grad=True)
     bwd_tid = set()
@@ -119,7 +126,8 @@ def main():
         print(json.dumps(rows[-1]), flush=True)
     med = lambda k: sorted(r[k] for r in rows)[len(rows) // 2]  # noqa: E731
     summ = {"config": args.config, "simulated_ws": ws, "iters_per_block": args.iters,
-            "no_events": args.no_events,
+            "no_events": args.no_events, "gather_wave": opt.runtime.wave,
+            "bucket_mb": args.bucket_mb,
             "autograd_thread_is_main": bool(bwd_tid and bwd_tid <= {main_tid}),
             "median": {k: med(k) for k in ("wall_ms", "cpu_ms", "main_thread_ms",
                                            "autograd_thread_ms", "other_threads_ms")},
