@@ -1,0 +1,34 @@
+"""Post-accumulate-grad hook callbacks that hold their owner weakly.
+
+torch keeps a tensor's post-accumulate-grad hooks in a dict referenced from C++ (the autograd
+meta), and the garbage collector does not traverse that edge: a hook whose closure reaches the
+parameter again (hook -> optimizer -> its parameter list -> the parameter -> hook) is a cycle the
+collector cannot see, so dropping the optimizer and the model would never free them — nor the
+flat arenas and optimizer state they hold (tests/test_gpu_placement.py).  Every post-accumulate
+hook of the package therefore calls its owner through ``WeakCall``: the owner (an engine, a
+reducer, a hook state) is kept alive by whoever uses it, and the hook left on a parameter after
+its owner is gone is a no-op.
+"""
+from __future__ import annotations
+
+import weakref
+
+
+class WeakCall:
+    """``owner.<name>(*args)`` through a weak reference to ``owner``; the tensor the hook passes is
+    dropped.  A no-op once the owner is gone."""
+
+    __slots__ = ("_ref", "_name", "_args")
+
+    def __init__(self, owner, name: str, *args):
+        self._ref = weakref.ref(owner)
+        self._name = name
+        self._args = args
+
+    def __call__(self, _tensor=None):
+        owner = self._ref()
+        if owner is not None:
+            getattr(owner, self._name)(*self._args)
+
+    def alive(self) -> bool:
+        return self._ref() is not None

@@ -39,6 +39,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from ._hooks import WeakCall
 from .engine import ALIGN_ELEMS, ShardEngine, _ptr
 from .kernels import CopySet
 
@@ -282,11 +283,13 @@ class FlatEngine(ShardEngine):
 
     def _hook_new(self, req: np.ndarray):
         """Hook every parameter that requires grad and has no hook of this engine yet."""
-        fn = self._ov_ready if self.overlap else self._mark
+        name = "_ov_ready" if self.overlap else "_mark"
         for i in np.nonzero(req & ~self.hooked)[0]:
             i = int(i)
+            # the engine is reached weakly: a strong closure would be a cycle through the
+            # parameter's C++-held hook dict that the garbage collector cannot see (_hooks.py)
             self._mark_hooks.append(self.params[i].register_post_accumulate_grad_hook(
-                lambda _p, i=i: fn(i)))
+                WeakCall(self, name, i)))
             self.hooked[i] = True
 
     # ------------------------------------------------------------------------------------------

@@ -28,6 +28,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from ._hooks import WeakCall
 from .comm import comm_stream
 from .kernels import CopySet
 
@@ -132,8 +133,10 @@ class GradBuckets:
         handles = []
         for i, p in enumerate(self.params):
             if p.requires_grad:
+                # weakly: the buckets are owned by the engine (engine.gb); a strong closure would
+                # be a cycle through the parameter's C++-held hook dict (_hooks.py)
                 handles.append(p.register_post_accumulate_grad_hook(
-                    lambda _p, i=i: self.on_grad_ready(i)))
+                    WeakCall(self, "on_grad_ready", i)))
         return handles
 
     # ------------------------------------------------------------------------------------------

@@ -37,7 +37,6 @@ on the same side stream, so one communicator sees one totally ordered sequence o
 from __future__ import annotations
 
 import contextlib
-import functools
 import time
 import weakref
 
@@ -49,6 +48,7 @@ from torch.utils.weak import WeakIdKeyDictionary
 from . import _lib
 from ._lib import ZS_BF16, ZS_BF16_SPLIT, ZS_F32
 from . import checkpoint as ckpt
+from ._hooks import WeakCall
 from ._sharded import adam_group_hparams
 from .comm import RcclComm, comm_stream, zs_dtype
 from .engine import ALIGN_ELEMS, probed_zeros
@@ -618,6 +618,12 @@ class Zero3ParamManager:
         self.full_data = None
 
 
+class _TensorHookState:
+    """Holder of the tensor-style backward bookkeeping's ``grad_ready`` (register_zero3_hooks)."""
+
+    grad_ready = None
+
+
 def _grad_tensors(output):
     """The tensors of a module's output (nested tuples / lists / dicts) that autograd will
     differentiate through."""
@@ -772,12 +778,16 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
                 # newly trainable: its post-accumulate hook from now on (keyed by id, so the hook
                 # the parameter holds keeps no reference to it)
                 hooked_params.add(id(p))
-                handles.append(_add_post_accumulate_hook(p, functools.partial(grad_ready, id(p))))
+                handles.append(_add_post_accumulate_hook(p, WeakCall(state, "grad_ready", id(p))))
 
     open_ = {}     # id(module) -> managers gathered for its backward, not released yet
     pending = {}   # id(module) -> parameter gradients still to come this backward
     queued = [False]
     warned = set()
+    # the parameters' post-accumulate hooks reach grad_ready through a weak reference to this
+    # holder (a strong closure would be a cycle through the parameter's C++-held hook dict,
+    # _hooks.py); the module hooks below keep it alive as long as the model has them
+    state = _TensorHookState()
 
     def end_backward():
         queued[0] = False
@@ -829,7 +839,7 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
                     RuntimeWarning, stacklevel=2)
         return None
 
-    def grad_ready(pid, _p):
+    def grad_ready(pid):
         for mid in param_mods.get(pid, ()):
             if mid in open_:
                 pending[mid] -= 1
@@ -837,6 +847,8 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
                     for mg in open_.pop(mid):
                         mg.release()
 
+    state.grad_ready = grad_ready
+    forward_pre.state = state  # (the strong reference: module hook -> forward_pre -> state)
     for m in hooked:
         handles.append(m.register_forward_pre_hook(forward_pre))
         handles.append(m.register_forward_hook(forward_post))
@@ -963,7 +975,8 @@ class _GradReducer:
         self.launched_in_backward = 0
 
     def register_hooks(self):
-        return [_add_post_accumulate_hook(p, functools.partial(self.on_grad_ready, i))
+        # weakly (_hooks.py): the reducer is owned by its optimizer
+        return [_add_post_accumulate_hook(p, WeakCall(self, "on_grad_ready", i))
                 for i, p in enumerate(self.opt.params) if p.requires_grad]
 
     def on_grad_ready(self, i: int, _param=None):
@@ -1111,9 +1124,9 @@ class _GradReducer:
                 opt.comm.reduce_scatter_group(sp, recv, count, dt, cs)
         else:
             with _group_ctx(opt.comm):
-                for i, send in sends:
+                for i, send in sends:  # (a zero-copy send is the grad itself: flatten the view)
                     s = int(ar.slot[i])
-                    opt.comm.reduce_scatter(send, opt._G[s:s + int(ar.S[i])], cs)
+                    opt.comm.reduce_scatter(send.view(-1), opt._G[s:s + int(ar.S[i])], cs)
         # the group has been enqueued: a buffer freed from here on is only reused after it
         for i, send in sends:
             send.record_stream(cs)

@@ -62,3 +62,27 @@ def test_probe_keeps_callers_cached_block(gpu, pg1):
     torch.cuda.synchronize()
     assert engine.placed_bytes() == before  # placed buffers went back with their tensors
     assert torch.cuda.mem_get_info(dev)[0] > free0 + held // 2
+
+
+def test_zero3_update_state_freed_with_optimizer(gpu, pg1):
+    """ZeRO-3 update mode: the placed Adam state (here 2 x 8192^2 fp32 chunks: 1 GiB of m / v)
+    goes back to the device when the model and the optimizer are dropped — the reducer's
+    post-accumulate hooks hold it weakly (zero_amd/_hooks.py)."""
+    import gc
+
+    from zero_amd import engine, zero3
+
+    before = engine.placed_bytes()
+    model = torch.nn.Sequential(torch.nn.Linear(8192, 8192, bias=False),
+                                torch.nn.Linear(8192, 8192, bias=False)).to(gpu)
+    opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True)
+    zero3.register_zero3_hooks(model, opt.param_managers)
+    assert engine.placed_bytes() - before >= 2 * 2 * 8192 * 8192 * 4
+    x = torch.randn(4, 8192, device=gpu)
+    model(x).sum().backward()
+    opt.step()
+    torch.cuda.synchronize()
+    del opt, model, x
+    gc.collect()
+    torch.cuda.synchronize()
+    assert engine.placed_bytes() == before

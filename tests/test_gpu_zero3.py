@@ -388,9 +388,9 @@ def test_c5_paramset_step_rank0_of_ws8(gpu, monkeypatch, ws):
         assert opt._reducer.launched_in_backward == opt._reducer.K
         opt.step()
         torch.cuda.synchronize()
-        # forward + backward per layer, plus the prefetch of the next iteration's first gather
+        # forward + backward per layer, plus the prefetch of the next iteration's first wave
         # (ws = 1: no hooks at all)
-        assert opt.runtime.n_gathers == (2 * len(model.layers) + 1 if ws > 1 else 0)
+        assert opt.runtime.n_gathers == (2 * len(model.layers) + opt.runtime.wave if ws > 1 else 0)
         ar = opt._arena
         if ws == 1:
             assert ar.P.numel() > 2 ** 32

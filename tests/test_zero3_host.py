@@ -200,3 +200,45 @@ def test_comm_time_waits_for_both_events():
     opt._comm_spans = [(Ev(False), Ev(True)), (Ev(True), Ev(True))]
     opt._collect_comm_time(completed_only=True)
     assert len(opt._comm_spans) == 1 and opt.communication_time == 2.0 / 1e3
+
+
+def test_weak_post_accumulate_callbacks_do_not_leak():
+    """torch does not let the garbage collector traverse a tensor's post-accumulate-grad hooks,
+    so a hook closure that reaches its parameter again is an uncollectable cycle; the package's
+    post-accumulate hooks call their owners through zero_amd._hooks.WeakCall instead."""
+    from zero_amd._hooks import WeakCall
+
+    class Owner:
+        def __init__(self):
+            self.p = torch.nn.Parameter(torch.zeros(3))
+            self.calls = []
+            self.p.register_post_accumulate_grad_hook(WeakCall(self, "hit", 7))
+
+        def hit(self, i):
+            self.calls.append(i)
+
+    o = Owner()
+    (o.p * 2).sum().backward()
+    assert o.calls == [7]
+    ref = weakref.ref(o)
+    del o
+    gc.collect()
+    assert ref() is None  # (a plain `lambda _p: self.hit(7)` keeps it alive forever)
+
+
+def test_tensor_hooks_release_their_managers():
+    """register_zero3_hooks' tensor-style bookkeeping: once the model and the managers are dropped,
+    nothing the parameters' hooks hold keeps the managers alive."""
+    z3 = _zero3()
+    model = torch.nn.Sequential(torch.nn.Linear(4, 4), torch.nn.Linear(4, 4))
+    log = []
+    rt = _FakeRuntime(log)
+    mgrs = {p: _FakeManager(p, str(i), rt, log) for i, p in enumerate(model.parameters())}
+    z3.register_zero3_hooks(model, mgrs, backward_hooks="tensor")
+    model(torch.randn(2, 4)).sum().backward()
+    ref = weakref.ref(next(iter(mgrs.values())))
+    params = list(model.parameters())  # the parameters outlive the model, as a user's may
+    del model, mgrs, rt
+    gc.collect()
+    assert ref() is None
+    del params
