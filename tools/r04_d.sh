@@ -12,4 +12,12 @@ timeout -k 10 400 python3 tools/z3_host_ab.py --baseline r03 --blocks 4 --out "$
 tail -1 "$O/z3_ab.log"
 timeout -k 10 300 python3 tools/z3_host_threads.py --blocks 3 --out "$O/z3_threads.json" > "$O/z3_threads.log" 2>&1 || { tail -20 "$O/z3_threads.log"; exit 1; }
 grep '^{' "$O/z3_threads.log" | tail -1
+# the runtime thread's CPU: HIP runtime knobs for cross-queue dependencies (diagnostic)
+for e in "ROC_CPU_WAIT_FOR_SIGNAL=0" "ROC_ACTIVE_WAIT_TIMEOUT=0" "HSA_ENABLE_INTERRUPT=0"; do
+  tag=$(echo "$e" | tr '=' '_')
+  env $e timeout -k 10 120 python3 tools/hip_event_cost.py > "$O/hip_event_cost_$tag.log" 2>&1 || { tail -5 "$O/hip_event_cost_$tag.log"; exit 1; }
+  echo "== $e"; grep '"ordered' "$O/hip_event_cost_$tag.log"
+  env $e timeout -k 10 300 python3 tools/z3_host_threads.py --blocks 3 --out "$O/z3_threads_$tag.json" > "$O/z3_threads_$tag.log" 2>&1 || { tail -5 "$O/z3_threads_$tag.log"; exit 1; }
+  grep '^{' "$O/z3_threads_$tag.log" | tail -1
+done
 echo "[r04d] done"
