@@ -85,6 +85,30 @@ def main():
                      "other_threads_us": {f"{names.get(t, '?')}[{t}]": round(v / args.n * 1e6, 2)
                                           for v, t in others}})
         print(json.dumps(rows[-1]), flush=True)
+    # time-based or count-based?  ONE cross-stream wait on an event behind ~`long_ms` of work on
+    # the other stream, the host idle meanwhile (torch.cuda.synchronize): the runtime threads'
+    # CPU over the whole span, vs the same work with no cross-stream wait
+    big = torch.empty(1 << 28, device=dev)  # 1 GiB
+    big2 = torch.empty_like(big)
+    for wait in (False, True, False, True):
+        torch.cuda.synchronize()
+        s0, w0 = snap(), time.perf_counter()
+        for _ in range(5):
+            for _ in range(20):
+                big2.copy_(big)  # ~20 x 0.35 ms on s1
+            ev[2].record(s1)
+            if wait:
+                s2.wait_event(ev[2])
+                ev[3].record(s2)
+            torch.cuda.synchronize()
+        w, s_1 = time.perf_counter() - w0, snap()
+        d = {t: s_1[t] - s0.get(t, 0.0) for t in s_1}
+        other = sum(v for t, v in d.items() if t != main_tid)
+        print(json.dumps({"case": f"long work on s1, cross-stream wait on it: {wait}",
+                          "wall_ms_per_rep": round(w / 5 * 1e3, 3),
+                          "other_threads_ms_per_rep": round(other / 5 * 1e3, 3),
+                          "main_thread_ms_per_rep": round(d.get(main_tid, 0.0) / 5 * 1e3, 3)}),
+              flush=True)
     print(json.dumps({"threads": sorted(set(thread_names().values()))}), flush=True)
 
 
