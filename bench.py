@@ -622,6 +622,9 @@ def _zero3_report(args, opt, world, rank, red_dev, el, total, workload, extra):
                       else "fp32"),
             "data": "synthetic",
             "config": dict(workload=workload, params=int(total), param_dtype=args.dtype, zero=3,
+                           collective_stream=("compute (single stream)" if opt.runtime.stream is None
+                                              else "side stream, prefetched in waves of "
+                                              f"{opt.runtime.wave}"),
                            update="real ZeRO-3 (update=True)", bucket_mb=args.bucket_mb or 512.0,
                            gather_dtype=args.gather or args.dtype, parallelism=f"dp{world}",
                            gathers=("none at N=1: every shard is its whole parameter, no hooks "
@@ -773,7 +776,8 @@ def zero3_gather_check(opt, model, shapes, full_copies, dev, world, rank, red_de
     ms = [opt.param_managers[getattr(layer, f"p{k}")] for k in range(layer.n)]
     rt.launch(("exchange-check",), ms)
     out, ev, _hold, _, _ = rt.pending.pop(("exchange-check",))
-    torch.cuda.current_stream(dev).wait_event(ev)
+    if ev is not None:  # (single-stream mode: already in order on this stream)
+        torch.cuda.current_stream(dev).wait_event(ev)
     torch.cuda.synchronize()
     bits = lambda t: t.reshape(-1).view(torch.int16 if t.element_size() == 2 else torch.int32)  # noqa: E731
     bad = [i for (m, full), i in zip(out, idx) if not torch.equal(bits(full[:m.numel]),
@@ -1094,8 +1098,11 @@ def bench_zero3_paramset(args, world, rank, dev, use_nccl):
         zero3.get = lambda what, dm=None: {"ws": sim_ws, "rank": 0}.get(what) \
             if what in ("ws", "rank") else real_get(what, dm)
     kw = {} if comm is None else {"comm": comm}
+    # the synthetic layers compute nothing, so there is nothing to overlap the collectives with:
+    # by default they run on the compute stream itself (no cross-stream ordering)
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
-                                 sync=False, gather_dtype=args.gather, bucket_mb=args.bucket_mb or 512.0, **kw)
+                                 sync=False, gather_dtype=args.gather, bucket_mb=args.bucket_mb or 512.0,
+                                 side_stream=args.z3_stream == "side", **kw)
     zero3.register_zero3_hooks(model, opt.param_managers)
     gather_check = None
     if world > 1:
@@ -1276,6 +1283,10 @@ def main(argv=None):
                          "chunks, i.e. one parameter gather per iteration")
     ap.add_argument("--batch", type=int, default=None,
                     help="ZeRO-3 MLP batch (default 16, zero1.py:144) / --train batch (default 1)")
+    ap.add_argument("--z3-stream", default="single", choices=["single", "side"],
+                    help="--zero 3 on the C4/C5 parameter sets: collectives on the compute stream "
+                         "(single: the synthetic layers compute nothing to overlap with) or on a "
+                         "side stream with prefetch (side: what a model with compute uses)")
     ap.add_argument("--gather", default=None, choices=["fp8"],
                     help="--zero 3: all-gather parameters as row-scaled fp8 E4M3 (SURVEY §8(f) 4)")
     ap.add_argument("--train", default=None, choices=["smollm3"],

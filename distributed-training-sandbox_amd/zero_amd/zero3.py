@@ -133,17 +133,25 @@ class _GatherRuntime:
     the caller (profiles/r04_hip_event_cost.json), and at one wait pair per module those were 6 of
     the 12 ms of host CPU of a simulated ws = 8 C5 iteration.  ``wave = 1`` is the per-module
     ordering.  ``end_iteration`` (called at the end of step()) prefetches the first wave of the next
-    iteration."""
+    iteration.
 
-    def __init__(self, ws, rank, comm, device, wave: int = 2):
+    ``side_stream=False``: every collective is enqueued on the stream that asks for it (the current
+    stream), in order with the compute — no events, no cross-stream waits, the reference's own
+    structure (zero3.py:36-41 gathers synchronously in the hook).  For a model with nothing to
+    overlap the collectives with (the synthetic parameter-set model of BASELINE.json configs[4])
+    the GPU time is the same, and the host saves the stream ordering and the HIP runtime thread
+    that polls while a cross-stream dependency is pending (≈ one core for as long as the host runs
+    ahead of the GPU: profiles/r04_hip_event_cost.jsonl)."""
+
+    def __init__(self, ws, rank, comm, device, wave: int = 2, side_stream: bool = True):
         self.ws, self.rank, self.comm, self.device = ws, rank, comm, device
         if int(wave) < 1:
             raise ValueError(f"gather wave must be >= 1 (got {wave})")
         self.wave = int(wave)
         self._waves_launched = set()  # wave indices launched this iteration
         self._waited = {}             # done-event handle -> stream handle that waited on it
-        self.stream = comm_stream(device)
-        self._side_h = self.stream.cuda_stream
+        self.stream = comm_stream(device) if side_stream else None
+        self._side_h = self.stream.cuda_stream if side_stream else None
         # the current stream as a raw handle (torch.cuda.current_stream builds a Stream object per
         # call; the hot path only needs the handle for the library's ordered calls)
         self._dev_idx = device.index if device.index is not None else torch.cuda.current_device()
@@ -177,6 +185,10 @@ class _GatherRuntime:
     def _cur_h(self) -> int:
         return torch._C._cuda_getCurrentRawStream(self._dev_idx)
 
+    def side(self):
+        """The stream collectives go to: the side stream, or (single-stream mode) the current."""
+        return self.stream if self.stream is not None else torch.cuda.current_stream(self.device)
+
     def launch(self, key, managers, cur_h=None):
         """Enqueue the all-gather of ``managers`` on the side stream; returns immediately.
         ``cur_h``: the raw handle of the stream the gathered tensors will be read on (default:
@@ -195,7 +207,17 @@ class _GatherRuntime:
             cur_h = self._cur_h()
         timed = self.gather_events is not None and self.ws > 1
         plan = self._tables[key] if key in self._tables else self._table(key, managers)
-        side = self.stream
+        if plan is not None and plan[-1] is not None and not timed and self.stream is None:
+            # single-stream mode: the RCCL group on the consumer's stream, nothing to order
+            send, count, offs, total, dt, es, views, recv, raw, ordered = plan
+            hold = torch.empty(total, dtype=managers[0].shard.dtype, device=self.device)
+            np.add(offs, np.uint64(hold.data_ptr()), out=recv)
+            ordered(cur_h, 0, cur_h, 0)
+            self.pending[key] = ([(m, hold.as_strided(shape, stride, off)) for m, (shape, stride, off)
+                                  in zip(managers, views)], None, hold, cur_h, None)
+            self.n_gathers += 1
+            return
+        side = self.side()
         if plan is not None and plan[-1] is not None and not timed:
             # one allocation for the module's full tensors and ONE library call: ready event on
             # the compute stream (the shards may just have been updated), the side stream's wait,
@@ -406,19 +428,25 @@ class _GatherRuntime:
             for k, ms in todo:
                 self.launch(k, ms, cur_h)
             return
-        ready_h = self._key_events(todo[0][0])[2]
-        _, done_ev, _, done_h = self._key_events(todo[-1][0])
-        self._waited.pop(done_h, None)
+        single = self.stream is None
+        if single:  # everything on the consumer's stream: no events
+            ready_h = done_h = 0
+            done_ev = None
+        else:
+            ready_h = self._key_events(todo[0][0])[2]
+            _, done_ev, _, done_h = self._key_events(todo[-1][0])
+            self._waited.pop(done_h, None)
         last = len(todo) - 1
-        side, side_h = self.stream, self._side_h
+        side, side_h = self.stream, (cur_h if single else self._side_h)
         for j, ((k, ms), plan) in enumerate(zip(todo, plans)):
             send, count, offs, total, dt, es, views, recv, raw, ordered = plan
             hold = torch.empty(total, dtype=ms[0].shard.dtype, device=self.device)
-            hold.record_stream(side)
+            if not single:
+                hold.record_stream(side)
             np.add(offs, np.uint64(hold.data_ptr()), out=recv)
             ordered(cur_h, ready_h if j == 0 else 0, side_h, done_h if j == last else 0)
             self.pending[k] = ([(m, hold.as_strided(shape, stride, off)) for m, (shape, stride, off)
-                                in zip(ms, views)], done_ev, hold, cur_h, done_h)
+                                in zip(ms, views)], done_ev, hold, cur_h, done_h or None)
             self.n_gathers += 1
 
     def _ensure_wave(self, w, cur_h=None):
@@ -459,15 +487,21 @@ class _GatherRuntime:
             self.n_prefetch_hits += 1
         self.launch(key, managers, cur_h)
         out, ev, hold, alloc_h, wait_h = self.pending.pop(key)
-        if ev is None:  # ws == 1
+        if ev is None and hold is None:  # ws == 1
             for m, full in out:
                 m._install_full(full)
             return
-        if self._waited.get(wait_h) != cur_h:  # once per wave and consuming stream
-            rc = _lib.lib.zs_stream_wait_event(cur_h, wait_h)
-            if rc:
-                _lib.check(rc, "zs_stream_wait_event")
-            self._waited[wait_h] = cur_h
+        if wait_h is not None:
+            if self._waited.get(wait_h) != cur_h:  # once per wave and consuming stream
+                rc = _lib.lib.zs_stream_wait_event(cur_h, wait_h)
+                if rc:
+                    _lib.check(rc, "zs_stream_wait_event")
+                self._waited[wait_h] = cur_h
+        elif alloc_h is not None and alloc_h != cur_h:
+            # single-stream mode, gathered on another stream than this one: order the two
+            e = torch.cuda.Event()
+            e.record(torch.cuda.ExternalStream(alloc_h, device=self.device))
+            torch.cuda.current_stream(self.device).wait_event(e)
         if hold is not None and alloc_h is not None and alloc_h != cur_h:
             # prefetched under another current stream (a user stream in forward, autograd's in
             # backward): the allocator must not reuse the block while THIS stream reads it
@@ -951,7 +985,7 @@ class _GradReducer:
         self._shard_grad = [None] * n  # cached grad-arena views handed out as shard grads
         self.ev_done = [torch.cuda.Event() for _ in range(self.K)]
         self.ev_ready = [torch.cuda.Event() for _ in range(self.K)]
-        cs = opt.runtime.stream if opt.world_size > 1 else None
+        cs = opt.runtime.stream if opt.world_size > 1 else None  # (None: single-stream mode)
         if cs is not None:  # torch creates a HIP event at its first record: the raw handles are
             for e in self.ev_done + self.ev_ready:  # what the ordered library calls record
                 e.record(cs)
@@ -1012,7 +1046,7 @@ class _GradReducer:
         if opt.world_size == 1:
             return
         cur = torch.cuda.current_stream(opt._arena.device)
-        if self.K:
+        if self.K and opt.runtime.stream is not None:
             cur.wait_event(self.ev_done[self.K - 1])
         if opt._G.dtype != opt.params[0].dtype:  # a bf16 exchange's chunks stay internal
             return
@@ -1093,8 +1127,20 @@ class _GradReducer:
                         send = torch.zeros(ws * S, dtype=wdt, device=dev)
                         send[:N].copy_(flat)
             sends.append((i, send))
-        cs = opt.runtime.stream
+        single = opt.runtime.stream is None
         tab = self._rs_table(k) if hasattr(opt.comm, "reduce_scatter_group") else None
+        if single and tab is not None and tab[5] is not None and self.timing is None:
+            # single-stream mode: the bucket's RCCL group on the stream that produced the grads
+            recv, count, dt, sp, raw, ordered = tab
+            for j, (_, t) in enumerate(sends):
+                sp[j] = t.data_ptr()
+            ordered(cur_h, 0, cur_h, 0)
+            for i, _ in sends:
+                opt.params[i].grad = None
+            return
+        if cur is None:
+            cur = torch.cuda.current_stream(dev)
+        cs = cur if single else opt.runtime.stream
         if tab is not None and tab[5] is not None and self.timing is None:
             # ONE library call: ready event on the stream that produced the grads, the side
             # stream's wait, the bucket's RCCL group of reduce-scatters, the done event
@@ -1106,8 +1152,6 @@ class _GradReducer:
                 send.record_stream(cs)
                 opt.params[i].grad = None
             return
-        if cur is None:
-            cur = torch.cuda.current_stream(dev)
         ready = self.ev_ready[k]
         ready.record(cur)
         cs.wait_event(ready)
@@ -1156,7 +1200,7 @@ class ShardedOptimizer:
 
     def __init__(self, optimizer: Optimizer, *, update: bool = False, comm=None, sync: bool = True,
                  gather_dtype=None, bucket_mb: float = RS_BUCKET_MB, grad_comm: str | None = None,
-                 gather_wave: int = GATHER_WAVE):
+                 gather_wave: int = GATHER_WAVE, side_stream: bool = True):
         if not isinstance(optimizer, torch.optim.Adam):
             raise TypeError("zero_amd ShardedOptimizer wraps torch.optim.Adam / AdamW")
         self.optimizer = optimizer
@@ -1194,7 +1238,8 @@ class ShardedOptimizer:
         if comm is None:
             comm = RcclComm()
         self.comm = comm
-        self.runtime = _GatherRuntime(world_size, rank, comm, dev, wave=gather_wave)
+        self.runtime = _GatherRuntime(world_size, rank, comm, dev, wave=gather_wave,
+                                      side_stream=side_stream)
         # zero3.py:104-110: every param becomes its dim-0 chunk — here a view of the chunk arena
         # (the full tensor is released); one manager per param
         self._arena = _ChunkArena(self.params, world_size, rank)
@@ -1302,7 +1347,7 @@ class ShardedOptimizer:
                 shards.append((g.contiguous(), n, g.shape))
         ready = torch.cuda.Event()
         ready.record(cur)
-        cs = self.runtime.stream
+        cs = self.runtime.side()
         cs.wait_event(ready)
         with _group_ctx(self.comm):
             for buf, _, _ in shards:
@@ -1349,8 +1394,12 @@ class ShardedOptimizer:
         red.flush()  # grads assigned outside backward (or backward without hooks firing)
         done = None
         if self.world_size > 1 and red.K:
-            done = red.ev_done[red.K - 1]
-            cur.wait_event(done)
+            if self.runtime.stream is None:  # single stream: the reduce-scatters are behind us
+                done = torch.cuda.Event(enable_timing=True)
+                done.record(cur)
+            else:
+                done = red.ev_done[red.K - 1]
+                cur.wait_event(done)
         idx = np.nonzero(red.had_grad & (ar.ln > 0))[0]
         self._steps[idx] += 1
         hps = {gi: adam_group_hparams(self._groups[gi], self.optimizer) for gi in set(self._group_of)}
@@ -1441,8 +1490,11 @@ class ShardedOptimizer:
         with torch.no_grad():
             done = self._step_update() if self.update else self._reduce_reference()
         if done is not None and self.world_size > 1:
-            e1 = torch.cuda.Event(enable_timing=True)
-            e1.record(self.runtime.stream)  # after the last gradient collective
+            if self.runtime.stream is None:  # single stream: `done` follows the last collective
+                e1 = done
+            else:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record(self.runtime.stream)  # after the last gradient collective
             self._comm_spans.append((e0, e1))
         retired = len(self._retired) if self.update else 0
         if self._sync or retired > 64:

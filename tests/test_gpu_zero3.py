@@ -56,14 +56,15 @@ def _set_grad(p, g):
     p.data = shard
 
 
-def _ref_mode(rank, ws, name, dev, comm=None):
+def _ref_mode(rank, ws, name, dev, comm=None, side_stream=True):
     """Reference mode with the real hooks: forward/backward gather, step reduces and discards."""
     from zero_amd import zero3
 
     z = np.load(GOLDEN / name)
     model = _model(z, dev)
     kw = {} if comm is None else {"comm": comm}
-    opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), **kw)
+    opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3),
+                                 side_stream=side_stream, **kw)
     zero3.register_zero3_hooks(model, opt.param_managers)
     x, y = _xy(z, rank, dev)
     for t in range(int(z["steps"])):
@@ -135,7 +136,8 @@ def _update_injected(rank, ws, name, dev, comm=None, dtype=torch.float32):
             assert rel(st["exp_avg"].cpu().numpy(), _chunk(z[key], ws, rank)) <= 1e-6
 
 
-def _update_hooks(rank, ws, name, dev, comm=None, backward_hooks=None):
+def _update_hooks(rank, ws, name, dev, comm=None, backward_hooks=None, side_stream=True,
+                  gather_wave=None):
     """update=True through the real hooks: forward / backward all-gathers, gradients
     reduce-scattered from the post-accumulate-grad hooks during backward, fused Adam on the
     chunks.  Grads come from hipBLAS GEMMs, so the bound vs the CPU reference is 1e-4.  Backward
@@ -146,8 +148,11 @@ def _update_hooks(rank, ws, name, dev, comm=None, backward_hooks=None):
     z = np.load(GOLDEN / name)
     model = _model(z, dev)
     kw = {} if comm is None else {"comm": comm}
+    if gather_wave is not None:
+        kw["gather_wave"] = gather_wave
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
-                                 bucket_mb=2e-3, **kw)  # ~2 KB buckets: several launches in backward
+                                 bucket_mb=2e-3, side_stream=side_stream,
+                                 **kw)  # ~2 KB buckets: several launches in backward
     zero3.register_zero3_hooks(model, opt.param_managers, backward_hooks=backward_hooks)
     params = list(model.parameters())
     x, y = _xy(z, rank, dev)
@@ -173,6 +178,20 @@ def _update_hooks(rank, ws, name, dev, comm=None, backward_hooks=None):
 
 def _update_hooks_module(rank, ws, name, dev, comm=None):
     _update_hooks(rank, ws, name, dev, comm=comm, backward_hooks="module")
+
+
+def _update_hooks_single(rank, ws, name, dev, comm=None):
+    """update mode with every collective on the compute stream (side_stream=False)."""
+    _update_hooks(rank, ws, name, dev, comm=comm, side_stream=False)
+
+
+def _update_hooks_wave3(rank, ws, name, dev, comm=None):
+    """update mode with gathers ordered in waves of 3 (six Linear modules: two waves per pass)."""
+    _update_hooks(rank, ws, name, dev, comm=comm, gather_wave=3)
+
+
+def _ref_mode_single(rank, ws, name, dev, comm=None):
+    _ref_mode(rank, ws, name, dev, comm=comm, side_stream=False)
 
 
 @pytest.fixture

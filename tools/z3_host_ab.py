@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--baseline", default="r02", choices=["r02", "r03"])
     ap.add_argument("--out", default=None)
+    ap.add_argument("--single", action="store_true",
+                    help="also time the current runtime with side_stream=False")
     args = ap.parse_args()
 
     import torch
@@ -59,7 +61,7 @@ def main():
     shapes = CONFIGS[args.config][1]()
     ws = args.ws
 
-    def build(mod, seed):
+    def build(mod, seed, **okw):
         gen = torch.Generator(device=dev).manual_seed(seed)
         params = [torch.nn.Parameter(torch.empty(s, device=dev, dtype=torch.bfloat16).normal_(
             0.0, 0.02, generator=gen)) for s in shapes]
@@ -71,7 +73,7 @@ def main():
         mod.get = lambda what, dm=None: {"ws": ws, "rank": 0}.get(what) if what in ("ws", "rank") \
             else real_get(what, dm)
         opt = mod.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
-                                   sync=False, comm=bench._NoComm(ws))
+                                   sync=False, comm=bench._NoComm(ws), **okw)
         mod.register_zero3_hooks(model, opt.param_managers)
         x = torch.zeros(1, device=dev, requires_grad=True)
 
@@ -82,13 +84,16 @@ def main():
         return step
 
     variants = {base: build(z3_old, 0), "current": build(z3_new, 0)}
+    if args.single:  # the current runtime with its collectives on the compute stream
+        variants["current_single_stream"] = build(z3_new, 0, side_stream=False)
     for st in variants.values():
         for _ in range(args.warmup):
             st()
     torch.cuda.synchronize()
     rows = []
     for b in range(args.blocks):
-        for name in ((base, "current") if b % 2 == 0 else ("current", base)):
+        names = list(variants)
+        for name in (names if b % 2 == 0 else names[::-1]):
             st = variants[name]
             torch.cuda.synchronize()
             w0, c0 = time.perf_counter(), time.process_time()
