@@ -657,7 +657,8 @@ __global__ __launch_bounds__(kThreads) void fp8_quantize_rowset_kernel(const QSe
 // issued before the stores of the current one, so on gfx950, whose vmcnt counts loads and stores
 // together, waiting for a batch's data never waits for the previous batch's stores: each wave keeps
 // one batch of loads and one of stores in flight throughout.
-constexpr int kDqU = 8;  // default accesses in flight per lane (zs_tune "dq_unroll": 4 / 8 / 16)
+constexpr int kDqU = 4;  // default accesses in flight per lane (zs_tune "dq_unroll": 4 / 8 / 16;
+                         // 4 measured best at ws = 1 and ws = 8, profiles/r04_dq_ab.json)
 
 struct DqSet {
   const unsigned char* q;

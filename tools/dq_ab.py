@@ -19,7 +19,7 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO / "distributed-training-sandbox_amd"))
 
 VARIANTS = [  # (dq_unroll, dq_nt_store, dq_wg_per_cu); the first is the library default
-    (8, 1, 0), (4, 1, 0), (16, 1, 0), (8, 0, 0), (16, 0, 0), (8, 1, 8), (16, 1, 4)]
+    (4, 1, 0), (8, 1, 0), (16, 1, 0), (4, 0, 0), (8, 0, 0), (4, 1, 8), (8, 1, 8)]
 
 
 def main():
