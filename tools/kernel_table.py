@@ -117,7 +117,7 @@ def main():
           "fp8_quantize_rows_wave_kernel<unsigned short,", len(layer))
     timed("fp8_dequantize_rows (7 launches, one per matrix; the gathered kernel at ws = 1)", dequant,
           3 * elems + 4 * nrows, f"one C5 decoder layer, {elems:,} elements",
-          "fp8_dequantize_gathered_kernel<unsigned short>", len(layer))
+          "fp8_dequantize_gathered_kernel<unsigned short,", len(layer))
     # the same layer through the gather group's fused forms: one quantise launch per register
     # class into one concatenated send buffer, one dequantise launch from it (ws = 1 layout: the
     # gathered buffer is the send buffer)
@@ -144,7 +144,7 @@ def main():
                             rows_a.ctypes.data, len_a.ctypes.data, dst.ctypes.data, _lib.ZS_BF16,
                             stream_handle(st)),
           3 * elems + 4 * nrows, f"one C5 decoder layer, {elems:,} elements",
-          "fp8_dequantize_gathered_kernel<unsigned short>", 1)
+          "fp8_dequantize_gathered_kernel<unsigned short,", 1)
     # (the in-place copies over these buffers run at the very end: see below)
 
     # DDP scale, in place: a 256 MiB bucket (fits the 256 MB MALL, so repeated launches partly hit
