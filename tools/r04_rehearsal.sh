@@ -5,6 +5,8 @@ set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(pwd)}"; O="$R/gpurun_out/r04r"; mkdir -p "$O"
 export TMPDIR=/tmp
 cd "$R" || exit 2
+timeout -k 10 90 tools/event_poll_probe 200 > "$O/event_poll_probe.jsonl" 2>&1 || { tail -5 "$O/event_poll_probe.jsonl"; exit 1; }
+cat "$O/event_poll_probe.jsonl"
 run() {
   local tag=$1 t=$2; shift 2
   GPU_MAX_HW_QUEUES=2 timeout -k 10 $t python3 bench.py --share-gpu --no-cpu-baseline --watchdog-s $((t - 20)) "$@" > "$O/$tag.json" 2> "$O/$tag.err"
