@@ -736,6 +736,7 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
         rt.key_managers = {}
         rt._tables = {}  # a key's managers may differ from an earlier registration
         rt._fp8_tables = {}
+        rt.iteration_callbacks = []  # (an earlier registration's bookkeeping is replaced)
         for mod in model.modules():
             ms = mod_managers[id(mod)]
             if ms:
