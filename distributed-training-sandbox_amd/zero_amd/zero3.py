@@ -121,8 +121,8 @@ def _add_post_accumulate_hook(param, fn):
 
 
 class _GatherRuntime:
-    """Side-stream collectives of one ShardedOptimizer: module all-gathers with one-ahead prefetch
-    (and, in update mode, the gradient reduce-scatters, on the same stream).
+    """Side-stream collectives of one ShardedOptimizer: module all-gathers prefetched one wave
+    ahead (and, in update mode, the gradient reduce-scatters, on the same stream).
 
     The first iteration records the order in which module groups are materialised (forward, then
     backward); afterwards the learned sequence is cut into *waves* of ``wave`` consecutive groups,
