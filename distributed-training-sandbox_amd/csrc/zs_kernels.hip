@@ -362,15 +362,17 @@ __device__ __forceinline__ T from_f32(float x) {
 
 // In place, kScaleU 16-B accesses per lane in flight: a wave step covers kScaleU contiguous 1 KiB
 // blocks (lane l of block u at 16-B chunk 64u + l), every load issued before the first store;
-// default cache policy (not non-temporal): a DDP bucket (64 MiB) is scaled right after the
-// all-reduce wrote it, while it is still in the 256 MB MALL; grid-stride over wave steps; the tail
-// (n % elements per step) by block 0.
+// grid-stride over wave steps; the tail (n % elements per step) by block 0.  Cache policy by size
+// (NT): a DDP bucket (64 MiB) is scaled right after the all-reduce wrote it, while it is still in
+// the 256 MB MALL — default policy; a buffer larger than the MALL cannot be there, so its loads
+// and stores carry the non-temporal hint (kScaleNtBytes; `zs_tune("scale_nt")` forces either).
 // (Round 2's one access in flight per lane measured 0.61 of 8 TB/s on a 4 GiB buffer.)
 // fp32: IEEE division (x / div), or an exact reciprocal multiply when div is a power of two;
 // bf16: the same in fp32, rounded to bf16 (RNE) — torch's div_ on a bf16 tensor.
 constexpr int kScaleU = 4;
+constexpr int64_t kScaleNtBytes = int64_t(256) << 20;
 
-template <typename T>
+template <typename T, bool NT>
 __global__ __launch_bounds__(kThreads) void scale_kernel(T* __restrict__ x, int64_t n, float div,
                                                          float inv, int pow2) {
 #pragma clang fp contract(off)
@@ -386,13 +388,17 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(T* __restrict__ x, int6
     T* base = x + w * kSpan + int64_t(lane) * V;
     uint4 raw[kScaleU];
 #pragma unroll
-    for (int u = 0; u < kScaleU; ++u) raw[u] = *reinterpret_cast<gptr<const uint4>>(glob(base + u * 64 * V));
+    for (int u = 0; u < kScaleU; ++u) {
+      if constexpr (NT) raw[u] = nt_ld16(base + u * 64 * V);
+      else raw[u] = *reinterpret_cast<gptr<const uint4>>(glob(base + u * 64 * V));
+    }
 #pragma unroll
     for (int u = 0; u < kScaleU; ++u) {
       T* e = reinterpret_cast<T*>(&raw[u]);
 #pragma unroll
       for (int j = 0; j < V; ++j) e[j] = from_f32<T>(op(to_f32<T>(e[j])));
-      *reinterpret_cast<gptr<uint4>>(glob(base + u * 64 * V)) = raw[u];
+      if constexpr (NT) nt_st16(base + u * 64 * V, raw[u]);
+      else *reinterpret_cast<gptr<uint4>>(glob(base + u * 64 * V)) = raw[u];
     }
   }
   if (blockIdx.x == 0) {
@@ -798,6 +804,12 @@ DqTune& dq_tune() {
   return t;
 }
 
+// zs_scale's cache policy: -1 by size (kScaleNtBytes), 0 default policy, 1 non-temporal
+int& scale_nt_mode() {
+  static int mode = -1;
+  return mode;
+}
+
 int dq_grid(int64_t rows) {
   int64_t cap = grid_cap();
   const int per_cu = dq_tune().wg_per_cu;
@@ -1028,12 +1040,16 @@ int zs_scale(void* x, int64_t n, int dtype, double div, uintptr_t stream) {
   const int64_t blocks = std::max<int64_t>(1, (n / span + 3) / 4);
   const int grid = int(std::min<int64_t>(blocks, grid_cap()));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (dtype == ZS_F32)
-    hipLaunchKernelGGL(scale_kernel<float>, dim3(grid), dim3(kThreads), 0, st,
-                       static_cast<float*>(x), n, fdiv, inv, pow2);
-  else
-    hipLaunchKernelGGL(scale_kernel<unsigned short>, dim3(grid), dim3(kThreads), 0, st,
-                       static_cast<unsigned short*>(x), n, fdiv, inv, pow2);
+  const int force = scale_nt_mode();
+  const bool nt = force < 0 ? n * (dtype == ZS_F32 ? 4 : 2) > kScaleNtBytes : force == 1;
+#define ZS_SCALE(T, NT) hipLaunchKernelGGL((scale_kernel<T, NT>), dim3(grid), dim3(kThreads), 0, st, \
+                                           static_cast<T*>(x), n, fdiv, inv, pow2)
+  if (dtype == ZS_F32) {
+    if (nt) ZS_SCALE(float, true); else ZS_SCALE(float, false);
+  } else {
+    if (nt) ZS_SCALE(unsigned short, true); else ZS_SCALE(unsigned short, false);
+  }
+#undef ZS_SCALE
   ZS_HIP(hipGetLastError());
   return ZS_OK;
 }
@@ -1502,6 +1518,9 @@ int zs_tune(const char* key, int64_t value, int64_t* previous) {
   } else if (std::strcmp(key, "dq_wg_per_cu") == 0) {
     slot = &dq_tune().wg_per_cu;
     ok = value >= 0 && value <= 128;
+  } else if (std::strcmp(key, "scale_nt") == 0) {
+    slot = &scale_nt_mode();
+    ok = value >= -1 && value <= 1;
   } else {
     return zs::fail(ZS_ERR_INVALID, "zs_tune: unknown key '%s'", key);
   }

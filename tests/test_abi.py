@@ -266,3 +266,23 @@ def test_device_alloc_validates_without_gpu():
     assert lib.zs_device_alloc(-5, ctypes.byref(out)) == _lib.ZS_ERR_INVALID
     assert lib.zs_device_alloc(64, None) == _lib.ZS_ERR_INVALID
     assert lib.zs_device_free(None) == _lib.ZS_OK
+
+
+def test_tune_knobs_validate_and_restore():
+    """zs_tune (diagnostic A/B knobs): known keys take their documented ranges and report the old
+    value; unknown keys and out-of-range values are rejected; nothing touches the GPU."""
+    from zero_amd import _lib
+
+    lib = _lib.lib
+    prev = ctypes.c_int64(99)
+    for key, good, bad, default in ((b"dq_unroll", 8, 5, 4), (b"dq_nt_store", 0, 2, 1),
+                                    (b"dq_wg_per_cu", 8, 129, 0), (b"scale_nt", 1, 2, -1)):
+        assert lib.zs_tune(key, good, ctypes.byref(prev)) == _lib.ZS_OK
+        assert prev.value == default
+        assert lib.zs_tune(key, bad, None) == _lib.ZS_ERR_INVALID
+        assert b"out of range" in lib.zs_last_error()
+        assert lib.zs_tune(key, default, ctypes.byref(prev)) == _lib.ZS_OK
+        assert prev.value == good
+    assert lib.zs_tune(b"no_such_knob", 1, None) == _lib.ZS_ERR_INVALID
+    assert b"unknown key" in lib.zs_last_error()
+    assert lib.zs_tune(None, 1, None) == _lib.ZS_ERR_INVALID

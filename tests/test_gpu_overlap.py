@@ -352,7 +352,8 @@ def test_ddp_sync_gradients(gpu, ws):
 # (a wave step of the vector path covers 1024 fp32 / 2048 bf16 elements; the rest is the tail)
 @pytest.mark.parametrize("n", [1, 7, 1000, 1024, 2051, 4099, 5 * 2048 + 1000, 1 << 20])
 @pytest.mark.parametrize("div", [2.0, 3.0, 8.0, 6.0])
-def test_scale_kernel_bit_exact(gpu, n, div):
+@pytest.mark.parametrize("nt", [-1, 1])  # cache policy by size (here: default) / forced non-temporal
+def test_scale_kernel_bit_exact(gpu, n, div, nt):
     from zero_amd import _lib
     from zero_amd.comm import zs_dtype
 
@@ -360,8 +361,13 @@ def test_scale_kernel_bit_exact(gpu, n, div):
     x = torch.randn(n, generator=g) * 10
     for dt in (torch.float32, torch.bfloat16):
         d = x.to(dt).to(gpu)
-        _lib.call("zs_scale", d.data_ptr(), n, zs_dtype(dt), div, torch.cuda.current_stream().cuda_stream)
-        torch.cuda.synchronize()
+        _lib.call("zs_tune", b"scale_nt", nt, None)
+        try:
+            _lib.call("zs_scale", d.data_ptr(), n, zs_dtype(dt), div,
+                      torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+        finally:
+            _lib.call("zs_tune", b"scale_nt", -1, None)
         if dt == torch.float32:
             want = x.numpy() / np.float32(div)
             assert np.array_equal(d.cpu().numpy(), want)

@@ -1,0 +1,99 @@
+"""In-process A/B of zs_scale's cache policy (zs_tune "scale_nt": 0 default policy, 1 non-temporal
+loads and stores) over buffer sizes either side of the 256 MB MALL, interleaved so placement and
+clock drift hit both alike.  Every buffer is a placed one (probed_zeros), and the in-place float4
+copy over the same buffer is timed beside them (this memory's streaming ceiling).  Both policies
+must give the same bits.
+
+Usage: python tools/scale_ab.py [--iters 20] [--blocks 4] [--out FILE]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO / "distributed-training-sandbox_amd"))
+
+SIZES_MIB = (64, 256, 1024, 4096)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--blocks", type=int, default=4)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+
+    import torch
+
+    from zero_amd import _lib
+    from zero_amd.engine import probed_zeros
+    from zero_amd.kernels import CopySet, stream_handle
+
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream(dev)
+    h = stream_handle(st)
+    nbytes = max(SIZES_MIB) << 20
+    buf, _ = probed_zeros(nbytes // 4, torch.float32, dev)
+    g = torch.Generator(device=dev).manual_seed(0)
+    buf.normal_(generator=g)
+    base = buf.clone()
+
+    def tune(v):
+        _lib.call("zs_tune", b"scale_nt", v, None)
+
+    def run(t, n):
+        _lib.call("zs_scale", t.data_ptr(), n, _lib.ZS_F32 if t.dtype == torch.float32 else _lib.ZS_BF16,
+                  3.0, h)
+
+    def timed(fn):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(args.iters):
+            fn()
+        e1.record(st)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / args.iters
+
+    # same bits under both policies (one scale of a fresh copy each)
+    for dt in (torch.float32, torch.bfloat16):
+        outs = []
+        for v in (0, 1):
+            tune(v)
+            buf.copy_(base)
+            t = buf.view(torch.uint8)[: 64 << 20].view(dt)
+            run(t, t.numel())
+            torch.cuda.synchronize()
+            outs.append(t.view(torch.int16 if dt == torch.bfloat16 else torch.int32).clone())
+        assert torch.equal(outs[0], outs[1]), ("bits differ", dt)
+    res = {}
+    for b in range(args.blocks):
+        for mib in SIZES_MIB:
+            nb = mib << 20
+            raw = buf.view(torch.uint8)[:nb]
+            for dt in (torch.float32, torch.bfloat16):
+                t = raw.view(dt)
+                for v in ((0, 1) if b % 2 == 0 else (1, 0)):
+                    tune(v)
+                    ms = timed(lambda: run(t, t.numel()))
+                    res.setdefault(f"{mib} MiB {str(dt)[6:]} nt{v}", []).append(ms)
+            cp = CopySet([raw.data_ptr()], [raw.data_ptr()], [nb])
+            res.setdefault(f"{mib} MiB copy in place", []).append(timed(lambda: cp.run(st)))
+    tune(-1)
+    rows = []
+    for k, v in res.items():
+        ms = sorted(v)[len(v) // 2]
+        nb = int(k.split()[0]) << 20
+        gbs = 2 * nb / (ms / 1e3) / 1e9
+        rows.append({"variant": k, "median_ms": ms, "gbs": gbs, "frac": gbs / 8000.0, "ms_blocks": v})
+        print(json.dumps({kk: (round(x, 4) if isinstance(x, float) else x) for kk, x in rows[-1].items()
+                          if kk != "ms_blocks"}), flush=True)
+    if args.out:
+        Path(args.out).write_text(json.dumps({"iters": args.iters, "rows": rows}, indent=1) + "\n")
+
+
+if __name__ == "__main__":
+    main()
