@@ -85,6 +85,31 @@ __device__ __forceinline__ void nt_st8(void* p, uint2 x) {
   const u32x2 v = {x.x, x.y};
   __builtin_nontemporal_store(v, (gptr<u32x2>)p);
 }
+// the same accesses with the cache policy chosen at compile time (NT: non-temporal hint)
+template <bool NT>
+__device__ __forceinline__ uint4 ld16(const void* p) {
+  if constexpr (NT) return nt_ld16(p);
+  else return *(gptr<const uint4>)p;
+}
+template <bool NT>
+__device__ __forceinline__ void st16(void* p, uint4 x) {
+  if constexpr (NT) nt_st16(p, x);
+  else *(gptr<uint4>)p = x;
+}
+template <bool NT>
+__device__ __forceinline__ uint2 ld8(const void* p) {
+  if constexpr (NT) return nt_ld8(p);
+  else return *(gptr<const uint2>)p;
+}
+template <bool NT>
+__device__ __forceinline__ void st8(void* p, uint2 x) {
+  if constexpr (NT) nt_st8(p, x);
+  else *(gptr<uint2>)p = x;
+}
+// Above this many bytes a buffer cannot sit in the 256 MB MALL (Infinity Cache): the in-place scale
+// and the conversions take the non-temporal policy there and the default policy below, where the
+// buffer was usually just written (an all-reduce, a backward) and is read next (the collective).
+constexpr int64_t kMallBytes = int64_t(256) << 20;
 
 // ----------------------------------------------------------------------------------------------
 // segment copy
@@ -365,12 +390,11 @@ __device__ __forceinline__ T from_f32(float x) {
 // grid-stride over wave steps; the tail (n % elements per step) by block 0.  Cache policy by size
 // (NT): a DDP bucket (64 MiB) is scaled right after the all-reduce wrote it, while it is still in
 // the 256 MB MALL — default policy; a buffer larger than the MALL cannot be there, so its loads
-// and stores carry the non-temporal hint (kScaleNtBytes; `zs_tune("scale_nt")` forces either).
+// and stores carry the non-temporal hint (kMallBytes; `zs_tune("scale_nt")` forces either).
 // (Round 2's one access in flight per lane measured 0.61 of 8 TB/s on a 4 GiB buffer.)
 // fp32: IEEE division (x / div), or an exact reciprocal multiply when div is a power of two;
 // bf16: the same in fp32, rounded to bf16 (RNE) — torch's div_ on a bf16 tensor.
 constexpr int kScaleU = 4;
-constexpr int64_t kScaleNtBytes = int64_t(256) << 20;
 
 template <typename T, bool NT>
 __global__ __launch_bounds__(kThreads) void scale_kernel(T* __restrict__ x, int64_t n, float div,
@@ -388,17 +412,13 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(T* __restrict__ x, int6
     T* base = x + w * kSpan + int64_t(lane) * V;
     uint4 raw[kScaleU];
 #pragma unroll
-    for (int u = 0; u < kScaleU; ++u) {
-      if constexpr (NT) raw[u] = nt_ld16(base + u * 64 * V);
-      else raw[u] = *reinterpret_cast<gptr<const uint4>>(glob(base + u * 64 * V));
-    }
+    for (int u = 0; u < kScaleU; ++u) raw[u] = ld16<NT>(base + u * 64 * V);
 #pragma unroll
     for (int u = 0; u < kScaleU; ++u) {
       T* e = reinterpret_cast<T*>(&raw[u]);
 #pragma unroll
       for (int j = 0; j < V; ++j) e[j] = from_f32<T>(op(to_f32<T>(e[j])));
-      if constexpr (NT) nt_st16(base + u * 64 * V, raw[u]);
-      else *reinterpret_cast<gptr<uint4>>(glob(base + u * 64 * V)) = raw[u];
+      st16<NT>(base + u * 64 * V, raw[u]);
     }
   }
   if (blockIdx.x == 0) {
@@ -415,13 +435,15 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(T* __restrict__ x, int6
 // block, so every wave instruction touches one contiguous 1 KiB (fp32) or 512 B (bf16) span.
 // (Round 2's lane-contiguous 8 elements per lane gave each fp32 instruction a 32-B lane stride —
 // half-dense — and measured 0.58 of 8 TB/s bf16 -> fp32, profiles/r03_kernels_table.json.)
-// All kConvU loads are issued before the first store; non-temporal (each byte is touched once);
-// grid-stride over wave steps; the n % kConvSpan tail by block 0.
+// All kConvU loads are issued before the first store; grid-stride over wave steps; the n % kConvSpan
+// tail by block 0.  Cache policy by size (NT), as zs_scale: non-temporal when the fp32 side is
+// larger than the MALL, the default policy below (a bucket's grads just written by backward, the
+// bf16 bucket read next by the collective); `zs_tune("convert_nt")` forces either.
 // fp32 -> bf16 rounds to nearest even (v_cvt_pk_bf16_f32), NaN stays NaN; bf16 -> fp32 is exact.
 constexpr int kConvU = 4;
 constexpr int64_t kConvSpan = 256 * kConvU;
 
-template <bool TO_BF16>
+template <bool TO_BF16, bool NT>
 __global__ __launch_bounds__(kThreads) void convert_kernel(const void* __restrict__ src,
                                                            void* __restrict__ dst, int64_t n) {
   const int64_t steps = n / kConvSpan;
@@ -434,26 +456,28 @@ __global__ __launch_bounds__(kThreads) void convert_kernel(const void* __restric
       const float* s = static_cast<const float*>(src) + base;
       float4 a[kConvU];
 #pragma unroll
-      for (int u = 0; u < kConvU; ++u) a[u] = ld4(s, 256 * u);
+      for (int u = 0; u < kConvU; ++u) {
+        const uint4 r = ld16<NT>(s + 256 * u);
+        a[u] = make_float4(__uint_as_float(r.x), __uint_as_float(r.y), __uint_as_float(r.z),
+                           __uint_as_float(r.w));
+      }
       unsigned short* d = static_cast<unsigned short*>(dst) + base;
 #pragma unroll
       for (int u = 0; u < kConvU; ++u) {
         const uint32_t lo = uint32_t(f32_to_bf16(a[u].x)) | (uint32_t(f32_to_bf16(a[u].y)) << 16);
         const uint32_t hi = uint32_t(f32_to_bf16(a[u].z)) | (uint32_t(f32_to_bf16(a[u].w)) << 16);
-        nt_st8(d + 256 * u, make_uint2(lo, hi));
+        st8<NT>(d + 256 * u, make_uint2(lo, hi));
       }
     } else {
       const unsigned short* s = static_cast<const unsigned short*>(src) + base;
       uint2 h[kConvU];
 #pragma unroll
-      for (int u = 0; u < kConvU; ++u) h[u] = nt_ld8(s + 256 * u);
+      for (int u = 0; u < kConvU; ++u) h[u] = ld8<NT>(s + 256 * u);
       float* d = static_cast<float*>(dst) + base;
 #pragma unroll
       for (int u = 0; u < kConvU; ++u)
-        st4(d, 256 * u, make_float4(__uint_as_float(h[u].x << 16),
-                                    __uint_as_float(h[u].x & 0xffff0000u),
-                                    __uint_as_float(h[u].y << 16),
-                                    __uint_as_float(h[u].y & 0xffff0000u)));
+        st16<NT>(d + 256 * u, make_uint4(h[u].x << 16, h[u].x & 0xffff0000u, h[u].y << 16,
+                                         h[u].y & 0xffff0000u));
     }
   }
   if (blockIdx.x == 0) {
@@ -804,8 +828,12 @@ DqTune& dq_tune() {
   return t;
 }
 
-// zs_scale's cache policy: -1 by size (kScaleNtBytes), 0 default policy, 1 non-temporal
+// zs_scale's / zs_convert's cache policy: -1 by size (kMallBytes), 0 default policy, 1 non-temporal
 int& scale_nt_mode() {
+  static int mode = -1;
+  return mode;
+}
+int& convert_nt_mode() {
   static int mode = -1;
   return mode;
 }
@@ -1041,7 +1069,7 @@ int zs_scale(void* x, int64_t n, int dtype, double div, uintptr_t stream) {
   const int grid = int(std::min<int64_t>(blocks, grid_cap()));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int force = scale_nt_mode();
-  const bool nt = force < 0 ? n * (dtype == ZS_F32 ? 4 : 2) > kScaleNtBytes : force == 1;
+  const bool nt = force < 0 ? n * (dtype == ZS_F32 ? 4 : 2) > kMallBytes : force == 1;
 #define ZS_SCALE(T, NT) hipLaunchKernelGGL((scale_kernel<T, NT>), dim3(grid), dim3(kThreads), 0, st, \
                                            static_cast<T*>(x), n, fdiv, inv, pow2)
   if (dtype == ZS_F32) {
@@ -1069,8 +1097,15 @@ int zs_convert(const void* src, int src_dtype, void* dst, int dst_dtype, int64_t
   const int grid = int(std::min<int64_t>(work, grid_cap()));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (vec) {
-    if (to_bf16) hipLaunchKernelGGL(convert_kernel<true>, dim3(grid), dim3(kThreads), 0, st, src, dst, n);
-    else hipLaunchKernelGGL(convert_kernel<false>, dim3(grid), dim3(kThreads), 0, st, src, dst, n);
+    const int force = convert_nt_mode();
+    const bool nt = force < 0 ? n * 4 > kMallBytes : force == 1;  // by the fp32 side's bytes
+#define ZS_CONV(B, NT) hipLaunchKernelGGL((convert_kernel<B, NT>), dim3(grid), dim3(kThreads), 0, st, src, dst, n)
+    if (to_bf16) {
+      if (nt) ZS_CONV(true, true); else ZS_CONV(true, false);
+    } else {
+      if (nt) ZS_CONV(false, true); else ZS_CONV(false, false);
+    }
+#undef ZS_CONV
   } else {
     if (to_bf16) hipLaunchKernelGGL(convert_scalar_kernel<true>, dim3(grid), dim3(kThreads), 0, st, src, dst, n);
     else hipLaunchKernelGGL(convert_scalar_kernel<false>, dim3(grid), dim3(kThreads), 0, st, src, dst, n);
@@ -1520,6 +1555,9 @@ int zs_tune(const char* key, int64_t value, int64_t* previous) {
     ok = value >= 0 && value <= 128;
   } else if (std::strcmp(key, "scale_nt") == 0) {
     slot = &scale_nt_mode();
+    ok = value >= -1 && value <= 1;
+  } else if (std::strcmp(key, "convert_nt") == 0) {
+    slot = &convert_nt_mode();
     ok = value >= -1 && value <= 1;
   } else {
     return zs::fail(ZS_ERR_INVALID, "zs_tune: unknown key '%s'", key);

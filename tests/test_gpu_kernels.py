@@ -393,13 +393,24 @@ def test_pack_unpack_through_plan_bit_exact(gpu, dtype):
 
 
 @pytest.mark.parametrize("n", [1, 7, 8, 1000, 1024, 1025, 4099, 3 * 1024 + 517, 1 << 20])
-@pytest.mark.parametrize("offset", [0, 1])
-def test_convert_fp32_bf16_bit_exact(gpu, n, offset):
+@pytest.mark.parametrize("offset,nt", [(0, -1), (0, 1), (1, -1)])
+def test_convert_fp32_bf16_bit_exact(gpu, n, offset, nt):
     """zs_convert fp32 → bf16 is round-to-nearest-even bit for bit (numpy restatement), including
     ties, subnormals, the overflow edge and infinities; NaN stays NaN; bf16 → fp32 is exact.
-    offset 1 makes the buffers unaligned (scalar path)."""
+    offset 1 makes the buffers unaligned (scalar path); nt 1 forces the vector path's non-temporal
+    policy (by size, these buffers take the default one)."""
     from oracle import zero_oracle as zo
+    from zero_amd import _lib
     from zero_amd.kernels import convert
+
+    _lib.call("zs_tune", b"convert_nt", nt, None)
+    try:
+        _convert_case(gpu, n, offset, zo, convert)
+    finally:
+        _lib.call("zs_tune", b"convert_nt", -1, None)
+
+
+def _convert_case(gpu, n, offset, zo, convert):
 
     rng = np.random.default_rng(n + offset)
     x = (rng.standard_normal(n + offset) * 10.0 ** rng.integers(-40, 39, n + offset)).astype(np.float32)

@@ -1,8 +1,8 @@
-"""In-process A/B of zs_scale's cache policy (zs_tune "scale_nt": 0 default policy, 1 non-temporal
-loads and stores) over buffer sizes either side of the 256 MB MALL, interleaved so placement and
-clock drift hit both alike.  Every buffer is a placed one (probed_zeros), and the in-place float4
-copy over the same buffer is timed beside them (this memory's streaming ceiling).  Both policies
-must give the same bits.
+"""In-process A/B of the cache policy of zs_scale and zs_convert (zs_tune "scale_nt" /
+"convert_nt": 0 default policy, 1 non-temporal loads and stores) over buffer sizes either side of
+the 256 MB MALL, interleaved so placement and clock drift hit both alike.  Every buffer is a placed
+one (probed_zeros), and the in-place float4 copy over the same buffer is timed beside them (this
+memory's streaming ceiling).  Both policies must give the same bits.
 
 Usage: python tools/scale_ab.py [--iters 20] [--blocks 4] [--out FILE]
 """
@@ -37,12 +37,18 @@ def main():
     h = stream_handle(st)
     nbytes = max(SIZES_MIB) << 20
     buf, _ = probed_zeros(nbytes // 4, torch.float32, dev)
+    half, _ = probed_zeros(nbytes // 4, torch.bfloat16, dev)  # the bf16 side of the conversions
     g = torch.Generator(device=dev).manual_seed(0)
     buf.normal_(generator=g)
     base = buf.clone()
 
-    def tune(v):
-        _lib.call("zs_tune", b"scale_nt", v, None)
+    def tune(v, key=b"scale_nt"):
+        _lib.call("zs_tune", key, v, None)
+
+    def conv(src, dst):
+        _lib.call("zs_convert", src.data_ptr(), _lib.ZS_F32 if src.dtype == torch.float32 else _lib.ZS_BF16,
+                  dst.data_ptr(), _lib.ZS_F32 if dst.dtype == torch.float32 else _lib.ZS_BF16,
+                  src.numel(), h)
 
     def run(t, n):
         _lib.call("zs_scale", t.data_ptr(), n, _lib.ZS_F32 if t.dtype == torch.float32 else _lib.ZS_BF16,
@@ -69,6 +75,12 @@ def main():
             torch.cuda.synchronize()
             outs.append(t.view(torch.int16 if dt == torch.bfloat16 else torch.int32).clone())
         assert torch.equal(outs[0], outs[1]), ("bits differ", dt)
+    for v in (0, 1):
+        tune(v, b"convert_nt")
+        conv(base[: 16 << 20], half[: 16 << 20])
+        torch.cuda.synchronize()
+        outs.append(half[: 16 << 20].view(torch.int16).clone())
+    assert torch.equal(outs[-2], outs[-1]), "convert bits differ"
     res = {}
     for b in range(args.blocks):
         for mib in SIZES_MIB:
@@ -82,12 +94,20 @@ def main():
                     res.setdefault(f"{mib} MiB {str(dt)[6:]} nt{v}", []).append(ms)
             cp = CopySet([raw.data_ptr()], [raw.data_ptr()], [nb])
             res.setdefault(f"{mib} MiB copy in place", []).append(timed(lambda: cp.run(st)))
+            f32, b16 = raw.view(torch.float32), half[: nb // 4]
+            for name, a, c in (("convert f32->bf16", f32, b16), ("convert bf16->f32", b16, f32)):
+                for v in ((0, 1) if b % 2 == 0 else (1, 0)):
+                    tune(v, b"convert_nt")
+                    ms = timed(lambda: conv(a, c))
+                    res.setdefault(f"{mib} MiB {name} nt{v}", []).append(ms)
     tune(-1)
+    tune(-1, b"convert_nt")
     rows = []
     for k, v in res.items():
         ms = sorted(v)[len(v) // 2]
         nb = int(k.split()[0]) << 20
-        gbs = 2 * nb / (ms / 1e3) / 1e9
+        moved = 1.5 * nb if "convert" in k else 2 * nb  # convert: the fp32 side + the bf16 side
+        gbs = moved / (ms / 1e3) / 1e9
         rows.append({"variant": k, "median_ms": ms, "gbs": gbs, "frac": gbs / 8000.0, "ms_blocks": v})
         print(json.dumps({kk: (round(x, 4) if isinstance(x, float) else x) for kk, x in rows[-1].items()
                           if kk != "ms_blocks"}), flush=True)
