@@ -436,9 +436,12 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(T* __restrict__ x, int6
 // (Round 2's lane-contiguous 8 elements per lane gave each fp32 instruction a 32-B lane stride —
 // half-dense — and measured 0.58 of 8 TB/s bf16 -> fp32, profiles/r03_kernels_table.json.)
 // All kConvU loads are issued before the first store; grid-stride over wave steps; the n % kConvSpan
-// tail by block 0.  Cache policy by size (NT), as zs_scale: non-temporal when the fp32 side is
-// larger than the MALL, the default policy below (a bucket's grads just written by backward, the
-// bf16 bucket read next by the collective); `zs_tune("convert_nt")` forces either.
+// tail by block 0.  Cache policy by size (NT), as zs_scale: non-temporal when source and destination
+// together are larger than the MALL, the default policy below (a bucket's grads just written by
+// backward, the bf16 bucket read next by the collective); `zs_tune("convert_nt")` forces either.
+// Round 4 A/B on placed buffers (profiles/r04_policy_ab.json): 64 MiB fp32 side, bf16 -> fp32 0.80
+// default vs 0.72 non-temporal (fp32 -> bf16 0.83 / 0.85); 256 MiB and above non-temporal wins
+// (0.84 / 0.74 fp32 -> bf16, 0.75 / 0.72 bf16 -> fp32).
 // fp32 -> bf16 rounds to nearest even (v_cvt_pk_bf16_f32), NaN stays NaN; bf16 -> fp32 is exact.
 constexpr int kConvU = 4;
 constexpr int64_t kConvSpan = 256 * kConvU;
@@ -1098,7 +1101,7 @@ int zs_convert(const void* src, int src_dtype, void* dst, int dst_dtype, int64_t
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (vec) {
     const int force = convert_nt_mode();
-    const bool nt = force < 0 ? n * 4 > kMallBytes : force == 1;  // by the fp32 side's bytes
+    const bool nt = force < 0 ? n * 6 > kMallBytes : force == 1;  // by both sides' bytes
 #define ZS_CONV(B, NT) hipLaunchKernelGGL((convert_kernel<B, NT>), dim3(grid), dim3(kThreads), 0, st, src, dst, n)
     if (to_bf16) {
       if (nt) ZS_CONV(true, true); else ZS_CONV(true, false);
