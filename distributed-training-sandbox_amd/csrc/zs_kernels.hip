@@ -121,7 +121,10 @@ struct CopySeg {
   int64_t vec;  // 1 if src and dst are 16-byte aligned (or src is null and dst aligned)
 };
 
-template <int U>
+// Cache policy by size (NT) as zs_scale / zs_convert: non-temporal when the set moves more than the
+// MALL holds (a C4 pack group, a checkpoint), the default policy below (a 64 MB overlap bucket, read
+// next by its collective); `zs_tune("copy_nt")` forces either.
+template <int U, bool NT>
 __global__ __launch_bounds__(kThreads) void copy_segments_kernel(
     const CopySeg* __restrict__ segs, const int64_t* __restrict__ chunk_prefix, int64_t nseg,
     int64_t total_chunks) {
@@ -140,13 +143,13 @@ __global__ __launch_bounds__(kThreads) void copy_segments_kernel(
       for (int u = 0; u < U; ++u) {  // all loads first: U x 16 B in flight per lane
         const int64_t off = b0 + (int64_t(u) * kThreads + threadIdx.x) * 16;
         val[u] = make_uint4(0, 0, 0, 0);
-        if (src && off + 16 <= b1) val[u] = nt_ld16(s.src + off);
+        if (src && off + 16 <= b1) val[u] = ld16<NT>(s.src + off);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t off = b0 + (int64_t(u) * kThreads + threadIdx.x) * 16;
         if (off + 16 <= b1) {
-          nt_st16(s.dst + off, val[u]);
+          st16<NT>(s.dst + off, val[u]);
         } else if (off < b1) {
           for (int64_t b = off; b < b1; ++b) dst[b] = src ? src[b] : 0;
         }
@@ -831,12 +834,17 @@ DqTune& dq_tune() {
   return t;
 }
 
-// zs_scale's / zs_convert's cache policy: -1 by size (kMallBytes), 0 default policy, 1 non-temporal
+// zs_scale's / zs_convert's / zs_copyset_run's cache policy: -1 by size (kMallBytes), 0 default
+// policy, 1 non-temporal
 int& scale_nt_mode() {
   static int mode = -1;
   return mode;
 }
 int& convert_nt_mode() {
+  static int mode = -1;
+  return mode;
+}
+int& copy_nt_mode() {
   static int mode = -1;
   return mode;
 }
@@ -871,6 +879,7 @@ struct zs_copyset {
   CopySeg* d_segs = nullptr;
   int64_t* d_prefix = nullptr;
   int64_t nseg = 0, total_chunks = 0;
+  int64_t bytes = 0;                // copied per run (read + write: 2x this)
   int unroll = kCopyUnrollDefault;  // 16-B accesses in flight per lane (chunk = 4 KiB * unroll)
 };
 
@@ -1002,6 +1011,7 @@ int zs_copyset_create(const uint64_t* src, const uint64_t* dst, const int64_t* n
   ZS_REQUIRE(n == 0 || (src && dst && nbytes), "zs_copyset_create: NULL table");
   std::vector<CopySeg> segs;
   std::vector<int64_t> prefix(1, 0);
+  int64_t bytes = 0;
   const int unroll = copy_unroll();
   const int64_t chunk = copy_chunk_bytes(unroll);
   for (int64_t i = 0; i < n; ++i) {
@@ -1014,12 +1024,14 @@ int zs_copyset_create(const uint64_t* src, const uint64_t* dst, const int64_t* n
     s.nbytes = nbytes[i];
     s.vec = aligned(src[i], 16) && aligned(dst[i], 16) ? 1 : 0;
     segs.push_back(s);
+    bytes += nbytes[i];
     prefix.push_back(prefix.back() + (nbytes[i] + chunk - 1) / chunk);
   }
   zs_copyset* cs = new (std::nothrow) zs_copyset();
   if (!cs) return zs::fail(ZS_ERR_NOMEM, "zs_copyset_create: out of memory");
   cs->nseg = int64_t(segs.size());
   cs->total_chunks = prefix.back();
+  cs->bytes = bytes;
   cs->unroll = unroll;
   int rc = upload(segs, &cs->d_segs);
   if (rc == ZS_OK) rc = upload(prefix, &cs->d_prefix);
@@ -1036,15 +1048,16 @@ int zs_copyset_run(const zs_copyset* cs, uintptr_t stream) {
   if (cs->total_chunks == 0) return ZS_OK;
   const int grid = int(std::min<int64_t>(cs->total_chunks, grid_cap()));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (cs->unroll == 8)
-    hipLaunchKernelGGL(copy_segments_kernel<8>, dim3(grid), dim3(kThreads), 0, st, cs->d_segs,
-                       cs->d_prefix, cs->nseg, cs->total_chunks);
-  else if (cs->unroll == 2)
-    hipLaunchKernelGGL(copy_segments_kernel<2>, dim3(grid), dim3(kThreads), 0, st, cs->d_segs,
-                       cs->d_prefix, cs->nseg, cs->total_chunks);
-  else
-    hipLaunchKernelGGL(copy_segments_kernel<4>, dim3(grid), dim3(kThreads), 0, st, cs->d_segs,
-                       cs->d_prefix, cs->nseg, cs->total_chunks);
+  const int force = copy_nt_mode();
+  const bool nt = force < 0 ? 2 * cs->bytes > kMallBytes : force == 1;
+#define ZS_COPY(U, NT) hipLaunchKernelGGL((copy_segments_kernel<U, NT>), dim3(grid), dim3(kThreads), 0, st, \
+                                          cs->d_segs, cs->d_prefix, cs->nseg, cs->total_chunks)
+  if (nt) {
+    switch (cs->unroll) { case 8: ZS_COPY(8, true); break; case 2: ZS_COPY(2, true); break; default: ZS_COPY(4, true); }
+  } else {
+    switch (cs->unroll) { case 8: ZS_COPY(8, false); break; case 2: ZS_COPY(2, false); break; default: ZS_COPY(4, false); }
+  }
+#undef ZS_COPY
   ZS_HIP(hipGetLastError());
   return ZS_OK;
 }
@@ -1561,6 +1574,9 @@ int zs_tune(const char* key, int64_t value, int64_t* previous) {
     ok = value >= -1 && value <= 1;
   } else if (std::strcmp(key, "convert_nt") == 0) {
     slot = &convert_nt_mode();
+    ok = value >= -1 && value <= 1;
+  } else if (std::strcmp(key, "copy_nt") == 0) {
+    slot = &copy_nt_mode();
     ok = value >= -1 && value <= 1;
   } else {
     return zs::fail(ZS_ERR_INVALID, "zs_tune: unknown key '%s'", key);

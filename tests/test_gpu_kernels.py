@@ -14,7 +14,18 @@ def _seed(n):
     return np.random.default_rng(n)
 
 
-def test_copy_segments_bit_exact(gpu):
+@pytest.mark.parametrize("nt", [-1, 1])  # cache policy by size (here: default) / non-temporal
+def test_copy_segments_bit_exact(gpu, nt):
+    from zero_amd import _lib
+
+    _lib.call("zs_tune", b"copy_nt", nt, None)
+    try:
+        _copy_case(gpu)
+    finally:
+        _lib.call("zs_tune", b"copy_nt", -1, None)
+
+
+def _copy_case(gpu):
     from zero_amd.kernels import CopySet
 
     rng = _seed(1)

@@ -1,5 +1,5 @@
-"""In-process A/B of the cache policy of zs_scale and zs_convert (zs_tune "scale_nt" /
-"convert_nt": 0 default policy, 1 non-temporal loads and stores) over buffer sizes either side of
+"""In-process A/B of the cache policy of zs_scale, zs_convert and the segment copy (zs_tune
+"scale_nt" / "convert_nt" / "copy_nt": 0 default policy, 1 non-temporal loads and stores) over buffer sizes either side of
 the 256 MB MALL, interleaved so placement and clock drift hit both alike.  Every buffer is a placed
 one (probed_zeros), and the in-place float4 copy over the same buffer is timed beside them (this
 memory's streaming ceiling).  Both policies must give the same bits.
@@ -93,7 +93,15 @@ def main():
                     ms = timed(lambda: run(t, t.numel()))
                     res.setdefault(f"{mib} MiB {str(dt)[6:]} nt{v}", []).append(ms)
             cp = CopySet([raw.data_ptr()], [raw.data_ptr()], [nb])
+            tune(1, b"copy_nt")  # the ceiling reference: the policy every earlier table used
             res.setdefault(f"{mib} MiB copy in place", []).append(timed(lambda: cp.run(st)))
+            # a pack-shaped copy: half of it from the fp32 buffer into the other buffer
+            pk = CopySet([raw.data_ptr()], [half.data_ptr()], [nb // 2])
+            for v in ((0, 1) if b % 2 == 0 else (1, 0)):
+                tune(v, b"copy_nt")
+                ms = timed(lambda: pk.run(st))
+                res.setdefault(f"{mib} MiB copy (half) to another buffer nt{v}", []).append(ms)
+            tune(-1, b"copy_nt")
             f32, b16 = raw.view(torch.float32), half[: nb // 4]
             for name, a, c in (("convert f32->bf16", f32, b16), ("convert bf16->f32", b16, f32)):
                 for v in ((0, 1) if b % 2 == 0 else (1, 0)):
@@ -106,7 +114,8 @@ def main():
     for k, v in res.items():
         ms = sorted(v)[len(v) // 2]
         nb = int(k.split()[0]) << 20
-        moved = 1.5 * nb if "convert" in k else 2 * nb  # convert: the fp32 side + the bf16 side
+        # convert: the fp32 side + the bf16 side; the half copy: nb / 2 read + nb / 2 written
+        moved = 1.5 * nb if "convert" in k else (nb if "(half)" in k else 2 * nb)
         gbs = moved / (ms / 1e3) / 1e9
         rows.append({"variant": k, "median_ms": ms, "gbs": gbs, "frac": gbs / 8000.0, "ms_blocks": v})
         print(json.dumps({kk: (round(x, 4) if isinstance(x, float) else x) for kk, x in rows[-1].items()
