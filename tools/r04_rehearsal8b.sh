@@ -1,6 +1,8 @@
 #!/bin/bash
-# round 4: more of the N = 8 lines at full size on the ONE GPU through real RCCL (--share-gpu):
-# C5 ZeRO-3 (configs[4], all 32 layers) single-stream, and C4 ZeRO-1
+# round 4: more of the N > 1 lines at full size on the ONE GPU through real RCCL (--share-gpu):
+# C5 ZeRO-3 (configs[4], all 32 layers) at N = 4 — at N = 8 the eight ranks' resident synthetic
+# full-size grads (16 GB each) and state do not fit one card (HIP OOM, gpurun_out/r04r8b first run)
+# — and C4 ZeRO-1 at N = 8
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(pwd)}"; O="$R/gpurun_out/r04r8b"; mkdir -p "$O"
 export TMPDIR=/tmp
@@ -12,6 +14,6 @@ run() {
   echo "== $tag rc=$rc"; tail -1 "$O/$tag.json" | cut -c1-250
   case $rc in 0) ;; *) tail -15 "$O/$tag.err"; exit 1;; esac
 }
-run c5z3_n8_full 560 --gpus 8 --zero 3 --config C5 --steps 2 --warmup 1
+run c5z3_n4_full 560 --gpus 4 --zero 3 --config C5 --steps 2 --warmup 1
 run c4z1_n8_full 500 --gpus 8 --zero 1 --steps 2 --warmup 1 --no-comm-sweep
 echo "[r04r8b] done"
