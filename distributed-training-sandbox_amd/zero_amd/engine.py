@@ -193,7 +193,8 @@ def probed_zeros(n: int, dtype, device, tries: int = 8, accept_gbs: float = PROB
     env = os.environ.get("ZERO_AMD_PROBE_ACCEPT_GBS")  # diagnostics: the acceptance threshold
     if env:
         accept_gbs = float(env)
-    if nbytes < PROBE_MIN_BYTES:
+    env = os.environ.get("ZERO_AMD_PROBE_MIN_BYTES")  # diagnostics: the smallest buffer probed
+    if nbytes < (int(env) if env else PROBE_MIN_BYTES):
         return torch.zeros(n, dtype=dtype, device=device), info
     device = torch.device(device)
     stream = torch.cuda.current_stream(device)
