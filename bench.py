@@ -1538,6 +1538,15 @@ def main(argv=None):
             _teardown_engine(opt)
             opt, step = build(best)
     arena_used = getattr(opt.engine, "arena_kind", "buckets") if multi else "none (ws=1: no exchange)"
+    lib_auto = None
+    if world > 1 and len(arenas) > 1 and args.layout == "reference" and args.comm in ("rccl", "c10d"):
+        # what the library's own arena="auto" (a sample exchange at construction) would pick on
+        # this interconnect, beside the full-step calibration above that chose the timed arena
+        from zero_amd._sharded import calibrate_arena
+
+        _phase("library arena=auto calibration")
+        lib_auto = calibrate_arena(opt)
+        lib_auto["agrees_with_full_step"] = lib_auto["chosen"] == arena_used
 
     _phase("warmup")
     for _ in range(args.warmup):
@@ -1700,6 +1709,8 @@ def main(argv=None):
         if arena_ab:
             out["arena_calibration_ms_per_step"] = arena_ab
             out["arena_calibration"] = arena_cal
+        if lib_auto is not None:
+            out["arena_calibration_library_auto"] = lib_auto
         out["host_enqueue_ms_per_step"] = host_ms  # rank 0's Python + launch time per step
         if collectives is not None:
             out["collectives"] = collectives

@@ -44,6 +44,8 @@ class ShardedOptimizerBase:
                  bucket_mb: float | None = None, comm=None, sync: bool = True, buckets: str = "ragged",
                  overlap: bool = False, overlap_bucket_mb: float = 64.0, master: str = "split",
                  arena: str = "flat", grad_comm: str | None = None):
+        if arena not in ("flat", "buckets", "auto"):
+            raise ValueError(f"arena must be 'flat', 'buckets' or 'auto' (got {arena!r})")
         if not isinstance(optimizer, torch.optim.Adam):
             raise TypeError("zero_amd ShardedOptimizer wraps torch.optim.Adam / AdamW "
                             f"(got {type(optimizer).__name__})")
@@ -73,17 +75,24 @@ class ShardedOptimizerBase:
         self.world_size, self.rank = world_size, rank
         self._layout = layout
         self._buckets = buckets
+        self._comm = comm
+        self.arena_calibration = None
+        if arena == "auto":
+            # measured on this job's interconnect at construction (a collective call): the flat
+            # arena's grouped reduce / broadcast against the bucket arena's reduce-scatter /
+            # all-gather plus its pack / unpack copies (calibrate_arena)
+            arena = "flat"
+            if world_size > 1 and layout == "reference" and grad_comm is None:
+                self.arena_calibration = calibrate_arena(self)
+                arena = self.arena_calibration["chosen"]
         # bytes per bucket (bucket arena) / per round (flat arena, all owners' windows together);
         # default 256 MiB / 1 GiB: a flat round has no pack to pipeline, so fewer, larger rounds
         # cost only the last round's Adam as exposed tail and cut the launches per step
         if bucket_mb is None:
             bucket_mb = 1024.0 if arena == "flat" else 256.0
         self._bucket_bytes = int(bucket_mb * (1 << 20))
-        self._comm = comm
         self._sync = sync
         self._master = master  # bf16 params: "split" (bf16 param + int16 residual) or "fp32"
-        if arena not in ("flat", "buckets"):
-            raise ValueError(f"arena must be 'flat' or 'buckets' (got {arena!r})")
         # ws > 1 exchange: "flat" = params and grads are views of one owner-major arena, rounds of
         # grouped reduce / broadcast, no pack / unpack (flat.py); "buckets" = the rank-major
         # bucket arena with pack / reduce-scatter / all-gather / unpack (engine.py)
@@ -326,6 +335,92 @@ class ShardedOptimizerBase:
     def __repr__(self):
         return (f"{type(self).__name__}(zero={self._variant}, ws={self.world_size}, rank={self.rank}, "
                 f"owned={self.local_param_indices[:1]}..{self.local_param_indices[-1:]})")
+
+
+CALIBRATION_BYTES = 256 << 20  # gradient bytes per calibration exchange (capped by the model's)
+
+
+def _owner_bytes(opt) -> list:
+    """Gradient bytes each rank owns under the reference's index ranges (zero1.py:55-62)."""
+    ws, n = opt.world_size, len(opt.params)
+    ppr, rem = n // ws, n % ws
+    out = []
+    for r in range(ws):
+        a = r * ppr + min(r, rem)
+        b = a + ppr + (1 if r < rem else 0)
+        out.append(sum(p.numel() * p.element_size() for p in opt.params[a:b]))
+    return out
+
+
+def calibrate_arena(opt, iters: int = 3) -> dict:
+    """``arena="auto"``: time both exchanges on this job's interconnect, at construction.
+
+    A ``CALIBRATION_BYTES`` sample of the gradient (the model's own size if smaller) is exchanged
+    the flat arena's way — one RCCL group of per-owner reduces then one of per-owner broadcasts,
+    windows in proportion to what each rank owns (uneven under the reference's index ranges) — and
+    the bucket arena's way — equal-chunk reduce-scatter then all-gather, plus the pack and unpack
+    copies it needs (two copies of the sample through the gfx950 copy kernel) — each ``iters``
+    times after one warm-up, on the collective stream.  Rank 0's times decide (a collective
+    finishes on every rank together) and its choice is broadcast, so every rank builds the same
+    arena.  Per-step estimates scale the sample to the model's gradient bytes; the bucket arena is
+    chosen only when it is at least 5 % faster (no overlap credit to either side)."""
+    import numpy as np
+
+    from .comm import RcclComm, comm_stream
+    from .kernels import CopySet
+
+    if opt._comm is None:
+        opt._comm = RcclComm()
+    comm, ws = opt._comm, opt.world_size
+    p0 = opt.params[0]
+    dev, dt = p0.device, p0.dtype
+    es = p0.element_size()
+    total = sum(p.numel() for p in opt.params) * es
+    align = ws * 64
+    n = max(align, min(total, CALIBRATION_BYTES) // es // align * align)  # elements in the sample
+    own = np.asarray(_owner_bytes(opt), np.float64)
+    share = own / own.sum() if own.sum() > 0 else np.full(ws, 1.0 / ws)
+    win_len = np.floor(share * n).astype(np.int64)
+    win_len[-1] += n - int(win_len.sum())
+    win_off = np.concatenate([[0], np.cumsum(win_len)[:-1]]).astype(np.int64)
+    stream = comm_stream(dev)
+    buf = torch.zeros(n, dtype=dt, device=dev)
+    chunk = torch.zeros(n // ws, dtype=dt, device=dev)
+    scratch = torch.empty_like(buf)
+    nb = n * es
+    copy = CopySet([buf.data_ptr()], [scratch.data_ptr()], [nb])
+
+    def flat():
+        comm.reduce_v(buf, win_off, win_len, stream)
+        comm.broadcast_v(buf, win_off, win_len, stream)
+
+    def buckets():
+        copy.run(stream)  # pack
+        comm.reduce_scatter(buf, chunk, stream)
+        comm.all_gather(chunk, buf, stream)
+        copy.run(stream)  # unpack
+
+    def timed(fn):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(iters):
+            fn()
+        e1.record(stream)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / iters
+
+    torch.cuda.synchronize(dev)
+    t_flat, t_buck = timed(flat), timed(buckets)
+    scale = total / nb
+    est = {"flat": t_flat * scale, "buckets": t_buck * scale}
+    chosen = "buckets" if est["buckets"] < 0.95 * est["flat"] else "flat"
+    obj = [chosen]
+    dist.broadcast_object_list(obj, src=0)
+    del buf, chunk, scratch, copy
+    return {"chosen": obj[0], "sample_bytes": nb, "grad_bytes": total,
+            "sample_ms": {"flat": t_flat, "buckets": t_buck},
+            "est_ms_per_step": est, "decided_by": "rank 0"}
 
 
 def is_initialized() -> bool:

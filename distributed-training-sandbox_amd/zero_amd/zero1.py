@@ -28,6 +28,8 @@ Mechanism (the same engine as ZeRO-2, ``zero2.py``):
   * ``arena="buckets"``: parameters and grads stay where the caller put them; grads are packed
     into rank-major buckets, moved by in-place reduce-scatter / all-gather (plus per-owner grouped
     reduce / broadcast for the ragged tail), unpacked; grads are released after the step.
+  * ``arena="auto"``: the two exchanges timed on a gradient sample at construction, the faster
+    built on every rank (as zero2.py describes).
 """
 from __future__ import annotations
 

@@ -24,7 +24,12 @@ Here:
     reduce / broadcast for the ragged tail) delivers each owner its summed grads, Adam updates
     them, an in-place all-gather per bucket replaces the per-param broadcasts, then unpack; grads
     are released after the step.
-Ownership, and therefore optimizer-state placement, is bit-identical to the reference on both.
+  * ``arena="auto"``: at construction (ws > 1, a collective call) a 256 MiB sample of the gradient
+    is exchanged both ways on this job's interconnect — grouped per-owner reduce + broadcast
+    against reduce-scatter + all-gather plus the pack / unpack copies — and the arena whose
+    estimate per step is lower (buckets only when >= 5 % faster) is built on every rank;
+    ``arena_calibration`` holds the times (``_sharded.calibrate_arena``).
+Ownership, and therefore optimizer-state placement, is bit-identical to the reference on all.
 """
 from __future__ import annotations
 

@@ -45,6 +45,24 @@ def set_grad(p, g):
         p.grad = g
 
 
+def check_auto_arena(opt, ws):
+    """arena="auto": calibrated at construction at ws > 1, the same choice on every rank, and the
+    engine built is the chosen one (the flat arena builds its engine at construction)."""
+    import torch.distributed as dist
+
+    cal = opt.arena_calibration
+    if ws == 1:
+        assert cal is None
+        return
+    assert cal["chosen"] in ("flat", "buckets") and cal["sample_bytes"] > 0
+    assert all(v > 0 for v in cal["sample_ms"].values())
+    every = [None] * ws
+    dist.all_gather_object(every, cal["chosen"])
+    assert len(set(every)) == 1, every
+    kind = getattr(opt.engine, "arena_kind", "buckets") if opt.engine is not None else "buckets"
+    assert kind == cal["chosen"], (kind, cal)
+
+
 def run_injected(z, variant: int, rank: int, ws: int, device, comm=None, window_elems=64, tol=1e-6,
                  buckets=None, arena=None):
     """Replay the fixture's grads through ShardedOptimizer; assert params match every step."""
@@ -59,6 +77,8 @@ def run_injected(z, variant: int, rank: int, ws: int, device, comm=None, window_
     if arena is not None:
         kw["arena"] = arena
     opt = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), **kw)
+    if arena == "auto":
+        check_auto_arena(opt, ws)
     worst = 0.0
     for t in range(steps):
         opt.zero_grad()

@@ -195,6 +195,10 @@ def _edge_worker(rank, ws, port, variant, buckets, arena="flat"):
     opt = module_for(variant).ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=test_comm(),
                                                bucket_mb=ws * 64 * 4 / (1 << 20), buckets=buckets,
                                                arena=arena)
+    if arena == "auto":
+        from _zero_run import check_auto_arena
+
+        check_auto_arena(opt, ws)
     if rank == 3:
         assert opt.local_param_indices == []
     for t in range(steps):
@@ -216,9 +220,10 @@ def _edge_worker(rank, ws, port, variant, buckets, arena="flat"):
 def test_multirank_fewer_params_than_ranks(gpu):
     """Edge cases of the reference's ownership rule on the device path: n < ws (empty ranks) and a
     zero-element parameter, against the oracle's restatement of the reference (ZeRO-1 and 2; flat
-    arena, ragged and padded bucket arena)."""
+    arena, ragged and padded bucket arena, and arena="auto" calibrating with an owner of nothing)."""
     spawn_batch(4, [(_edge_worker, (v, b, a)) for v in (1, 2)
-                    for b, a in (("ragged", "flat"), ("ragged", "buckets"), ("padded", "buckets"))])
+                    for b, a in (("ragged", "flat"), ("ragged", "buckets"), ("padded", "buckets"),
+                                 ("ragged", "auto"))])
 
 
 HP_CASES = {

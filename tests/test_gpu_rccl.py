@@ -52,11 +52,12 @@ def _zero12_cases(ws):
     from test_gpu_parity import (_bf16comm_worker, _carry_worker, _comm_time_worker, _edge_worker,
                                  _hp_worker, _mr_worker)
 
-    inj = {2: [(1, "distinct", None), (2, "distinct", None)],
+    inj = {2: [(1, "distinct", None), (2, "distinct", None), (2, "distinct", "auto")],
            3: [(1, "distinct", "buckets")],
            4: [(1, "ref", None), (2, "distinct", None), (2, "distinct", "buckets")],
            8: [(2, "distinct", None), (1, "distinct", None), (2, "distinct", "buckets"),
-               (1, "distinct", "buckets"), (1, "ref", None), (2, "ref", None)]}[ws]
+               (1, "distinct", "buckets"), (1, "ref", None), (2, "ref", None),
+               (1, "distinct", "auto")]}[ws]
     cases = [(_mr_worker, (v, f"traj_z{v}_ws{ws}_d16_{m}.npz", "ragged", a)) for v, m, a in inj]
     if ws == 2:
         from test_gpu_checkpoint import _ckpt_worker

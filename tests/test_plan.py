@@ -238,3 +238,23 @@ def test_smollm3_shapes_match_transformers_model():
     got = [tuple(p.shape) for p in model.parameters()]
     assert got == [tuple(s) for s in smollm3_3b_shapes()]
     assert sm.model_flops_per_token(model.config, 8192) > 6 * 3.0e9
+
+
+def test_arena_auto_owner_shares_and_validation():
+    """arena="auto"'s sample windows follow the reference's index ranges (zero1.py:55-62): bytes per
+    owner, empty owners included; an unknown arena is rejected before anything is built."""
+    import types
+
+    import pytest
+    import torch
+
+    from zero_amd import _sharded
+
+    ps = [torch.zeros(n) for n in (5, 7, 11)]
+    opt = types.SimpleNamespace(world_size=4, params=ps)
+    assert _sharded._owner_bytes(opt) == [20, 28, 44, 0]
+    opt = types.SimpleNamespace(world_size=2, params=ps + [torch.zeros(3, dtype=torch.bfloat16)])
+    assert _sharded._owner_bytes(opt) == [48, 50]
+    with pytest.raises(ValueError, match="arena must be"):
+        _sharded.ShardedOptimizerBase(torch.optim.Adam([torch.nn.Parameter(torch.zeros(4))]),
+                                      arena="fastest")
