@@ -253,16 +253,20 @@ def _bench_rank(rank, ws, port, argv):
             assert cal[kind]["busbw_gbs"] > 0 and cal[kind]["frac_of_peer_links"] > 0, cal
             assert cal[kind]["ms_per_step"] == out["arena_calibration_ms_per_step"][kind]
         assert out["rccl_selfcheck"]["all_ranks_ok"] and out["config"]["comm"] == "rccl"
+        lib = out["arena_calibration_library_auto"]  # the library's arena="auto" on the same wire
+        assert lib["chosen"] in ("flat", "buckets") and lib["sample_bytes"] > 0, lib
+        assert lib["agrees_with_full_step"] == (lib["chosen"] == out["config"]["arena"]), lib
 
 
 @pytest.mark.timeout(600)
 def test_bench_share_gpu_n8_both_arenas(gpu):
     """The driver's default N=8 run (C4 ZeRO-2, ``--arena auto``) rehearsed through real RCCL on a
-    4-layer copy of the SmolLM3-3B set (8 ranks x full C4 exceed one device): communicator
+    4-layer copy of the SmolLM3-3B set (the full set at N = 8 takes minutes over sockets:
+    tools/r04_rehearsal8.sh, profiles/r04_rccl_net/c4_n8_full.json): communicator
     self-check, then BOTH arenas the calibration can pick — the flat arena's grouped reduce /
     broadcast rounds and the bucket arena's pack / RS / AG / unpack — each exchange-checked (reduced
     grads within the ring bound, Adam within 1 bf16 ulp of the restatement, ranks bit-identical),
-    calibrated and timed."""
+    calibrated and timed; the library's own arena="auto" choice is reported beside it."""
     from _zero_run import spawn_ranks
 
     argv = ["--gpus", "8", "--share-gpu", "--no-cpu-baseline", "--watchdog-s", "0", "--config", "C4",
