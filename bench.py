@@ -1195,8 +1195,9 @@ def bench_train_smollm3(args, world, rank, dev, use_nccl):
         zero3.register_zero3_hooks(model, opt.param_managers, units=list(model.model.layers),
                                    reshard_after_forward=not args.no_reshard)
     else:
-        opt = zero2.ShardedOptimizer(torch.optim.AdamW(model.parameters(), lr=1e-5), overlap=True,
-                                     sync=False, arena="buckets" if args.arena == "buckets" else "flat")
+        opt = zero2.ShardedOptimizer(torch.optim.AdamW(model.parameters(), lr=1e-5),
+                                     overlap=not args.no_overlap, sync=False,
+                                     arena="buckets" if args.arena == "buckets" else "flat")
     batch = args.batch or 1
     g = torch.Generator(device=dev).manual_seed(42 + rank)  # each rank its own data shard
     ids = torch.randint(0, cfg.vocab_size, (batch, args.seq), device=dev, generator=g)
@@ -1298,6 +1299,8 @@ def main(argv=None):
     ap.add_argument("--no-reshard", action="store_true",
                     help="--train --zero 3: keep gathered parameters from forward through backward "
                          "(FSDP2 reshard_after_forward=False, the reference's 'ZeRO-2' run)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="--train --zero 1/2: reduce in step() instead of from backward hooks")
     ap.add_argument("--set-layers", type=int, default=None,
                     help="C4/C5: a copy of the parameter set with fewer decoder layers (tests and "
                          "N=8 rehearsals on one GPU; not the metric)")
