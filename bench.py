@@ -1474,7 +1474,7 @@ def main(argv=None):
             o._build_engine()  # (the bucket engine is otherwise built by the first step)
         if getattr(o.engine, "arena_kind", None) == "flat":
             # grads resident in HBM where a backward puts them: in the arena's grad views
-            o.zero_grad()
+            o.zero_grad(set_to_none=False)
             with torch.no_grad():
                 for p, g in zip(params, grads):
                     p.grad.copy_(g)

@@ -235,8 +235,10 @@ class ShardedOptimizerBase:
             p.grad = None
 
     def zero_grad(self, set_to_none: bool = True):
-        if self._flat():  # zeroed views of the grad arena (backward accumulates in place)
-            self.engine.zero_grad()
+        if self._flat():
+            # ZeRO-2: None, as the reference's (backward's fresh grads are copied into the arena);
+            # ZeRO-1: zeroed views of the grad arena (its carry follows the surviving views)
+            self.engine.zero_grad(set_to_none=set_to_none and not self._carry)
             return
         if self._overlap:  # grads become zeroed views of the overlap buckets (no pack copy)
             self.engine.gb.install_views()

@@ -11,8 +11,10 @@ outside the arena.  ``FlatEngine`` moves them in:
   assigns rank r the contiguous index range [start_r, end_r) (zero1.py:55-62), so rank r's
   parameters — its optimizer shard, its *stream* — are one contiguous region of P, each slot
   64-element aligned;
-* **G** — the gradients, the same layout; ``zero_grad()`` zeroes G and makes every ``p.grad`` a
-  view of its slot, so backward accumulates straight into it;
+* **G** — the gradients, the same layout; a fresh gradient from backward is copied into its slot
+  and ``p.grad`` becomes the slot's view (ZeRO-2's ``zero_grad()`` sets grads to None, as the
+  reference's does); ZeRO-1's ``zero_grad()`` zeroes G and makes every ``p.grad`` a view of its
+  slot, so backward accumulates straight into it (the carry needs the views to persist);
 * **R** — this rank's reduced gradient, one stream long.
 
 A step is cut into *rounds*; round j is window j (``W`` elements) of every owner's stream.  Per
@@ -136,6 +138,10 @@ class FlatEngine(ShardEngine):
         # parameters carrying this engine's post-accumulate-grad hook; requires_grad can change
         # after construction (gradual unfreezing), so the set is refreshed (_refresh_requires_grad)
         self.hooked = np.zeros(n, bool)
+        # a fresh gradient backward hands over (p.grad was None) becomes its arena view in the
+        # post-accumulate hook — except under ZeRO-1's carry, which reads "the caller replaced the
+        # view" from p.grad at step() (the module docstring)
+        self.adopt_fresh = self.carry is None
         self.overlap = False  # backward-overlapped reduces (enable_overlap)
         self.ov_K = 0
         self.launched_in_backward = 0
@@ -189,11 +195,22 @@ class FlatEngine(ShardEngine):
                 p.grad = self.grad_view(i)
             self._views[i] = p.grad
 
-    def zero_grad(self):
-        """The wrapper's zero_grad(): zero G and make every p.grad its arena view."""
-        self.G.zero_()
-        self.dirty[:] = False
-        self.install_views()
+    def zero_grad(self, set_to_none: bool = False):
+        """The wrapper's zero_grad().  ``set_to_none`` (ZeRO-2): every p.grad becomes None, as the
+        reference's zero_grad leaves them (zero2.py:113 + the inner optimizer's zero_grad), and G
+        keeps its stale values (``dirty``): backward then hands over fresh gradients, which are
+        copied into their slots — by the post-accumulate hook in overlap mode, by one copy launch
+        in step() otherwise — 4 B per bf16 element, where zeroing G and accumulating into its views
+        costs 8 (a memset plus an in-place add).  Otherwise (ZeRO-1, whose carry needs the views to
+        survive, or ``set_to_none=False``): G is zeroed and every p.grad made its arena view."""
+        if set_to_none:
+            for i, p in enumerate(self.params):
+                p.grad = None
+                self._views[i] = None
+        else:
+            self.G.zero_()
+            self.dirty[:] = False
+            self.install_views()
         self.zero_grad_calls += 1
         self.touched[:] = False
         self.any_touched = False
@@ -277,6 +294,19 @@ class FlatEngine(ShardEngine):
     def _mark(self, i: int):
         self.touched[i] = True
         self.any_touched = True
+        if self.adopt_fresh:
+            self._adopt(i)
+
+    def _adopt(self, i: int):
+        """A fresh gradient (zero_grad set p.grad to None) into its arena slot; p.grad becomes the
+        slot's view and the fresh tensor returns to the allocator now rather than at step()."""
+        p = self.params[i]
+        g = p.grad
+        if g is not None and not self.is_view(i, g):
+            v = self.grad_view(i)
+            v.copy_(g.reshape(p.shape))
+            p.grad = v
+            self._views[i] = v
 
     def _requires_grad(self) -> np.ndarray:
         return np.fromiter((p.requires_grad for p in self.params), bool, len(self.params))
@@ -370,9 +400,12 @@ class FlatEngine(ShardEngine):
         self.ov_marked[i] = True
         self.touched[i] = True
         self.any_touched = True
-        g = self.params[i].grad
-        if g is not None and not self.is_view(i, g):  # a fresh grad (the caller cleared the view)
-            self.grad_view(i).copy_(g.reshape(self.params[i].shape))
+        if self.adopt_fresh:  # a fresh grad (zero_grad set it to None): into the slot, adopted
+            self._adopt(i)
+        else:  # ZeRO-1: into the slot for the reduce; p.grad stays the caller's tensor (carry 0)
+            g = self.params[i].grad
+            if g is not None and not self.is_view(i, g):
+                self.grad_view(i).copy_(g.reshape(self.params[i].shape))
         self.ov_pending[self.ov_bucket_of[i]] -= 1
         while self.ov_next < self.ov_K and self.ov_pending[self.ov_next] == 0:
             self._ov_launch(self.ov_next)
