@@ -69,8 +69,8 @@ def test_c4_rank0_bucket_path_full_scale(gpu, monkeypatch, ws, buckets, arena):
         init = [p.detach().clone() for p in params]
         opt = zero2.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=IdentityComm(ws),
                                      buckets=buckets, arena=arena)
-        if arena == "flat":  # backward's way: into the zeroed arena views
-            opt.zero_grad()
+        if arena == "flat":  # into the arena views, as bench.py (set_to_none=False keeps them)
+            opt.zero_grad(set_to_none=False)
             for p, g in zip(params, grads):
                 p.grad.copy_(g)
         else:
