@@ -9,15 +9,17 @@ exactly data-parallel Adam.
 Here:
   * default ``arena="flat"``: every parameter is a view of one owner-major *flat parameter
     arena* (rank r's owned parameters, Layout R, are the contiguous stretch [base_r, base_r+L_r)),
-    and after ``zero_grad()`` every ``p.grad`` is a view of a flat gradient arena of the same
-    layout, so backward accumulates straight into it.  A step is a few *rounds* (window j of every
+    and every gradient lands in a flat gradient arena of the same layout: ``zero_grad()`` sets
+    the grads to None (as the reference's), and each fresh gradient backward produces is copied
+    into its slot by a post-accumulate-grad hook, ``p.grad`` becoming the slot's view.  A step is a few *rounds* (window j of every
     owner's stretch): ONE RCCL group of per-owner ``ncclReduce`` — each owner's window of the
     gradient arena summed into its reduced buffer, the reduce-scatter-v of zero2.py:94-113 —, the
     fused HIP Adam on the own window (``/ws`` folded in) writing the updated parameters straight
     into the arena, and ONE RCCL group of in-place ``ncclBroadcast`` of every owner's window, the
     all-gather-v of zero2.py:122-133.  No pack, no unpack: the parameters are the arena.  After
     the step ``p.grad`` is still the arena view holding this rank's local gradient (the reduce is
-    out of place); ``zero_grad()`` zeroes it.  ``overlap=True`` launches each round's reduces from
+    out of place) until ``zero_grad()`` (``set_to_none=False`` zeroes the views instead).
+    ``overlap=True`` launches each round's reduces from
     backward hooks as buckets complete.
   * ``arena="buckets"``: parameters and grads stay where the caller put them; grads are packed
     into rank-major buckets, one in-place RCCL reduce-scatter per even bucket (grouped per-owner
