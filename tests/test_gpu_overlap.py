@@ -88,6 +88,37 @@ def test_overlap_unused_param_keeps_value(gpu, pg1):
     assert "exp_avg" in opt.optimizer.state[ps[0]]
 
 
+@pytest.mark.parametrize("overlap", [False, True])
+def test_zero2_flat_zero_grad_sets_none_then_adopts(gpu, pg1, overlap):
+    """ZeRO-2 on the flat arena: zero_grad() leaves p.grad None (the reference's state after
+    zero_grad); backward's fresh gradient lands in its arena slot and p.grad becomes the slot's
+    view; a second backward accumulates in the view (without overlap, which allows it);
+    zero_grad(set_to_none=False) hands out zeroed views; ZeRO-1 keeps zeroed views (its carry)."""
+    from zero_amd import zero1, zero2
+
+    ps = [torch.nn.Parameter(torch.randn(64, 8, device=gpu)) for _ in range(3)]
+    opt = zero2.ShardedOptimizer(torch.optim.Adam(ps, lr=1e-2), overlap=overlap,
+                                 overlap_bucket_mb=1e-3)
+    eng = opt.engine
+    opt.zero_grad()
+    assert all(p.grad is None for p in ps)
+    w = [torch.randn(64, 8, device=gpu) for _ in ps]
+    sum((p * x).sum() for p, x in zip(ps, w)).backward()
+    for i, (p, x) in enumerate(zip(ps, w)):
+        assert eng.is_view(i, p.grad) and torch.equal(p.grad, x)
+    if not overlap:
+        sum((p * x).sum() for p, x in zip(ps, w)).backward()
+        for p, x in zip(ps, w):
+            assert torch.equal(p.grad, x + x)
+    opt.step()
+    opt.zero_grad(set_to_none=False)
+    assert all(eng.is_view(i, p.grad) and not p.grad.any() for i, p in enumerate(ps))
+    q = torch.nn.Parameter(torch.randn(8, device=gpu))
+    z1 = zero1.ShardedOptimizer(torch.optim.Adam([q], lr=1e-2))
+    z1.zero_grad()
+    assert q.grad is not None and not q.grad.any() and z1.engine.is_view(0, q.grad)
+
+
 def test_overlap_double_backward_raises(gpu, pg1):
     from zero_amd import zero2
 
