@@ -124,6 +124,34 @@ struct CopySeg {
 // Cache policy by size (NT) as zs_scale / zs_convert: non-temporal when the set moves more than the
 // MALL holds (a C4 pack group, a checkpoint), the default policy below (a 64 MB overlap bucket, read
 // next by its collective); `zs_tune("copy_nt")` forces either.
+// One chunk [b0, b1) of one segment, by the whole workgroup.
+template <int U, bool NT>
+__device__ __forceinline__ void copy_chunk(const unsigned char* s_src, unsigned char* s_dst, bool vec,
+                                           int64_t b0, int64_t b1) {
+  const gptr<const unsigned char> src = glob(s_src);
+  const gptr<unsigned char> dst = glob(s_dst);
+  if (vec) {
+    uint4 val[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // all loads first: U x 16 B in flight per lane
+      const int64_t off = b0 + (int64_t(u) * kThreads + threadIdx.x) * 16;
+      val[u] = make_uint4(0, 0, 0, 0);
+      if (s_src && off + 16 <= b1) val[u] = ld16<NT>(s_src + off);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t off = b0 + (int64_t(u) * kThreads + threadIdx.x) * 16;
+      if (off + 16 <= b1) {
+        st16<NT>(s_dst + off, val[u]);
+      } else if (off < b1) {
+        for (int64_t b = off; b < b1; ++b) dst[b] = s_src ? src[b] : 0;
+      }
+    }
+  } else {
+    for (int64_t b = b0 + threadIdx.x; b < b1; b += kThreads) dst[b] = s_src ? src[b] : 0;
+  }
+}
+
 template <int U, bool NT>
 __global__ __launch_bounds__(kThreads) void copy_segments_kernel(
     const CopySeg* __restrict__ segs, const int64_t* __restrict__ chunk_prefix, int64_t nseg,
@@ -134,29 +162,33 @@ __global__ __launch_bounds__(kThreads) void copy_segments_kernel(
     while (chunk_prefix[seg + 1] <= c) ++seg;  // uniform forward scan
     const CopySeg s = segs[seg];
     const int64_t b0 = (c - chunk_prefix[seg]) * kChunk;
-    const int64_t b1 = min(b0 + kChunk, s.nbytes);
-    const gptr<const unsigned char> src = glob(s.src);
-    const gptr<unsigned char> dst = glob(s.dst);
-    if (s.vec) {
-      uint4 val[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {  // all loads first: U x 16 B in flight per lane
-        const int64_t off = b0 + (int64_t(u) * kThreads + threadIdx.x) * 16;
-        val[u] = make_uint4(0, 0, 0, 0);
-        if (src && off + 16 <= b1) val[u] = ld16<NT>(s.src + off);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t off = b0 + (int64_t(u) * kThreads + threadIdx.x) * 16;
-        if (off + 16 <= b1) {
-          st16<NT>(s.dst + off, val[u]);
-        } else if (off < b1) {
-          for (int64_t b = off; b < b1; ++b) dst[b] = src ? src[b] : 0;
-        }
-      }
-    } else {
-      for (int64_t b = b0 + threadIdx.x; b < b1; b += kThreads) dst[b] = src ? src[b] : 0;
-    }
+    copy_chunk<U, NT>(s.src, s.dst, s.vec != 0, b0, min(b0 + kChunk, s.nbytes));
+  }
+}
+
+// The same copy with up to kDirectMax segments passed BY VALUE in the kernel arguments: no
+// descriptor table to allocate and upload, so a set whose pointers change every call (backward's
+// fresh gradients into their arena slots) costs one launch and nothing else.
+constexpr int kDirectMax = 64;
+struct DirectSet {
+  const unsigned char* src[kDirectMax];  // nullptr = zero fill
+  unsigned char* dst[kDirectMax];
+  int64_t nbytes[kDirectMax];
+  int64_t prefix[kDirectMax + 1];  // chunk prefix over the segments
+  uint64_t vec_mask;               // bit i: segment i is 16-byte aligned on both sides
+  int n;
+};
+
+template <int U, bool NT>
+__global__ __launch_bounds__(kThreads) void copy_direct_kernel(const DirectSet set) {
+  constexpr int64_t kChunk = copy_chunk_bytes(U);
+  const int64_t total = set.prefix[set.n];
+  int seg = 0;
+  for (int64_t c = blockIdx.x; c < total; c += gridDim.x) {
+    while (set.prefix[seg + 1] <= c) ++seg;  // uniform forward scan
+    const int64_t b0 = (c - set.prefix[seg]) * kChunk;
+    copy_chunk<U, NT>(set.src[seg], set.dst[seg], (set.vec_mask >> seg) & 1, b0,
+                      min(b0 + kChunk, set.nbytes[seg]));
   }
 }
 
@@ -1067,6 +1099,45 @@ int zs_copyset_destroy(zs_copyset* cs) {
   if (cs->d_segs) (void)hipFree(cs->d_segs);
   if (cs->d_prefix) (void)hipFree(cs->d_prefix);
   delete cs;
+  return ZS_OK;
+}
+
+int zs_copy_direct(int64_t n, const uint64_t* src, const uint64_t* dst, const int64_t* nbytes,
+                   uintptr_t stream) {
+  ZS_REQUIRE(n >= 0, "zs_copy_direct: n < 0");
+  if (n == 0) return ZS_OK;
+  ZS_REQUIRE(src && dst && nbytes, "zs_copy_direct: NULL table");
+  int64_t total_bytes = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    ZS_REQUIRE(nbytes[i] >= 0, "zs_copy_direct: nbytes[%lld] < 0", (long long)i);
+    ZS_REQUIRE(nbytes[i] == 0 || dst[i] != 0, "zs_copy_direct: dst[%lld] is NULL", (long long)i);
+    total_bytes += nbytes[i];
+  }
+  const int force = copy_nt_mode();
+  const bool nt = force < 0 ? 2 * total_bytes > kMallBytes : force == 1;
+  constexpr int U = kCopyUnrollDefault;
+  const int64_t chunk = copy_chunk_bytes(U);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int64_t i0 = 0; i0 < n;) {  // launches of up to kDirectMax non-empty segments
+    DirectSet set{};
+    int k = 0;
+    for (; i0 < n && k < kDirectMax; ++i0) {
+      if (nbytes[i0] == 0) continue;
+      set.src[k] = reinterpret_cast<const unsigned char*>(src[i0]);
+      set.dst[k] = reinterpret_cast<unsigned char*>(dst[i0]);
+      set.nbytes[k] = nbytes[i0];
+      set.prefix[k + 1] = set.prefix[k] + (nbytes[i0] + chunk - 1) / chunk;
+      if (aligned(src[i0], 16) && aligned(dst[i0], 16)) set.vec_mask |= uint64_t(1) << k;
+      ++k;
+    }
+    set.n = k;
+    if (k == 0) break;
+    for (int j = k; j < kDirectMax; ++j) set.prefix[j + 1] = set.prefix[k];
+    const int grid = int(std::min<int64_t>(set.prefix[k], grid_cap()));
+    if (nt) hipLaunchKernelGGL((copy_direct_kernel<U, true>), dim3(grid), dim3(kThreads), 0, st, set);
+    else hipLaunchKernelGGL((copy_direct_kernel<U, false>), dim3(grid), dim3(kThreads), 0, st, set);
+    ZS_HIP(hipGetLastError());
+  }
   return ZS_OK;
 }
 

@@ -20,7 +20,7 @@ ZS_OK, ZS_ERR_INVALID, ZS_ERR_HIP, ZS_ERR_RCCL, ZS_ERR_NOMEM = 0, 1, 2, 3, 4
 ZS_F32, ZS_BF16, ZS_U8, ZS_BF16_SPLIT = 0, 1, 2, 3
 ZS_LAYOUT_R, ZS_LAYOUT_Z, ZS_LAYOUT_F = 0, 1, 2
 ZS_BUCKETS_RAGGED, ZS_BUCKETS_PADDED = 0, 1
-ABI_VERSION = 10
+ABI_VERSION = 11
 ZS_UNIQUE_ID_BYTES = 128
 
 # Every symbol include/zero_amd.h declares (tests check the library exports all of them).
@@ -30,7 +30,7 @@ EXPORTED = (
     "zs_plan_stream_len", "zs_plan_num_pieces", "zs_plan_pieces", "zs_plan_bucket",
     "zs_plan_num_segments", "zs_plan_segments", "zs_plan_num_buckets", "zs_plan_bucket_bytes",
     "zs_pack", "zs_unpack",
-    "zs_copyset_create", "zs_copyset_run", "zs_copyset_destroy", "zs_scale",
+    "zs_copyset_create", "zs_copyset_run", "zs_copyset_destroy", "zs_copy_direct", "zs_scale",
     "zs_convert", "zs_fp8_quantize_rows", "zs_fp8_dequantize_rows", "zs_fp8_quantize_rowset",
     "zs_fp8_dequantize_gathered",
     "zs_adam_hparams_init", "zs_adamset_create", "zs_adamset_run", "zs_adamset_destroy",
@@ -98,6 +98,7 @@ _SIGS = {
     "zs_unpack": ([_P, _I64, _P, _PU64, ctypes.c_int, _U], ctypes.c_int),
     "zs_copyset_create": ([_PU64, _PU64, _PI64, _I64, ctypes.POINTER(_P)], ctypes.c_int),
     "zs_copyset_run": ([_P, _U], ctypes.c_int),
+    "zs_copy_direct": ([_I64, _P, _P, _P, _U], ctypes.c_int),
     "zs_copyset_destroy": ([_P], ctypes.c_int),
     "zs_scale": ([_P, _I64, ctypes.c_int, ctypes.c_double, _U], ctypes.c_int),
     "zs_convert": ([_P, ctypes.c_int, _P, ctypes.c_int, _I64, _U], ctypes.c_int),

@@ -43,7 +43,7 @@ import torch
 from . import _lib
 from ._hooks import WeakCall
 from .engine import ALIGN_ELEMS, ShardEngine, _ptr
-from .kernels import CopySet
+from .kernels import copy_direct
 
 _I32P = np.int32
 
@@ -294,19 +294,28 @@ class FlatEngine(ShardEngine):
     def _mark(self, i: int):
         self.touched[i] = True
         self.any_touched = True
-        if self.adopt_fresh:
-            self._adopt(i)
 
-    def _adopt(self, i: int):
-        """A fresh gradient (zero_grad set p.grad to None) into its arena slot; p.grad becomes the
-        slot's view and the fresh tensor returns to the allocator now rather than at step()."""
-        p = self.params[i]
-        g = p.grad
-        if g is not None and not self.is_view(i, g):
-            v = self.grad_view(i)
-            v.copy_(g.reshape(p.shape))
-            p.grad = v
-            self._views[i] = v
+    def _land(self, idx, grads, zero, stream, adopt: bool):
+        """Fresh gradients ``grads`` of parameters ``idx`` (not arena views: zero_grad set p.grad
+        to None, or the caller assigned them) copied into their G slots, and the slots of ``zero``
+        zero-filled — ONE zs_copy_direct on ``stream`` (the segments travel in the kernel
+        arguments: nothing to upload for pointers that change every step).  ``adopt``: p.grad
+        becomes the slot's view, so the fresh tensor returns to the allocator now (stream-ordered
+        after the copy that reads it)."""
+        idx = np.asarray(idx, np.int64)
+        zero = np.asarray(zero, np.int64)
+        if not len(idx) and not len(zero):
+            return
+        all_idx = np.concatenate([idx, zero])
+        src = np.concatenate([np.fromiter((_ptr(g) for g in grads), np.uint64, len(idx)),
+                              np.zeros(len(zero), np.uint64)])
+        dst = np.uint64(self.G.data_ptr()) + (self.slot[all_idx] * self.es).astype(np.uint64)
+        copy_direct(src, dst, self.numel[all_idx] * self.es, stream)
+        if adopt:
+            for i in idx:
+                v = self.grad_view(int(i))
+                self.params[i].grad = v
+                self._views[i] = v
 
     def _requires_grad(self) -> np.ndarray:
         return np.fromiter((p.requires_grad for p in self.params), bool, len(self.params))
@@ -364,6 +373,7 @@ class FlatEngine(ShardEngine):
         return self._mark_hooks
 
     def _ov_reset(self):
+        self.ov_fresh = [[] for _ in range(self.ov_K)]  # per bucket: fresh grads to land
         self.ov_pending = self.ov_size.copy()
         self.ov_marked = np.zeros(len(self.params), bool)
         self.ov_next = 0
@@ -400,12 +410,9 @@ class FlatEngine(ShardEngine):
         self.ov_marked[i] = True
         self.touched[i] = True
         self.any_touched = True
-        if self.adopt_fresh:  # a fresh grad (zero_grad set it to None): into the slot, adopted
-            self._adopt(i)
-        else:  # ZeRO-1: into the slot for the reduce; p.grad stays the caller's tensor (carry 0)
-            g = self.params[i].grad
-            if g is not None and not self.is_view(i, g):
-                self.grad_view(i).copy_(g.reshape(self.params[i].shape))
+        g = self.params[i].grad
+        if g is not None and not self.is_view(i, g):  # fresh (zero_grad set it to None): landed
+            self.ov_fresh[self.ov_bucket_of[i]].append(i)  # with its bucket, one copy launch
         self.ov_pending[self.ov_bucket_of[i]] -= 1
         while self.ov_next < self.ov_K and self.ov_pending[self.ov_next] == 0:
             self._ov_launch(self.ov_next)
@@ -415,6 +422,10 @@ class FlatEngine(ShardEngine):
     def _ov_launch(self, k: int, stream=None):
         cur = torch.cuda.current_stream(self.device) if stream is None else stream
         lo, hi, r = int(self.ov_lo[k]), int(self.ov_hi[k]), int(self.ov_owner[k])
+        fresh = self.ov_fresh[k]
+        if fresh:  # ZeRO-2 adopts the slots as p.grad; ZeRO-1's carry needs the caller's tensors
+            self._land(fresh, [self.params[i].grad for i in fresh], (), cur, self.adopt_fresh)
+            self.ov_fresh[k] = []
         if self.grad_comm:  # the bucket's grads as bf16 for the wire (gfx950 RNE kernel)
             from .kernels import convert
 
@@ -452,14 +463,7 @@ class FlatEngine(ShardEngine):
         # step is zero-filled — only in buckets not launched yet (a launched bucket is complete)
         copy = np.nonzero(has & ~view & ~marked)[0]
         zero = np.nonzero(~has & self.dirty & ~marked)[0]
-        if len(copy) or len(zero):
-            src = np.concatenate([np.fromiter((_ptr(grads[i]) for i in copy), np.uint64, len(copy)),
-                                  np.zeros(len(zero), np.uint64)])
-            idx = np.concatenate([copy, zero]).astype(np.int64)
-            dst = np.uint64(self.G.data_ptr()) + (self.slot[idx] * es).astype(np.uint64)
-            nb = self.numel[idx] * es
-            cs_ = self._cached(("gcopy",), src.tobytes() + dst.tobytes(), lambda: CopySet(src, dst, nb))
-            self._run_copy("pack", cs_, stream)
+        self._land(copy, [grads[i] for i in copy], zero, stream, adopt=False)
         self.dirty = has.copy()
         with _lib.phase_range("all_reduce_gradients"):  # what backward did not reduce
             while self.ov_next < self.ov_K:
@@ -515,17 +519,10 @@ class FlatEngine(ShardEngine):
         # gradients not accumulated into the arena (assigned tensors, fresh grads after the caller
         # cleared the views) are copied in; a stale slot whose grad is gone is zero-filled
         # (overlap mode: in _step_overlap, for the parameters no hook has handled)
-        copy = np.nonzero(has & ~view)[0] if not self.overlap else ()
-        zero = np.nonzero(~has & self.dirty)[0] if not self.overlap else ()
-        if len(copy) or len(zero):
-            src = np.concatenate([np.fromiter((_ptr(grads[i]) for i in copy), np.uint64, len(copy)),
-                                  np.zeros(len(zero), np.uint64)])
-            idx = np.concatenate([copy, zero]).astype(np.int64)
-            dst = np.uint64(self.G.data_ptr()) + (self.slot[idx] * es).astype(np.uint64)
-            nb = self.numel[idx] * es
-            cs_ = self._cached(("gcopy",), src.tobytes() + dst.tobytes(), lambda: CopySet(src, dst, nb))
-            self._run_copy("pack", cs_, stream)
         if not self.overlap:
+            copy = np.nonzero(has & ~view)[0]
+            self._land(copy, [grads[i] for i in copy], np.nonzero(~has & self.dirty)[0], stream,
+                       adopt=False)  # (_reinstall makes them views after the step)
             self.dirty = has.copy()
         # ZeRO-1: the carry weight per owned param (see the module docstring)
         cmul = np.where(view, self.ws - 1, 0).astype(np.int64)

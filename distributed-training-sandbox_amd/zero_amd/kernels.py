@@ -1,6 +1,7 @@
 """Python handles for the gfx950 kernels behind the C ABI (csrc/zs_kernels.hip).
 
 ``CopySet``  — one launch of the descriptor-driven gather/scatter copy (pack / unpack).
+``copy_direct`` — the same copy with the segments in the kernel arguments (no table to keep).
 ``AdamSet``  — one launch of the fused Adam/AdamW update over a list of segments.
 ``adam_step`` — the same update over one contiguous range (zs_adam_step_ex; no table to keep).
 
@@ -51,6 +52,19 @@ class CopySet:
             except Exception:  # interpreter teardown
                 pass
             self._h = None
+
+
+def copy_direct(src, dst, nbytes, stream) -> None:
+    """Copy ``nbytes[i]`` bytes from ``src[i]`` to ``dst[i]`` (src 0 = zero fill) with the segments
+    in the kernel arguments (zs_copy_direct): nothing uploaded, so for pointers that change on
+    every call (backward's fresh gradients)."""
+    src = np.ascontiguousarray(np.asarray(src, dtype=np.uint64))
+    dst = np.ascontiguousarray(np.asarray(dst, dtype=np.uint64))
+    nb = np.ascontiguousarray(np.asarray(nbytes, dtype=np.int64))
+    assert src.shape == dst.shape == nb.shape
+    if nb.size:
+        _lib.call("zs_copy_direct", int(nb.size), src.ctypes.data, dst.ctypes.data, nb.ctypes.data,
+                  stream_handle(stream))
 
 
 def adam_hparams(lr, beta1, beta2, eps, weight_decay, step, *, decoupled=False, amsgrad=False,

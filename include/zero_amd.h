@@ -29,7 +29,7 @@ extern "C" {
  * the *_ex entry points), so a caller built against an older header links and then passes the
  * wrong arguments.  The Python binding (zero_amd/_lib.py) and tests/c/abi_host.c refuse a
  * mismatch. */
-#define ZS_ABI_VERSION 10
+#define ZS_ABI_VERSION 11
 
 enum zs_status {
   ZS_OK = 0,
@@ -158,6 +158,12 @@ int zs_copyset_create(const uint64_t* src, const uint64_t* dst, const int64_t* n
                       zs_copyset** out);
 int zs_copyset_run(const zs_copyset* cs, uintptr_t stream);
 int zs_copyset_destroy(zs_copyset* cs);
+/* The same copy without a table (ABI v11): the segments travel in the kernel arguments, up to 64
+ * per launch (more take more launches), so pointers that change on every call cost nothing to
+ * set up — backward's fresh gradients copied into their flat-arena slots (zero2.py:99-104's
+ * flatten, per overlap bucket).  src[i]==0: zero fill; empty segments are skipped. */
+int zs_copy_direct(int64_t n, const uint64_t* src, const uint64_t* dst, const int64_t* nbytes,
+                   uintptr_t stream);
 
 /* In-place x[i] /= div over n elements (dtype ZS_F32 / ZS_BF16, x 16-byte aligned): the
  * `param.grad /= dist.get_world_size()` of DDP's sync_gradients (DDP/ddp.py:45-47), applied to a

@@ -37,7 +37,7 @@ def test_library_is_gfx950_code_object():
 def test_abi_version_and_error_text():
     from zero_amd import _lib
 
-    assert _lib.lib.zs_abi_version() == _lib.ABI_VERSION == 10
+    assert _lib.lib.zs_abi_version() == _lib.ABI_VERSION == 11
     h = ctypes.c_void_p()
     rc = _lib.lib.zs_plan_create_ex(0, None, None, 0, 0, 0, 64, 0, 0, ctypes.byref(h))
     assert rc == _lib.ZS_ERR_INVALID
@@ -287,3 +287,22 @@ def test_tune_knobs_validate_and_restore():
     assert lib.zs_tune(b"no_such_knob", 1, None) == _lib.ZS_ERR_INVALID
     assert b"unknown key" in lib.zs_last_error()
     assert lib.zs_tune(None, 1, None) == _lib.ZS_ERR_INVALID
+
+
+def test_copy_direct_validates_without_gpu():
+    """ABI v11's zs_copy_direct: argument checks before any launch; n == 0 and all-empty segments
+    launch nothing."""
+    from zero_amd import _lib
+
+    lib = _lib.lib
+    z = np.zeros(3, np.uint64)
+    assert lib.zs_copy_direct(-1, None, None, None, 0) == _lib.ZS_ERR_INVALID
+    assert lib.zs_copy_direct(0, None, None, None, 0) == _lib.ZS_OK
+    assert lib.zs_copy_direct(3, None, None, None, 0) == _lib.ZS_ERR_INVALID
+    nb = np.array([0, 0, 0], np.int64)
+    assert lib.zs_copy_direct(3, z.ctypes.data, z.ctypes.data, nb.ctypes.data, 0) == _lib.ZS_OK
+    nb = np.array([0, -4, 0], np.int64)
+    assert lib.zs_copy_direct(3, z.ctypes.data, z.ctypes.data, nb.ctypes.data, 0) == _lib.ZS_ERR_INVALID
+    nb = np.array([8, 0, 0], np.int64)
+    assert lib.zs_copy_direct(3, z.ctypes.data, z.ctypes.data, nb.ctypes.data, 0) == _lib.ZS_ERR_INVALID
+    assert b"dst[0] is NULL" in lib.zs_last_error()

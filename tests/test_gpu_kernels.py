@@ -444,3 +444,38 @@ def _convert_case(gpu, n, offset, zo, convert):
     torch.cuda.synchronize()
     b = back.cpu().numpy()
     assert np.array_equal(b[~nan].view(np.uint32), zo.bf16_bits_to_f32(got[~nan]).view(np.uint32))
+
+
+@pytest.mark.parametrize("nt", [-1, 1])
+def test_copy_direct_matches_copyset(gpu, nt):
+    """zs_copy_direct (segments in the kernel arguments, ABI v11) writes exactly what the table
+    copy writes: > 64 segments (several launches), empty and zero-fill segments, unaligned ones."""
+    from zero_amd import _lib
+    from zero_amd.kernels import CopySet, copy_direct
+
+    rng = _seed(7)
+    src = torch.randint(0, 256, (1 << 21,), dtype=torch.uint8, device=gpu)
+    outs = [torch.full((1 << 22,), 7, dtype=torch.uint8, device=gpu) for _ in range(2)]
+    segs, doff = [], 0
+    for k in range(150):
+        ln = int(rng.choice([0, 1, 15, 16, 17, 4096, 65537, 200_000]))
+        align = k % 3 != 0
+        so = int(rng.integers(0, 1000)) * (16 if align else 1)
+        doff = (doff + 15) // 16 * 16 if align else doff + 5
+        segs.append((0 if k % 11 == 4 else so, doff, ln))
+        doff += ln
+    _lib.call("zs_tune", b"copy_nt", nt, None)
+    try:
+        for out, fn in zip(outs, ("set", "direct")):
+            s = [0 if a == 0 and k % 11 == 4 else src.data_ptr() + a for k, (a, _, _) in enumerate(segs)]
+            d = [out.data_ptr() + b for _, b, _ in segs]
+            n = [c for _, _, c in segs]
+            if fn == "set":
+                CopySet(s, d, n).run(torch.cuda.current_stream())
+            else:
+                copy_direct(s, d, n, torch.cuda.current_stream())
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("zs_tune", b"copy_nt", -1, None)
+    assert torch.equal(outs[0], outs[1])
+    assert (outs[1][:doff] != 7).any()

@@ -91,9 +91,10 @@ def test_overlap_unused_param_keeps_value(gpu, pg1):
 @pytest.mark.parametrize("overlap", [False, True])
 def test_zero2_flat_zero_grad_sets_none_then_adopts(gpu, pg1, overlap):
     """ZeRO-2 on the flat arena: zero_grad() leaves p.grad None (the reference's state after
-    zero_grad); backward's fresh gradient lands in its arena slot and p.grad becomes the slot's
-    view; a second backward accumulates in the view (without overlap, which allows it);
-    zero_grad(set_to_none=False) hands out zeroed views; ZeRO-1 keeps zeroed views (its carry)."""
+    zero_grad); backward's fresh gradient lands in its arena slot — with its bucket during backward
+    (overlap: p.grad becomes the slot's view there) or in step() (one zs_copy_direct launch), a
+    second backward accumulating in the fresh tensor first — and p.grad is the slot's view after
+    step(); zero_grad(set_to_none=False) hands out zeroed views; ZeRO-1 keeps zeroed views."""
     from zero_amd import zero1, zero2
 
     ps = [torch.nn.Parameter(torch.randn(64, 8, device=gpu)) for _ in range(3)]
@@ -105,12 +106,14 @@ def test_zero2_flat_zero_grad_sets_none_then_adopts(gpu, pg1, overlap):
     w = [torch.randn(64, 8, device=gpu) for _ in ps]
     sum((p * x).sum() for p, x in zip(ps, w)).backward()
     for i, (p, x) in enumerate(zip(ps, w)):
-        assert eng.is_view(i, p.grad) and torch.equal(p.grad, x)
+        assert eng.is_view(i, p.grad) == overlap and torch.equal(p.grad, x)
     if not overlap:
         sum((p * x).sum() for p, x in zip(ps, w)).backward()
         for p, x in zip(ps, w):
             assert torch.equal(p.grad, x + x)
     opt.step()
+    for i, (p, x) in enumerate(zip(ps, w)):
+        assert eng.is_view(i, p.grad) and torch.equal(p.grad, x if overlap else x + x)
     opt.zero_grad(set_to_none=False)
     assert all(eng.is_view(i, p.grad) and not p.grad.any() for i, p in enumerate(ps))
     q = torch.nn.Parameter(torch.randn(8, device=gpu))
