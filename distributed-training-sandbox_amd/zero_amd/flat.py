@@ -306,13 +306,25 @@ class FlatEngine(ShardEngine):
         zero = np.asarray(zero, np.int64)
         if not len(idx) and not len(zero):
             return
+        # the copy kernel reads numel * es contiguous bytes: anything else (strided, another dtype)
+        # goes through torch's copy into the view
+        dense = np.fromiter((g.is_contiguous() and g.dtype == self.dtype
+                             and g.numel() == int(self.numel[i]) for i, g in zip(idx, grads)),
+                            bool, len(idx))
+        if not dense.all():
+            for i, g in zip(idx[~dense], [g for g, d in zip(grads, dense) if not d]):
+                self.grad_view(int(i)).copy_(g.reshape(self.params[i].shape))
+            grads = [g for g, d in zip(grads, dense) if d]
+            slow, idx = idx[~dense], idx[dense]
+        else:
+            slow = idx[:0]
         all_idx = np.concatenate([idx, zero])
         src = np.concatenate([np.fromiter((_ptr(g) for g in grads), np.uint64, len(idx)),
                               np.zeros(len(zero), np.uint64)])
         dst = np.uint64(self.G.data_ptr()) + (self.slot[all_idx] * self.es).astype(np.uint64)
         copy_direct(src, dst, self.numel[all_idx] * self.es, stream)
         if adopt:
-            for i in idx:
+            for i in np.concatenate([idx, slow]):
                 v = self.grad_view(int(i))
                 self.params[i].grad = v
                 self._views[i] = v
