@@ -38,6 +38,16 @@ def peer_link_peak_gbs(world: int) -> float:
     each rank has one direct link to every peer, so min(world-1, 7) links can carry its traffic
     (one link at N=2, all seven at N=8)."""
     return XGMI_LINK_GBS * max(1, min(world - 1, XGMI_LINKS))
+HANDOFF_WHAT = {
+    "default": ("every step: opt.zero_grad() (every grad None, zero2.py:138-139), fresh gradient "
+                "tensors (two alternating sets), opt.step(); ws = 1: Adam reads them in place "
+                "(zs_adamset_set_grads, no copy); ws > 1: no backward ran, so no hook landed them "
+                "and step() copies them into the arena first"),
+    "views": ("gradients resident in the flat arena's grad views (as the drop-in's hooks leave "
+              "backward's gradients at ws > 1; zero_grad(set_to_none=False) at ws = 1); bucket "
+              "arena: the caller's tensors"),
+}
+
 METRIC = "ZeRO step time & params/sec at 1/2/4/8 GPU; Adam HBM GB/s vs peak"
 
 
@@ -645,6 +655,10 @@ def _zero3_report(args, opt, world, rank, red_dev, el, total, workload, extra):
         }
         if comm is not None:
             out["collectives"] = comm
+        if "expected" in extra:  # the slowest rank's iteration beside the prediction
+            e = extra["expected"]
+            e["measured_ms"] = ms
+            e["measured_over_ideal"] = ms / e["ideal_ms"] if e["ideal_ms"] else None
         out.update(extra)
         if _REHEARSAL[0]:
             out["rehearsal"] = _REHEARSAL[0]
@@ -696,6 +710,87 @@ class ExchangeCheckFailed(RuntimeError):
 
 
 _IN_PROCESS = [False]  # main() called from a test process: raise instead of exiting it
+
+
+NORTH_STAR_ADAM_FRAC = 0.70  # BASELINE.json north_star: fused Adam >= 70 % of peak HBM bandwidth
+NORTH_STAR_BUS_FRAC = 0.60   # ... and reduce-scatter / all-gather >= 60 % of xGMI bus bandwidth
+
+
+def expected_scaling(shapes, zero: int, arena: str, world: int, elem_bytes: int = 2,
+                     adam_bytes_per_elem: int = 26, bucket_mb: float | None = None) -> dict:
+    """The step the planner predicts on ``world`` GPUs, before it is measured (VERDICT r4 #3), for
+    the slowest rank — no overlap credit, like ``step_roofline``:
+
+    * ZeRO-1/2 (Layout R, zero1.py:55-62): HBM = the max-rank optimizer shard x the Adam bytes per
+      element (26 B bf16 split master; ZeRO-1 + 8 B carry), bucket arena + pack and unpack (read +
+      write of every gradient / parameter byte); bus per rank = flat arena: a reduce and a
+      broadcast group of every owner's stream, ring-equivalent 2 x sum_r L_r x es x (N-1)/N; bucket
+      arena: RS / AG of the even buckets at (N-1)/N, per-owner reduce / broadcast of the ragged
+      ones at their message bytes (the accounting bench.py's comm events use);
+    * ZeRO-3 (Layout Z, zero3.py:105-110) hooked iteration: HBM = the max-rank chunks x Adam bytes;
+      bus = forward gather + backward gather + gradient reduce-scatter of every padded chunk,
+      3 x sum_i S_i x N x es x (N-1)/N.
+
+    ``ideal_ms`` = HBM / 8 TB/s + bus / the peer links (min(N-1, 7) x 153 GB/s);
+    ``at_north_star_ms`` = HBM / (70 % of 8 TB/s) + bus / (60 % of the peer links): the step the
+    north star's targets would give (Adam >= 70 % of HBM peak, RS/AG >= 60 % of xGMI busBW)."""
+    import numpy as np
+
+    from zero_amd.plan import Plan
+
+    numels = [int(np.prod(s)) for s in shapes]
+    dim0 = [int(s[0]) if len(s) else 1 for s in shapes]
+    es, ws = int(elem_bytes), int(world)
+    bpe = adam_bytes_per_elem + (8 if zero == 1 and ws > 1 else 0)
+    total = sum(numels)
+    if zero == 3:
+        plan = Plan(numels, ws, 0, "chunk", dim0=dim0, align_elems=64)
+        own = max(int(plan.pieces(r).length.sum()) for r in range(ws))
+        padded = sum(-(-d // ws) * (n // max(d, 1)) for n, d in zip(numels, dim0)) * ws
+        bus = 3 * padded * es * (ws - 1) / ws if ws > 1 else 0.0
+        hbm = bpe * own
+        model = "ZeRO-3: forward + backward gathers and the reduce-scatter of every padded chunk"
+    else:
+        win = 0
+        if arena == "buckets" and ws > 1:
+            win = max(64, int((bucket_mb or 256.0) * (1 << 20)) // (ws * es))
+        plan = Plan(numels, ws, 0, "reference", dim0=dim0, align_elems=64, window_elems=win)
+        own = max(int(plan.pieces(r).length.sum()) for r in range(ws))
+        hbm = bpe * own
+        if ws == 1:
+            bus = 0.0
+        elif arena == "flat":
+            bus = 2 * sum(plan.stream_len(r) for r in range(ws)) * es * (ws - 1) / ws
+        else:
+            hbm += 4 * es * total  # pack + unpack: read + write of every gradient / parameter
+            bus = 0.0
+            for k in range(plan.num_buckets):
+                b = plan.bucket(k)
+                bus += 2 * (b.elems * es * (ws - 1) / ws if b.even else int(b.win_len.sum()) * es)
+        model = f"ZeRO-{zero} {arena} arena"
+    links = peer_link_peak_gbs(ws) * 1e9
+    hbm_ms = hbm / (HBM_PEAK_GBS * 1e9) * 1e3
+    bus_ms = bus / links * 1e3
+    return {"n_gpus": ws, "model": model, "max_rank_adam_gb": bpe * own / 1e9,
+            "hbm_gb_per_rank": hbm / 1e9, "bus_gb_per_rank": bus / 1e9,
+            "ideal_ms": hbm_ms + bus_ms, "ideal_overlapped_ms": max(hbm_ms, bus_ms),
+            "at_north_star_ms": hbm_ms / NORTH_STAR_ADAM_FRAC + bus_ms / NORTH_STAR_BUS_FRAC,
+            "peer_links_gbs": links / 1e9,
+            "note": "planner prediction made before the run (no overlap credit in ideal_ms; "
+                    "ideal_overlapped_ms = the longer of the two)"}
+
+
+def _expected_block(shapes, zero, arena, world, es, bpe, bucket_mb, measured_ms) -> dict:
+    """``expected`` of a bench line: the planner's prediction for this N beside the measured step,
+    and the predicted curve over N = 1, 2, 4, 8 (VERDICT r4 #3)."""
+    e = expected_scaling(shapes, zero, arena, world, es, bpe, bucket_mb)
+    e["measured_ms"] = measured_ms
+    e["measured_over_ideal"] = measured_ms / e["ideal_ms"] if e["ideal_ms"] else None
+    e["curve"] = {str(n): {k: round(v, 3) for k, v in expected_scaling(
+        shapes, zero, arena, n, es, bpe, bucket_mb).items()
+        if k in ("ideal_ms", "ideal_overlapped_ms", "at_north_star_ms", "hbm_gb_per_rank",
+                 "bus_gb_per_rank")} for n in (1, 2, 4, 8)}
+    return e
 
 
 def match_traffic(want: dict, alg_bytes_per_launch: float, traffic_json=None):
@@ -1135,6 +1230,9 @@ def bench_zero3_paramset(args, world, rank, dev, use_nccl):
         dist.destroy_process_group()
         return
     extra = {}
+    # the planner's prediction beside the measured iteration
+    extra["expected"] = _expected_block(shapes, 3, "chunk", world, 2 if args.dtype == "bf16" else 4,
+                                        26 if args.dtype == "bf16" else 28, None, el / args.steps * 1e3)
     if chk is not None:
         extra["rccl_selfcheck"] = chk
     if gather_check is not None:
@@ -1332,6 +1430,16 @@ def main(argv=None):
                     help="N=1 bf16: skip timing the same step with the exact fp32 master beside "
                          "the split-master headline")
     ap.add_argument("--cpu-sample", type=int, default=256 << 20)
+    ap.add_argument("--grad-handoff", default="auto", choices=["auto", "views", "default"],
+                    help="ZeRO-1/2 parameter sets: how the timed step gets its gradients. views: "
+                         "zero_grad(set_to_none=False) once, grads written into the arena's grad "
+                         "views (resident, as a backward into the views leaves them); default: "
+                         "every step opt.zero_grad() (grads None) then fresh gradient tensors "
+                         "(two alternating sets), as backward leaves them after the drop-in's "
+                         "default zero_grad() (zero2.py:138-139); auto: default at N=1, views "
+                         "at N>1 (where the hooks land backward's grads into the views)")
+    ap.add_argument("--no-default-leg", action="store_true",
+                    help="skip timing the other hand-off beside the headline's")
     ap.add_argument("--simulate-ws", type=int, default=0,
                     help="DIAGNOSTIC (N=1 only): run the ws>1 bucket path of rank 0 of a ws-rank job "
                          "with the collectives replaced by no-ops, to time pack / Adam / unpack "
@@ -1466,14 +1574,37 @@ def main(argv=None):
     arenas = ["flat", "buckets"] if (args.arena == "auto" and multi) else \
         [args.arena if args.arena != "auto" else "flat"]
 
-    def build(arena, master=None):
-        o = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), layout=args.layout,
-                                 bucket_mb=args.bucket_mb, sync=False, buckets=args.buckets,
-                                 master=master or args.master, arena=arena, **kw)
-        if o.engine is None:
-            o._build_engine()  # (the bucket engine is otherwise built by the first step)
+    grad_sets = [grads]
+    # what the timed step's gradients look like.  auto: what a training loop calling the drop-in's
+    # default opt.zero_grad() / backward() / step() hands step() — at ws = 1 backward's fresh
+    # tensors (read in place), at ws > 1 the arena's grad views (the hooks land backward's fresh
+    # gradients there during backward); a hand-assigned fresh set at ws > 1 ("default") adds the
+    # landing copy to step() that a real backward overlaps
+    handoff_used = args.grad_handoff
+    if handoff_used == "auto":
+        handoff_used = "default" if not multi else "views"
+
+    def default_step(o):
+        """The drop-in's default hand-off: opt.zero_grad() sets every grad to None, then the
+        step gets fresh gradient tensors (two sets, alternating, so every step sees new
+        addresses, as backward's allocations may be)."""
+        if len(grad_sets) == 1:
+            grad_sets.append([g.clone() for g in grads])
+        k = [0]
+
+        def st():
+            o.zero_grad()
+            for p, g in zip(params, grad_sets[k[0] & 1]):
+                p.grad = g
+            k[0] += 1
+            o.step()
+        return st
+
+    def views_step(o):
+        """Gradients resident in HBM where a backward puts them: the flat arena's grad views (at
+        ws > 1 the drop-in's hooks land backward's fresh gradients there and adopt the views);
+        the bucket arena takes the caller's tensors every step."""
         if getattr(o.engine, "arena_kind", None) == "flat":
-            # grads resident in HBM where a backward puts them: in the arena's grad views
             o.zero_grad(set_to_none=False)
             with torch.no_grad():
                 for p, g in zip(params, grads):
@@ -1486,7 +1617,15 @@ def main(argv=None):
                 for p, g in zip(params, grads):
                     p.grad = g
                 o.step()
-        return o, st
+        return st
+
+    def build(arena, master=None, handoff=None):
+        o = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), layout=args.layout,
+                                 bucket_mb=args.bucket_mb, sync=False, buckets=args.buckets,
+                                 master=master or args.master, arena=arena, **kw)
+        if o.engine is None:
+            o._build_engine()  # (the bucket engine is otherwise built by the first step)
+        return o, (default_step if (handoff or handoff_used) == "default" else views_step)(o)
 
     def timed(st, n):
         torch.cuda.synchronize()
@@ -1595,12 +1734,36 @@ def main(argv=None):
         want["master"] = args.master
     if world > 1 or args.simulate_ws > 1:
         want["arena"] = arena_used
+    if handoff_used == "default":  # Adam reads backward's tensors in place: its own PMC summary
+        want["grad_handoff"] = "default"
     traffic, traffic_src, traffic_note = match_traffic(want, float(stats[2]), args.traffic_json)
 
     placement = {"state": eng.placement, "arena": getattr(eng, "arena_placement", None),
                  "grads": getattr(eng, "grad_placement", None),
                  "reduced": getattr(eng, "reduced_placement", None)}
     bucket_mb, n_buckets = opt._bucket_bytes / (1 << 20), eng.K
+    other_leg = None
+    if not args.no_default_leg and args.simulate_ws <= 1:
+        # the same optimizer through the other gradient hand-off, beside the headline's
+        other = "views" if handoff_used == "default" else "default"
+        _phase(f"{other} hand-off leg")
+        ostep = (default_step if other == "default" else views_step)(opt)
+        for _ in range(args.warmup):
+            ostep()
+        eng.timing_events = []
+        n_o = min(args.steps, 300)
+        ms_o = timed(ostep, n_o)
+        ev_o, eng.timing_events = eng.timing_events, None
+        a_ms = sum(a.elapsed_time(b) for a, b, _ in ev_o)
+        a_b = sum(nb for *_, nb in ev_o)
+        gbs = a_b / (a_ms / 1e3) / 1e9 if a_ms > 0 else 0.0
+        other_leg = {
+            "handoff": other, "ms_per_step": ms_o, "value": total / (ms_o / 1e3), "steps": n_o,
+            "vs_headline": ms_o / ms, "adam_achieved_gbs": gbs, "adam_frac": gbs / HBM_PEAK_GBS,
+            "adam_launches_per_step": len(ev_o) / n_o,
+            "grads_read_in_place": int(getattr(eng, "inplace_reads", 0)) if other == "default" else 0,
+            "what": HANDOFF_WHAT[other]}
+        torch.cuda.synchronize()
     fp32_master = None
     if (world == 1 and args.simulate_ws <= 1 and args.dtype == "bf16" and args.master == "split"
             and not args.no_fp32_master_line):
@@ -1675,7 +1838,8 @@ def main(argv=None):
             "data": "synthetic",
             "config": {
                 "workload": (f"{args.config} {name} synthetic parameter set: ZeRO-{args.zero} "
-                             f"ShardedOptimizer(Adam lr=1e-3).step(), grads resident in HBM"),
+                             f"ShardedOptimizer(Adam lr=1e-3).step(), grads resident in HBM "
+                             f"({handoff_used} hand-off)"),
                 "params": total, "tensors": len(shapes),
                 "param_dtype": args.dtype, "grad_dtype": args.dtype,
                 "state_dtype": ("fp32 exp_avg, exp_avg_sq; fp32 master held as the bf16 param + "
@@ -1699,10 +1863,24 @@ def main(argv=None):
             },
         }
         out["step_roofline"] = step_roofline
+        if args.simulate_ws <= 1 and args.layout == "reference":
+            out["expected"] = _expected_block(shapes, args.zero, arena_used if multi else "flat",
+                                              world, es=2 if args.dtype == "bf16" else 4,
+                                              bpe=26 if (args.dtype == "bf16" and args.master == "split")
+                                              else 28, bucket_mb=bucket_mb, measured_ms=ms)
         out["placement"] = placement
         if fp32_master is not None:
             out["fp32_master_ms_per_step"] = fp32_master["ms_per_step"]
             out["fp32_master"] = fp32_master
+        out["grad_handoff"] = {"handoff": handoff_used, "what": HANDOFF_WHAT[handoff_used]}
+        if handoff_used == "default":
+            out["grad_handoff"]["grads_read_in_place"] = int(getattr(eng, "inplace_reads", 0))
+            out["default_zero_grad_ms_per_step"] = ms
+        if other_leg is not None:
+            out[f"{other_leg['handoff']}_handoff_ms_per_step"] = other_leg["ms_per_step"]
+            out[f"{other_leg['handoff']}_handoff"] = other_leg
+            if other_leg["handoff"] == "default":
+                out["default_zero_grad_ms_per_step"] = other_leg["ms_per_step"]
         if selfcheck is not None:
             out["rccl_selfcheck"] = selfcheck
         if exchange_check:

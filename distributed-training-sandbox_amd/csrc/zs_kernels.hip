@@ -934,7 +934,49 @@ struct zs_adamset {
   int64_t* d_sca_prefix = nullptr;
   int64_t nvec = 0, vec_chunks = 0, nsca = 0, sca_chunks = 0, elems = 0, bytes = 0;
   int g_dtype = ZS_F32, p_dtype = ZS_BF16, has_carry = 0, has_vmax = 0;
+  // zs_adamset_set_grads: which input segment each table entry came from (the scalar entries with
+  // their byte offset into that input's gradient), the gradient each input is bound to now, its
+  // elements, whether it has a vector part (then its gradient must keep the vector alignment), and
+  // the algorithmic bytes of one run without any gradient read
+  int32_t* d_vec_in = nullptr;
+  int32_t* d_sca_in = nullptr;
+  int64_t* d_sca_goff = nullptr;
+  std::vector<uint64_t> in_g;
+  std::vector<int64_t> in_n;
+  std::vector<unsigned char> in_vec;
+  int64_t bytes_no_g = 0;
 };
+
+namespace {
+// zs_adamset_set_grads: new gradient pointers for inputs [k0, k0 + n) of a set, in the kernel
+// arguments (no upload, no host synchronisation), patched into the device tables in stream order.
+constexpr int kGradPatchMax = 224;
+struct GradPatch {
+  uint64_t g[kGradPatchMax];
+  int64_t k0;
+  int n;
+};
+
+__global__ __launch_bounds__(kThreads) void adam_patch_grads_kernel(
+    AdamSeg* __restrict__ vec, const int32_t* __restrict__ vec_in, int64_t nvec,
+    AdamSeg* __restrict__ sca, const int32_t* __restrict__ sca_in,
+    const int64_t* __restrict__ sca_goff, int64_t nsca, const GradPatch p) {
+  for (int64_t j = int64_t(blockIdx.x) * kThreads + threadIdx.x; j < nvec + nsca;
+       j += int64_t(gridDim.x) * kThreads) {
+    if (j < nvec) {
+      const int64_t k = int64_t(vec_in[j]) - p.k0;
+      if (k >= 0 && k < p.n) glob(&vec[j].g)[0] = reinterpret_cast<const void*>(p.g[k]);
+    } else {
+      const int64_t t = j - nvec;
+      const int64_t k = int64_t(sca_in[t]) - p.k0;
+      if (k >= 0 && k < p.n) {
+        const uint64_t g = p.g[k];
+        glob(&sca[t].g)[0] = reinterpret_cast<const void*>(g ? g + uint64_t(sca_goff[t]) : 0);
+      }
+    }
+  }
+}
+}  // namespace
 
 // zs_adam_step's one-range tables: [vector segment, tail segment], prefixes {0, vch, 0, sch}.
 struct AdamTables {
@@ -1423,13 +1465,22 @@ int zs_adamset_create(const zs_adam_seg* in, int64_t n, int g_dtype, int p_dtype
   ZS_REQUIRE(!split || g_dtype == ZS_BF16, "zs_adamset_create: ZS_BF16_SPLIT needs bf16 grads");
   const int64_t msz = split ? 2 : 4;  // bytes per element of master / master_out
   const int64_t gsz = g_dtype == ZS_F32 ? 4 : 2;
+  ZS_REQUIRE(n < (int64_t(1) << 31), "zs_adamset_create: %lld segments (max 2^31 - 1)",
+             (long long)n);
   std::vector<AdamSeg> vec, sca;
   std::vector<int64_t> vpre(1, 0), spre(1, 0);
+  std::vector<int32_t> vec_in, sca_in;
+  std::vector<int64_t> sca_goff;
+  std::vector<uint64_t> in_g(size_t(n), 0);
+  std::vector<int64_t> in_n(size_t(n), 0);
+  std::vector<unsigned char> in_vec(size_t(n), 0);
   int carry_state = -1, vmax_state = -1;
-  int64_t elems = 0, bytes = 0;
+  int64_t elems = 0, bytes = 0, bytes_no_g = 0;
   for (int64_t i = 0; i < n; ++i) {
     const zs_adam_seg& s = in[i];
     ZS_REQUIRE(s.n >= 0, "zs_adamset_create: seg %lld n < 0", (long long)i);
+    in_g[size_t(i)] = s.g;
+    in_n[size_t(i)] = s.n;
     if (s.n == 0) continue;
     ZS_REQUIRE(s.master && s.m && s.v, "zs_adamset_create: seg %lld missing master/m/v",
                (long long)i);
@@ -1460,6 +1511,8 @@ int zs_adamset_create(const zs_adam_seg* in, int64_t n, int g_dtype, int p_dtype
     if (nv) {
       d.n = nv;
       vec.push_back(d);
+      vec_in.push_back(int32_t(i));
+      in_vec[size_t(i)] = 1;
       vpre.push_back(vpre.back() + (nv + adam_chunk(split) - 1) / adam_chunk(split));
     }
     if (nv < s.n) {  // tail (or the whole unaligned segment) through the scalar kernel
@@ -1478,15 +1531,18 @@ int zs_adamset_create(const zs_adam_seg* in, int64_t n, int g_dtype, int p_dtype
       t.carry = adv(d.carry, 4);
       t.n = s.n - nv;
       sca.push_back(t);
+      sca_in.push_back(int32_t(i));
+      sca_goff.push_back(nv * gsz);
       spre.push_back(spre.back() + (t.n + kThreads - 1) / kThreads);
     }
     elems += s.n;
-    int64_t b = (s.g ? gsz : 0) + msz /*master*/ + 8 /*m*/ + 8 /*v*/;
+    int64_t b = msz /*master*/ + 8 /*m*/ + 8 /*v*/;
     if (s.master_out) b += split ? 4 /*residual read + write*/ : 4;
     if (s.p_out) b += 2;
     if (s.vmax) b += 8;
     if (s.carry) b += 8;
-    bytes += b * s.n;
+    bytes_no_g += b * s.n;
+    bytes += (b + (s.g ? gsz : 0)) * s.n;
   }
   zs_adamset* as = new (std::nothrow) zs_adamset();
   if (!as) return zs::fail(ZS_ERR_NOMEM, "zs_adamset_create: out of memory");
@@ -1500,14 +1556,21 @@ int zs_adamset_create(const zs_adam_seg* in, int64_t n, int g_dtype, int p_dtype
   as->p_dtype = p_dtype;
   as->has_carry = carry_state > 0 ? 1 : 0;
   as->has_vmax = vmax_state > 0 ? 1 : 0;
+  as->in_g = std::move(in_g);
+  as->in_n = std::move(in_n);
+  as->in_vec = std::move(in_vec);
+  as->bytes_no_g = bytes_no_g;
   int rc = ZS_OK;
   if (as->nvec) {
     rc = upload(vec, &as->d_vec);
     if (rc == ZS_OK) rc = upload(vpre, &as->d_vec_prefix);
+    if (rc == ZS_OK) rc = upload(vec_in, &as->d_vec_in);
   }
   if (rc == ZS_OK && as->nsca) {
     rc = upload(sca, &as->d_sca);
     if (rc == ZS_OK) rc = upload(spre, &as->d_sca_prefix);
+    if (rc == ZS_OK) rc = upload(sca_in, &as->d_sca_in);
+    if (rc == ZS_OK) rc = upload(sca_goff, &as->d_sca_goff);
   }
   if (rc != ZS_OK) {
     zs_adamset_destroy(as);
@@ -1610,12 +1673,56 @@ int zs_adam_step(float* p, uint16_t* p_bf16, const void* g, int g_dtype, float* 
                          carry, carry_scale, stream);
 }
 
+int zs_adamset_set_grads(zs_adamset* as, int64_t n, const uint64_t* g, uintptr_t stream) {
+  ZS_REQUIRE(as != nullptr, "zs_adamset_set_grads: NULL set");
+  ZS_REQUIRE(n == int64_t(as->in_g.size()),
+             "zs_adamset_set_grads: %lld gradients for a set of %lld segments", (long long)n,
+             (long long)as->in_g.size());
+  ZS_REQUIRE(n == 0 || g != nullptr, "zs_adamset_set_grads: NULL table");
+  const uint64_t galign = as->g_dtype == ZS_F32 ? 16 : 8;
+  int64_t lo = n, hi = -1, g_elems = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    // the set's vector / scalar split was made on the create-time alignment: a gradient of an
+    // input with a vector part must keep it (torch allocations are 512-B aligned)
+    ZS_REQUIRE(!as->in_vec[size_t(i)] || aligned(g[i], galign),
+               "zs_adamset_set_grads: g[%lld] = %#llx is not %llu-byte aligned", (long long)i,
+               (unsigned long long)g[i], (unsigned long long)galign);
+    if (g[i] != as->in_g[size_t(i)]) {
+      lo = std::min(lo, i);
+      hi = i;
+    }
+    if (g[i]) g_elems += as->in_n[size_t(i)];
+  }
+  if (hi < lo) return ZS_OK;  // bound to these gradients already: nothing to launch
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t nseg = as->nvec + as->nsca;
+  const int grid = int(std::max<int64_t>(1, std::min<int64_t>((nseg + kThreads - 1) / kThreads, 64)));
+  for (int64_t k0 = lo; k0 <= hi; k0 += kGradPatchMax) {
+    GradPatch p{};
+    p.k0 = k0;
+    p.n = int(std::min<int64_t>(kGradPatchMax, hi + 1 - k0));
+    for (int k = 0; k < p.n; ++k) p.g[k] = g[k0 + k];
+    if (nseg)
+      hipLaunchKernelGGL(adam_patch_grads_kernel, dim3(grid), dim3(kThreads), 0, st, as->d_vec,
+                         as->d_vec_in, as->nvec, as->d_sca, as->d_sca_in, as->d_sca_goff, as->nsca,
+                         p);
+    ZS_HIP(hipGetLastError());
+  }
+  std::copy(g, g + n, as->in_g.begin());
+  const int64_t gsz = as->g_dtype == ZS_F32 ? 4 : 2;
+  as->bytes = as->bytes_no_g + gsz * g_elems;
+  return ZS_OK;
+}
+
 int zs_adamset_destroy(zs_adamset* as) {
   if (!as) return ZS_OK;
   if (as->d_vec) (void)hipFree(as->d_vec);
   if (as->d_vec_prefix) (void)hipFree(as->d_vec_prefix);
   if (as->d_sca) (void)hipFree(as->d_sca);
   if (as->d_sca_prefix) (void)hipFree(as->d_sca_prefix);
+  if (as->d_vec_in) (void)hipFree(as->d_vec_in);
+  if (as->d_sca_in) (void)hipFree(as->d_sca_in);
+  if (as->d_sca_goff) (void)hipFree(as->d_sca_goff);
   delete as;
   return ZS_OK;
 }

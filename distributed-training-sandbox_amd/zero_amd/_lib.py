@@ -20,7 +20,7 @@ ZS_OK, ZS_ERR_INVALID, ZS_ERR_HIP, ZS_ERR_RCCL, ZS_ERR_NOMEM = 0, 1, 2, 3, 4
 ZS_F32, ZS_BF16, ZS_U8, ZS_BF16_SPLIT = 0, 1, 2, 3
 ZS_LAYOUT_R, ZS_LAYOUT_Z, ZS_LAYOUT_F = 0, 1, 2
 ZS_BUCKETS_RAGGED, ZS_BUCKETS_PADDED = 0, 1
-ABI_VERSION = 11
+ABI_VERSION = 12
 ZS_UNIQUE_ID_BYTES = 128
 
 # Every symbol include/zero_amd.h declares (tests check the library exports all of them).
@@ -33,7 +33,7 @@ EXPORTED = (
     "zs_copyset_create", "zs_copyset_run", "zs_copyset_destroy", "zs_copy_direct", "zs_scale",
     "zs_convert", "zs_fp8_quantize_rows", "zs_fp8_dequantize_rows", "zs_fp8_quantize_rowset",
     "zs_fp8_dequantize_gathered",
-    "zs_adam_hparams_init", "zs_adamset_create", "zs_adamset_run", "zs_adamset_destroy",
+    "zs_adam_hparams_init", "zs_adamset_create", "zs_adamset_run", "zs_adamset_set_grads", "zs_adamset_destroy",
     "zs_adamset_stats", "zs_adam_step", "zs_adam_step_ex",
     "zs_comm_unique_id", "zs_comm_init", "zs_comm_destroy", "zs_reduce_scatter", "zs_all_gather",
     "zs_all_reduce", "zs_reduce", "zs_broadcast", "zs_reduce_group", "zs_broadcast_group", "zs_all_gather_group", "zs_reduce_scatter_group",
@@ -113,6 +113,7 @@ _SIGS = {
     "zs_adamset_create": ([ctypes.POINTER(AdamSeg), _I64, ctypes.c_int, ctypes.c_int,
                            ctypes.POINTER(_P)], ctypes.c_int),
     "zs_adamset_run": ([_P, ctypes.POINTER(AdamHParams), _U], ctypes.c_int),
+    "zs_adamset_set_grads": ([_P, _I64, _P, _U], ctypes.c_int),
     "zs_adamset_destroy": ([_P], ctypes.c_int),
     "zs_adamset_stats": ([_P, _PI64, _PI64], ctypes.c_int),
     "zs_adam_step": ([_P, _P, _P, ctypes.c_int, _P, _P, _I64] + [ctypes.c_float] * 5 +

@@ -236,9 +236,10 @@ class ShardedOptimizerBase:
 
     def zero_grad(self, set_to_none: bool = True):
         if self._flat():
-            # ZeRO-2: None, as the reference's (backward's fresh grads are copied into the arena);
-            # ZeRO-1: zeroed views of the grad arena (its carry follows the surviving views)
-            self.engine.zero_grad(set_to_none=set_to_none and not self._carry)
+            # ZeRO-2 (and ZeRO-1 at ws = 1, which has no carry): None, as the reference's —
+            # backward's fresh grads are then read in place (ws = 1) or landed in the arena;
+            # ZeRO-1 at ws > 1: zeroed views of the grad arena (its carry follows the views)
+            self.engine.zero_grad(set_to_none=set_to_none and not (self._carry and self.world_size > 1))
             return
         if self._overlap:  # grads become zeroed views of the overlap buckets (no pack copy)
             self.engine.gb.install_views()

@@ -399,10 +399,11 @@ class ShardEngine:
         mst = np.uint64(self.master.data_ptr()) + so64 * np.uint64(4)
         return self._adam_rows(idx, g, mst, mst, p_out, so, n)
 
-    def _run_adam(self, tag, rows, param_idx, hparams_of, stream, carry_mul=None):
+    def _run_adam(self, tag, rows, param_idx, hparams_of, stream, carry_mul=None, gptr=None):
         """Partition rows by (group, step, carry multiplier) — torch's bias correction is per param,
         and the ZeRO-1 carry weight depends on which grads survived since the last step — and
-        launch one fused-Adam set per part."""
+        launch one fused-Adam set per part.  ``gptr`` (per row): gradient addresses bound into the
+        sets before they run (AdamSet.set_grads; the rows then carry g = 0)."""
         if len(rows) == 0:
             return
         if carry_mul is None:
@@ -416,6 +417,8 @@ class ShardEngine:
             gz = getattr(self, "czdtype", self.zdtype)  # dtype of the reduced grad Adam reads
             aset = self._cached(("adam", tag, gidx, len(sel), int(sel[0])), sub.tobytes(),
                                 lambda: AdamSet(sub, gz, self.p_dtype))
+            if gptr is not None:
+                aset.set_grads(np.asarray(gptr, np.uint64)[sel], stream)
             hpd = hparams_of(gidx)
             if hpd["amsgrad"] and self.vmax is None:
                 raise RuntimeError("amsgrad state buffer missing")
@@ -461,7 +464,7 @@ class ShardEngine:
         elif self.ws == 1:
             self._step_local(gptr, has, hparams_of, stream)
         else:
-            self._step_buckets(gptr, has, hparams_of, stream)
+            self._step_buckets(gptr, has, hparams_of, stream, grads)
 
     def _step_local(self, gptr, has, hparams_of, stream):
         pc = self.pieces
@@ -524,7 +527,9 @@ class ShardEngine:
             e1.record(cs)
             self.comm_events.append((kind, bool(b.even), e0, e1, bus))
 
-    def _step_buckets(self, gptr, has, hparams_of, stream):
+    def _step_buckets(self, gptr, has, hparams_of, stream, grads=()):
+        from .kernels import CHECK_EXTENTS
+
         if self.arena is None:
             self.arena, self.arena_placement = probed_zeros(self.plan.arena_elems, self.dtype,
                                                             self.device, self.placement_tries)
@@ -544,7 +549,8 @@ class ShardEngine:
                     nb.append(s.length * self.es)
                 src, dst, nb = np.concatenate(src), np.concatenate(dst), np.concatenate(nb)
                 sig = src.tobytes() + dst.tobytes()
-                pack = self._cached(("pack", gi), sig, lambda: CopySet(src, dst, nb))
+                pack = self._cached(("pack", gi), sig, lambda: CopySet(
+                    src, dst, nb, bounds=(list(grads), [self.arena]) if CHECK_EXTENTS else None))
                 self._run_copy("pack", pack, stream)
                 for k in grp:
                     self.ev_pack[k].record(stream)
@@ -594,7 +600,8 @@ class ShardEngine:
                     nb.append(s.length * self.es)
                 src, dst, nb = np.concatenate(src), np.concatenate(dst), np.concatenate(nb)
                 unpack = self._cached(("unpack", gi), src.tobytes() + dst.tobytes(),
-                                      lambda: CopySet(src, dst, nb))
+                                      lambda: CopySet(src, dst, nb, bounds=(
+                                          [self.arena], self.params) if CHECK_EXTENTS else None))
                 self._run_copy("unpack", unpack, stream)
 
     # ------------------------------------------------------------------------------------------

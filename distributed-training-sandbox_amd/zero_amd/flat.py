@@ -43,9 +43,10 @@ import torch
 from . import _lib
 from ._hooks import WeakCall
 from .engine import ALIGN_ELEMS, ShardEngine, _ptr
-from .kernels import copy_direct
+from .kernels import check_extents, check_extents_enabled, copy_direct
 
 _I32P = np.int32
+LAND_BATCH_BYTES = 64 << 20  # fresh gradients landed per hook batch (ws > 1, no overlap)
 
 
 class _Round:
@@ -93,7 +94,6 @@ class FlatEngine(ShardEngine):
                 s = int(self.slot[i])
                 self.P[s:s + int(self.numel[i])].copy_(p.detach().reshape(-1))
                 p.data = self.P[s:s + int(self.numel[i])].view(p.shape)
-        self.G, self.grad_placement = _zeros_placed(total, dt, dev, placement_tries)
         # bf16 gradient exchange for fp32 parameters: G is converted into Gc
         # (bf16, same layout) before the reduces, which then move and sum 2 B per element; Adam
         # reads the bf16 sum (its fp32 master is the fp32 parameter itself)
@@ -102,12 +102,20 @@ class FlatEngine(ShardEngine):
         self.grad_comm = grad_comm if dt == torch.float32 else None
         if grad_comm == "bf16" and dt != torch.float32:
             raise ValueError("grad_comm='bf16' is for fp32 parameters (bf16 grads already are)")
+        # ws == 1 (no bf16 exchange): nothing to reduce, so Adam reads every gradient where it is —
+        # the arena view, or the fresh tensor backward left after a set-to-None zero_grad(), in
+        # place (zero2.py:120 reads p.grad as backward left it): no landing copy, and G exists
+        # only once a caller asks for grad views (zero_grad(set_to_none=False), ZeRO-1's views)
+        self.inplace = ws == 1 and self.grad_comm is None
+        self.G, self.grad_placement = None, None
+        self._total = total
+        if not self.inplace:
+            self._ensure_G()
         cdt = torch.bfloat16 if self.grad_comm else dt
         self.Gc = torch.zeros(total, dtype=cdt, device=dev) if self.grad_comm else self.G
-        self.ces = self.Gc.element_size()
+        self.ces = torch.empty((), dtype=cdt).element_size()
         self.czdtype = _lib.ZS_BF16 if self.grad_comm else self.zdtype
-        # ws == 1: nothing to reduce — Adam reads the gradient arena itself (R aliases Gc) and the
-        # step is one round with no collective; the arena still places P and G by probe
+        # ws == 1 with the bf16 exchange: Adam reads Gc (R aliases it), one round, no collective
         self.reduced_placement = None
         if ws == 1:
             self.R = self.Gc
@@ -145,13 +153,36 @@ class FlatEngine(ShardEngine):
         self.overlap = False  # backward-overlapped reduces (enable_overlap)
         self.ov_K = 0
         self.launched_in_backward = 0
+        # ws > 1 without overlap: fresh gradients are landed from the post-accumulate hooks in
+        # batches of about this many bytes (and adopted), so backward never holds G plus a full
+        # set of fresh gradients (the reference holds one set)
+        self.land_batch_bytes = LAND_BATCH_BYTES
+        self.land_pending, self.land_pending_bytes = [], 0
+        self.inplace_reads = 0  # gradients the last step's Adam read in place (ws == 1)
+
+    # ------------------------------------------------------------------------------------------
+    def _ensure_G(self):
+        """The gradient arena (placed by probe), allocated at construction when ws > 1 and on first
+        use at ws == 1 (grad views handed out, or a gradient Adam cannot read in place)."""
+        if self.G is None:
+            self.G, self.grad_placement = _zeros_placed(self._total, self.dtype, self.device,
+                                                        self.placement_tries)
+            if getattr(self, "grad_comm", None) is None and hasattr(self, "Gc"):
+                self.Gc = self.G
+                if self.ws == 1:
+                    self.R = self.G
+        return self.G
 
     # ------------------------------------------------------------------------------------------
     def _make_round(self, j: int) -> _Round:
         ws, es, W, r0 = self.ws, self.es, self.W, self.rank
         lo = j * W
         count = np.clip(self.Ls - lo, 0, W)
-        gb, pb, rb = self.Gc.data_ptr(), self.P.data_ptr(), self.R.data_ptr()
+        pb = self.P.data_ptr()
+        # in place (ws == 1): the rows' gradients are bound per step (AdamSet.set_grads); 0 here
+        gb = rb = 0 if self.inplace else None
+        if gb is None:
+            gb, rb = self.Gc.data_ptr(), self.R.data_ptr()
         ces = self.ces  # element size on the wire (bf16 exchange of fp32 grads: 2)
         send = np.uint64(gb) + ((self.base + lo) * ces).astype(np.uint64)
         recv = send.copy()
@@ -166,7 +197,7 @@ class FlatEngine(ShardEngine):
         idx, a, b = pc.param[keep], a[keep], b[keep]
         so = a.astype(np.int64)
         ln = (b - a).astype(np.int64)
-        g = np.uint64(rb) + (so * ces).astype(np.uint64)
+        g = np.zeros(len(so), np.uint64) if self.inplace else np.uint64(rb) + (so * ces).astype(np.uint64)
         pslot = np.uint64(pb) + ((self.base[r0] + so) * es).astype(np.uint64)
         if self.mixed:  # master from P (split: + residual) or the fp32 master; bf16 param out to P
             rows = self._mixed_rows(idx, g, pslot, pslot, so, ln)
@@ -179,10 +210,15 @@ class FlatEngine(ShardEngine):
         return buf[s:s + n].view(self.params[i].shape)
 
     def grad_view(self, i: int) -> torch.Tensor:
-        return self.slot_view(self.G, i)
+        return self.slot_view(self._ensure_G(), i)
+
+    def grad_slot_ptrs(self, idx) -> np.ndarray:
+        """Device addresses of the G slots of parameters ``idx``."""
+        idx = np.asarray(idx, np.int64)
+        return np.uint64(self._ensure_G().data_ptr()) + (self.slot[idx] * self.es).astype(np.uint64)
 
     def is_view(self, i: int, g) -> bool:
-        if g is None:
+        if g is None or self.G is None:
             return False
         if g is self._views[i]:
             return True
@@ -198,19 +234,22 @@ class FlatEngine(ShardEngine):
     def zero_grad(self, set_to_none: bool = False):
         """The wrapper's zero_grad().  ``set_to_none`` (ZeRO-2): every p.grad becomes None, as the
         reference's zero_grad leaves them (zero2.py:113 + the inner optimizer's zero_grad), and G
-        keeps its stale values (``dirty``): backward then hands over fresh gradients, which are
-        copied into their slots — by the post-accumulate hook in overlap mode, by one copy launch
-        in step() otherwise — 4 B per bf16 element, where zeroing G and accumulating into its views
-        costs 8 (a memset plus an in-place add).  Otherwise (ZeRO-1, whose carry needs the views to
-        survive, or ``set_to_none=False``): G is zeroed and every p.grad made its arena view."""
+        keeps its stale values (``dirty``): backward then hands over fresh gradients.  At ws == 1
+        Adam reads them in place (no copy at all); at ws > 1 they are copied into their slots and
+        p.grad becomes the slot's view — from the post-accumulate hooks, per overlap bucket in
+        overlap mode and in batches of ``land_batch_bytes`` otherwise — 4 B per bf16 element,
+        where zeroing G and accumulating into its views costs 8 (a memset plus an in-place add).
+        Otherwise (ZeRO-1 at ws > 1, whose carry needs the views to survive, or
+        ``set_to_none=False``): G is zeroed and every p.grad made its arena view."""
         if set_to_none:
             for i, p in enumerate(self.params):
                 p.grad = None
                 self._views[i] = None
         else:
-            self.G.zero_()
+            self._ensure_G().zero_()
             self.dirty[:] = False
             self.install_views()
+        self.land_pending, self.land_pending_bytes = [], 0
         self.zero_grad_calls += 1
         self.touched[:] = False
         self.any_touched = False
@@ -237,15 +276,18 @@ class FlatEngine(ShardEngine):
             rd.sets = sets
         return sets
 
-    def _adam_round_fast(self, rd: _Round, hps, stream) -> bool:
+    def _adam_round_fast(self, rd: _Round, hps, stream, gptr=None) -> bool:
         """Launch the round's static sets if every param in them shares its group's (step,
-        carry) key this step; returns False to fall back to the general partitioning."""
+        carry) key this step; returns False to fall back to the general partitioning.  ``gptr``
+        (in place, ws == 1): every parameter's gradient address, bound into the sets first."""
         sets = self._static_sets(rd)
         for gi, idx, aset in sets:
             hp = hps.get(gi)
             if hp is None:
                 return False
         for gi, idx, aset in sets:
+            if gptr is not None:
+                aset.set_grads(gptr[idx], stream)
             if self.timing_events is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
@@ -294,6 +336,27 @@ class FlatEngine(ShardEngine):
     def _mark(self, i: int):
         self.touched[i] = True
         self.any_touched = True
+        if self.inplace or not self.adopt_fresh:
+            return  # ws == 1 reads fresh grads in place; ZeRO-1's carry needs the caller's tensors
+        g = self.params[i].grad
+        if g is not None and not self.is_view(i, g):  # fresh: land with the next batch
+            self.land_pending.append(i)
+            self.land_pending_bytes += g.numel() * g.element_size()
+            if self.land_pending_bytes >= self.land_batch_bytes:
+                self._land_pending()
+
+    def _land_pending(self, stream=None):
+        """Copy the fresh gradients the hooks collected into their G slots (one zs_copy_direct on
+        the stream backward produced them on) and make the slots their p.grad: the fresh tensors
+        return to the allocator, stream-ordered after the copy."""
+        idx = self.land_pending
+        if not idx:
+            return
+        self.land_pending, self.land_pending_bytes = [], 0
+        cur = torch.cuda.current_stream(self.device) if stream is None else stream
+        live = [i for i in idx if self.params[i].grad is not None
+                and not self.is_view(i, self.params[i].grad)]
+        self._land(live, [self.params[i].grad for i in live], (), cur, adopt=True)
 
     def _land(self, idx, grads, zero, stream, adopt: bool):
         """Fresh gradients ``grads`` of parameters ``idx`` (not arena views: zero_grad set p.grad
@@ -321,8 +384,12 @@ class FlatEngine(ShardEngine):
         all_idx = np.concatenate([idx, zero])
         src = np.concatenate([np.fromiter((_ptr(g) for g in grads), np.uint64, len(idx)),
                               np.zeros(len(zero), np.uint64)])
-        dst = np.uint64(self.G.data_ptr()) + (self.slot[all_idx] * self.es).astype(np.uint64)
-        copy_direct(src, dst, self.numel[all_idx] * self.es, stream)
+        dst = self.grad_slot_ptrs(all_idx)
+        nbytes = self.numel[all_idx] * self.es
+        if check_extents_enabled():  # every segment inside its tensors (tests turn this on)
+            check_extents(src[:len(idx)], nbytes[:len(idx)], grads, "grad")
+            check_extents(dst, nbytes, [self.G], "G slot")
+        copy_direct(src, dst, nbytes, stream)
         if adopt:
             for i in np.concatenate([idx, slow]):
                 v = self.grad_view(int(i))
@@ -423,8 +490,10 @@ class FlatEngine(ShardEngine):
         self.touched[i] = True
         self.any_touched = True
         g = self.params[i].grad
-        if g is not None and not self.is_view(i, g):  # fresh (zero_grad set it to None): landed
-            self.ov_fresh[self.ov_bucket_of[i]].append(i)  # with its bucket, one copy launch
+        # fresh (zero_grad set it to None): landed with its bucket, one copy launch (ws == 1: read
+        # in place by step())
+        if g is not None and not self.inplace and not self.is_view(i, g):
+            self.ov_fresh[self.ov_bucket_of[i]].append(i)
         self.ov_pending[self.ov_bucket_of[i]] -= 1
         while self.ov_next < self.ov_K and self.ov_pending[self.ov_next] == 0:
             self._ov_launch(self.ov_next)
@@ -513,6 +582,12 @@ class FlatEngine(ShardEngine):
         stream = torch.cuda.current_stream(self.device) if stream is None else stream
         n = len(self.params)
         es = self.es
+        if self.land_pending:  # the hooks' last partial batch (ws > 1): land it, grads become views
+            pend = list(self.land_pending)
+            self._land_pending(stream)
+            grads = list(grads)
+            for i in pend:
+                grads[i] = self.params[i].grad
         vw = self._views
         view = np.fromiter((g is not None and (g is vw[i] or self.is_view(i, g))
                             for i, g in enumerate(grads)), bool, n)
@@ -528,10 +603,13 @@ class FlatEngine(ShardEngine):
             self.ensure_vmax()
             self.rebuild_rows()
         self.ev_c0.record(stream)
-        # gradients not accumulated into the arena (assigned tensors, fresh grads after the caller
-        # cleared the views) are copied in; a stale slot whose grad is gone is zero-filled
-        # (overlap mode: in _step_overlap, for the parameters no hook has handled)
-        if not self.overlap:
+        gptr = None
+        if self.inplace:  # ws == 1: every gradient read where it is (the odd one landed first)
+            gptr = self._bind_inplace(grads, has, view, stream)
+        elif not self.overlap:
+            # gradients not accumulated into the arena (assigned tensors, fresh grads the hooks
+            # did not land) are copied in; a stale slot whose grad is gone is zero-filled
+            # (overlap mode: in _step_overlap, for the parameters no hook has handled)
             copy = np.nonzero(has & ~view)[0]
             self._land(copy, [grads[i] for i in copy], np.nonzero(~has & self.dirty)[0], stream,
                        adopt=False)  # (_reinstall makes them views after the step)
@@ -560,7 +638,7 @@ class FlatEngine(ShardEngine):
                     decoupled=h["decoupled"], amsgrad=h["amsgrad"], maximize=h["maximize"],
                     grad_div=float(self.ws),
                     carry_mul=float(cm[0]) if self.carry is not None else 0.0)
-        if self.overlap:
+        if self.overlap and not self.inplace:
             self._step_overlap(grads, has, view, cmul, hps, hparams_of, stream)
             return
         if self.grad_comm:  # the exchange moves bf16: convert every local grad once (2 launches' worth
@@ -570,11 +648,16 @@ class FlatEngine(ShardEngine):
         if self.ws == 1:  # zero1.py:107-108 / zero2.py:120 at ws=1: Adam on the local grads
             with _lib.phase_range("optimizer_step"):
                 for rd in self.rounds:
-                    if len(rd.idx) and not (hps and self._adam_round_fast(rd, hps, stream)):
+                    if len(rd.idx) and not (hps and self._adam_round_fast(rd, hps, stream, gptr)):
                         live = has[rd.idx]
                         rows, idx = (rd.rows, rd.idx) if live.all() else (rd.rows[live], rd.idx[live])
                         self._run_adam(("flat", rd.j), rows, idx, hparams_of, stream,
-                                       carry_mul=cmul[idx])
+                                       carry_mul=cmul[idx],
+                                       gptr=None if gptr is None else gptr[idx])
+            if self.inplace:
+                if self.overlap:
+                    self._ov_reset()
+                return  # fresh gradients stay the caller's p.grad (read in place)
             self._reinstall(has, view)
             return
         self.ev_grads.record(stream)
@@ -608,6 +691,28 @@ class FlatEngine(ShardEngine):
                 self._timed_end(e0, cs, "ag", int(rd.count.sum()))
         stream.wait_event(self.ev_bc[self.K - 1])  # the parameters are P: next forward reads it
         self._reinstall(has, view)
+
+    def _bind_inplace(self, grads, has, view, stream) -> np.ndarray:
+        """ws == 1: the gradient address Adam reads per parameter (0 = none): an arena view's slot,
+        a fresh tensor itself (zero2.py:120 reads p.grad where backward left it) — or, for a
+        gradient the vector kernel cannot read in place (misaligned), its G slot after a copy,
+        p.grad then becoming the slot's view."""
+        n = len(self.params)
+        gptr = np.zeros(n, np.uint64)
+        align = 8 if self.dtype == torch.bfloat16 else 16
+        fresh = np.nonzero(has & ~view)[0]
+        ptrs = np.fromiter((_ptr(grads[i]) for i in fresh), np.uint64, len(fresh))
+        ok = (ptrs % np.uint64(align)) == 0
+        gptr[fresh[ok]] = ptrs[ok]
+        odd = fresh[~ok]
+        if len(odd):
+            self._land(odd, [grads[i] for i in odd], (), stream, adopt=True)
+        slots = np.nonzero(has & view)[0]
+        if len(slots) or len(odd):
+            both = np.concatenate([slots, odd]).astype(np.int64)
+            gptr[both] = self.grad_slot_ptrs(both)
+        self.inplace_reads = int(ok.sum())
+        return gptr
 
     def _reinstall(self, has, view):
         """Every p.grad is (again) its arena view, holding this step's local gradient."""

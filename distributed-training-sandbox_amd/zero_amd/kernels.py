@@ -11,6 +11,7 @@ They raise ``ZeroAmdError`` on any failure; there is no CPU path.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -26,14 +27,62 @@ def stream_handle(stream) -> int:
     return int(stream) if isinstance(stream, int) else int(stream.cuda_stream)
 
 
-class CopySet:
-    """Copy ``nbytes[i]`` bytes from ``src[i]`` to ``dst[i]`` (src 0 = zero fill)."""
+# Segment tables built from tensors are checked against those tensors' storage before anything is
+# launched when this is on (``ZERO_AMD_CHECK_EXTENTS=1``; tests/conftest.py sets it): the raw-pointer
+# entry points cannot check, and one segment past its buffer faults the device and fails every
+# later call in the process (the r04 session that lost a whole suite to one bad table).
+CHECK_EXTENTS = os.environ.get("ZERO_AMD_CHECK_EXTENTS", "0") not in ("", "0")
 
-    def __init__(self, src, dst, nbytes):
+
+def check_extents_enabled() -> bool:
+    return CHECK_EXTENTS
+
+
+def check_extents(ptrs, nbytes, tensors, what: str = "segment") -> None:
+    """Raise ``ValueError`` unless every segment [ptrs[i], ptrs[i] + nbytes[i]) with nbytes > 0 and
+    ptrs != 0 (0 = zero fill) lies inside the storage of one of ``tensors`` (None entries ignored)."""
+    ptrs = np.asarray(ptrs, dtype=np.uint64).reshape(-1)
+    nb = np.asarray(nbytes, dtype=np.int64).reshape(-1)
+    if ptrs.shape != nb.shape:
+        raise ValueError(f"zero_amd: {what}: {ptrs.size} pointers for {nb.size} lengths")
+    if (nb < 0).any():
+        raise ValueError(f"zero_amd: {what}: negative length")
+    live = (nb > 0) & (ptrs != 0)
+    if not live.any():
+        return
+    spans = sorted({(int(t.untyped_storage().data_ptr()), int(t.untyped_storage().nbytes()))
+                    for t in tensors if t is not None})
+    if not spans:
+        raise ValueError(f"zero_amd: {what}: no tensors to check the segments against")
+    lo = np.array([s for s, _ in spans], np.uint64)
+    hi = lo + np.array([n for _, n in spans], np.uint64)
+    p, n = ptrs[live], nb[live].astype(np.uint64)
+    k = np.searchsorted(lo, p, side="right") - 1
+    ok = (k >= 0) & (p + n <= hi[np.maximum(k, 0)])
+    if not ok.all():
+        j = int(np.nonzero(~ok)[0][0])
+        raise ValueError(f"zero_amd: {what} {int(np.nonzero(live)[0][j])}: [{int(p[j]):#x}, +{int(n[j])}) "
+                         "is outside every buffer it may touch (the copy was not launched)")
+
+
+def _check_bounds(src, dst, nb, bounds):
+    if bounds is not None and CHECK_EXTENTS:
+        src_t, dst_t = bounds
+        check_extents(src, nb, src_t, "source segment")
+        check_extents(dst, nb, dst_t, "destination segment")
+
+
+class CopySet:
+    """Copy ``nbytes[i]`` bytes from ``src[i]`` to ``dst[i]`` (src 0 = zero fill).  ``bounds``:
+    (source tensors, destination tensors) the segments must lie in, checked when
+    ``CHECK_EXTENTS`` is on."""
+
+    def __init__(self, src, dst, nbytes, bounds=None):
         src = np.ascontiguousarray(np.asarray(src, dtype=np.uint64))
         dst = np.ascontiguousarray(np.asarray(dst, dtype=np.uint64))
         nb = np.ascontiguousarray(np.asarray(nbytes, dtype=np.int64))
         assert src.shape == dst.shape == nb.shape
+        _check_bounds(src, dst, nb, bounds)
         self.nbytes = int(nb.sum()) if nb.size else 0
         self.nseg = int(nb.size)
         h = ctypes.c_void_p()
@@ -54,14 +103,15 @@ class CopySet:
             self._h = None
 
 
-def copy_direct(src, dst, nbytes, stream) -> None:
+def copy_direct(src, dst, nbytes, stream, bounds=None) -> None:
     """Copy ``nbytes[i]`` bytes from ``src[i]`` to ``dst[i]`` (src 0 = zero fill) with the segments
     in the kernel arguments (zs_copy_direct): nothing uploaded, so for pointers that change on
-    every call (backward's fresh gradients)."""
+    every call (backward's fresh gradients).  ``bounds`` as for ``CopySet``."""
     src = np.ascontiguousarray(np.asarray(src, dtype=np.uint64))
     dst = np.ascontiguousarray(np.asarray(dst, dtype=np.uint64))
     nb = np.ascontiguousarray(np.asarray(nbytes, dtype=np.int64))
     assert src.shape == dst.shape == nb.shape
+    _check_bounds(src, dst, nb, bounds)
     if nb.size:
         _lib.call("zs_copy_direct", int(nb.size), src.ctypes.data, dst.ctypes.data, nb.ctypes.data,
                   stream_handle(stream))
@@ -89,9 +139,25 @@ class AdamSet:
         h = ctypes.c_void_p()
         _lib.call("zs_adamset_create", arr, len(segs), int(g_dtype), int(p_dtype), ctypes.byref(h))
         self._h = h
+        self.nseg = len(segs)
+        self._g = np.ascontiguousarray(segs[:, 0])  # the gradients bound now, per input row
+        self._stats()
+
+    def _stats(self):
         e, b = ctypes.c_int64(), ctypes.c_int64()
         _lib.call("zs_adamset_stats", self._h, ctypes.byref(e), ctypes.byref(b))
         self.elems, self.bytes = e.value, b.value
+
+    def set_grads(self, g: np.ndarray, stream) -> None:
+        """Re-point row i's gradient to ``g[i]`` (0 = none) in stream order (zs_adamset_set_grads:
+        a patch kernel on ``stream`` when any pointer changed, nothing otherwise)."""
+        g = np.ascontiguousarray(np.asarray(g, dtype=np.uint64))
+        assert g.shape == (self.nseg,)
+        if np.array_equal(g, self._g):
+            return
+        _lib.call("zs_adamset_set_grads", self._h, self.nseg, g.ctypes.data, stream_handle(stream))
+        self._g = g
+        self._stats()
 
     def run(self, hp: AdamHParams, stream) -> None:
         _lib.call("zs_adamset_run", self._h, ctypes.byref(hp), stream_handle(stream))

@@ -8,10 +8,17 @@ exactly data-parallel Adam.
 
 Here:
   * default ``arena="flat"``: every parameter is a view of one owner-major *flat parameter
-    arena* (rank r's owned parameters, Layout R, are the contiguous stretch [base_r, base_r+L_r)),
-    and every gradient lands in a flat gradient arena of the same layout: ``zero_grad()`` sets
-    the grads to None (as the reference's), and each fresh gradient backward produces is copied
-    into its slot by a post-accumulate-grad hook, ``p.grad`` becoming the slot's view.  A step is a few *rounds* (window j of every
+    arena* (rank r's owned parameters, Layout R, are the contiguous stretch [base_r, base_r+L_r)).
+    ``zero_grad()`` sets the grads to None (as the reference's), and what happens to the fresh
+    gradients backward then produces depends on the world size:
+      - ws = 1: nothing is exchanged, so Adam reads them in place where backward left them (the
+        fused-Adam tables re-pointed in stream order, ``zs_adamset_set_grads``); no copy, and no
+        gradient arena unless the caller asks for grad views (``zero_grad(set_to_none=False)``);
+      - ws > 1: they are copied into a flat gradient arena of the same layout from the
+        post-accumulate-grad hooks — one copy launch per overlap bucket with ``overlap=True``,
+        per batch of ``land_batch_bytes`` (64 MiB) otherwise — and ``p.grad`` becomes the slot's
+        view, so backward never holds the arena plus a whole second set of gradients.
+    A step at ws > 1 is a few *rounds* (window j of every
     owner's stretch): ONE RCCL group of per-owner ``ncclReduce`` — each owner's window of the
     gradient arena summed into its reduced buffer, the reduce-scatter-v of zero2.py:94-113 —, the
     fused HIP Adam on the own window (``/ws`` folded in) writing the updated parameters straight

@@ -29,7 +29,7 @@ extern "C" {
  * the *_ex entry points), so a caller built against an older header links and then passes the
  * wrong arguments.  The Python binding (zero_amd/_lib.py) and tests/c/abi_host.c refuse a
  * mismatch. */
-#define ZS_ABI_VERSION 11
+#define ZS_ABI_VERSION 12
 
 enum zs_status {
   ZS_OK = 0,
@@ -262,8 +262,20 @@ typedef struct zs_adamset zs_adamset;
 int zs_adamset_create(const zs_adam_seg* segs, int64_t n, int g_dtype, int p_dtype,
                       zs_adamset** out);
 int zs_adamset_run(const zs_adamset* as, const zs_adam_hparams* hp, uintptr_t stream);
+/* Re-point the set's gradients (ABI v12): g[i] (0 = zero gradient) replaces the g of the i-th
+ * segment given to zs_adamset_create (n = that count).  The new pointers travel in the arguments
+ * of a small patch kernel enqueued on `stream`, which rewrites the device tables in stream order:
+ * no upload, no host synchronisation, nothing launched when every pointer is unchanged.  Runs of
+ * the set enqueued on `stream` afterwards read the new gradients; the set must not run on another
+ * stream concurrently.  A segment with a vector part needs its new g aligned as at creation (8 B
+ * bf16, 16 B fp32), else ZS_ERR_INVALID and nothing is changed.  The reference's `step()` reads
+ * `p.grad` wherever backward left it after `zero_grad()` (zero2.py:94-120, 138-139): at world
+ * size 1 the update reads those fresh gradient tensors in place instead of copying them into an
+ * arena first. */
+int zs_adamset_set_grads(zs_adamset* as, int64_t n, const uint64_t* g, uintptr_t stream);
 int zs_adamset_destroy(zs_adamset* as);
-/* total elements covered by the set and algorithmic HBM bytes one run moves */
+/* total elements covered by the set and algorithmic HBM bytes one run moves (with the gradients
+ * bound now) */
 int zs_adamset_stats(const zs_adamset* as, int64_t* elems, int64_t* bytes);
 
 /* Single-range form, SURVEY.md §8(b)'s signature: one torch.optim.Adam/AdamW step over n

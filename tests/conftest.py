@@ -11,6 +11,9 @@ for p in (str(REPO), str(PKG), str(REPO / "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+# every segment table the Python side builds from tensors is checked against their storage before
+# launch (zero_amd/kernels.py CHECK_EXTENTS): an out-of-range segment raises instead of faulting
+os.environ.setdefault("ZERO_AMD_CHECK_EXTENTS", "1")
 # This process (single-process kernel tests, rank 0 of the multi-rank ones) runs at the box's
 # default number of HIP hardware queues; only the ranks spawned beside it are given two
 # (tests/_zero_run.py CHILD_ENV), so up to 8 processes on the one GPU stay within the queues the

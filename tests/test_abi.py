@@ -37,7 +37,7 @@ def test_library_is_gfx950_code_object():
 def test_abi_version_and_error_text():
     from zero_amd import _lib
 
-    assert _lib.lib.zs_abi_version() == _lib.ABI_VERSION == 11
+    assert _lib.lib.zs_abi_version() == _lib.ABI_VERSION == 12
     h = ctypes.c_void_p()
     rc = _lib.lib.zs_plan_create_ex(0, None, None, 0, 0, 0, 64, 0, 0, ctypes.byref(h))
     assert rc == _lib.ZS_ERR_INVALID
@@ -306,3 +306,48 @@ def test_copy_direct_validates_without_gpu():
     nb = np.array([8, 0, 0], np.int64)
     assert lib.zs_copy_direct(3, z.ctypes.data, z.ctypes.data, nb.ctypes.data, 0) == _lib.ZS_ERR_INVALID
     assert b"dst[0] is NULL" in lib.zs_last_error()
+
+
+def test_table_wrappers_refuse_out_of_range_segments_without_gpu():
+    """the wrappers that build copy tables from tensors check every segment against
+    the tensors' storage first (CHECK_EXTENTS, on in tests): a segment past its buffer raises a
+    Python exception and nothing reaches the raw-pointer entry points (CPU tensors here: the check
+    runs before any HIP call)."""
+    import pytest
+    import torch
+
+    from zero_amd import kernels
+
+    assert kernels.check_extents_enabled()  # tests/conftest.py turns it on
+    src = torch.zeros(1000, dtype=torch.uint8)
+    dst = torch.zeros(4 << 20, dtype=torch.uint8)
+    ok = ([src.data_ptr()], [dst.data_ptr() + 100], [1000])
+    kernels.check_extents(ok[0], ok[2], [src], "src")
+    kernels.check_extents(ok[1], ok[2], [dst], "dst")
+    # r04s's fault: segments packed past a 4 MiB destination
+    over = ([src.data_ptr()], [dst.data_ptr() + (4 << 20) - 10], [1000])
+    with pytest.raises(ValueError, match="outside every buffer"):
+        kernels.copy_direct(*over, 0, bounds=([src], [dst]))
+    with pytest.raises(ValueError, match="outside every buffer"):
+        kernels.CopySet(*over, bounds=([src], [dst]))
+    # a source read past its tensor, a pointer before every buffer, a negative length
+    with pytest.raises(ValueError):
+        kernels.check_extents([src.data_ptr() + 1], [1000], [src])
+    with pytest.raises(ValueError):
+        kernels.check_extents([src.data_ptr() - 16], [8], [src, dst])
+    with pytest.raises(ValueError, match="negative"):
+        kernels.check_extents([src.data_ptr()], [-1], [src])
+    # zero fill (src 0) and empty segments are not checked; a view's storage counts
+    kernels.check_extents([0, src.data_ptr() + 999], [64, 0], [src])
+    kernels.check_extents([dst.data_ptr() + 5000], [64], [dst[4096:8192]])
+
+
+def test_adamset_set_grads_validates_without_gpu():
+    """ABI v12's zs_adamset_set_grads: a NULL set, a count other than the set's, a NULL table are
+    refused before anything is launched."""
+    from zero_amd import _lib
+
+    lib = _lib.lib
+    g = np.zeros(2, np.uint64)
+    assert lib.zs_adamset_set_grads(None, 2, g.ctypes.data, 0) == _lib.ZS_ERR_INVALID
+    assert b"NULL set" in lib.zs_last_error()

@@ -158,3 +158,31 @@ def test_cpu_baseline_sample_is_whole_decoder_layers():
         assert sum(int(np.prod(shapes[i])) for i in idx) >= 256 << 20
     idx, _ = bench._cpu_sample(mlp_shapes(4096), 64 << 20)
     assert idx == list(range(len(idx))) and len(idx) >= 1
+
+
+def test_expected_scaling_matches_the_planner_at_c4_n8():
+    """the prediction committed before the first 8-GPU line.  C4 ZeRO-2 on the flat
+    arena at N = 8: the slowest rank's Adam streams 15.23 GB of HBM and the exchange moves 10.76 GB
+    of bus bytes per rank — 11.95 ms at 8 TB/s + 7 x 153 GB/s, no overlap credit."""
+    import sys
+
+    sys.path.insert(0, str(bench.REPO / "distributed-training-sandbox_amd"))
+    from zero_amd.shapes import CONFIGS
+
+    c4 = CONFIGS["C4"][1]()
+    e = bench.expected_scaling(c4, 2, "flat", 8)
+    assert abs(e["hbm_gb_per_rank"] - 15.23) < 0.01 and abs(e["bus_gb_per_rank"] - 10.76) < 0.01
+    assert abs(e["ideal_ms"] - 11.95) < 0.01
+    assert e["at_north_star_ms"] > e["ideal_ms"] > e["ideal_overlapped_ms"]
+    # N = 1: no exchange, the whole 26 B x 3.075e9 Adam stream (the headline's 79.95 GB)
+    e1 = bench.expected_scaling(c4, 2, "flat", 1)
+    assert e1["bus_gb_per_rank"] == 0 and abs(e1["hbm_gb_per_rank"] - 79.9526) < 1e-3
+    # strong scaling of C4 is exchange-bound: at most ~1.1x over the measured N=1 step (13.05 ms)
+    assert 13.05 / e["ideal_ms"] < 1.15
+    # the bucket arena adds pack + unpack (4 B per bf16 element) and pays RS/AG bus bytes
+    b = bench.expected_scaling(c4, 2, "buckets", 8)
+    assert abs(b["hbm_gb_per_rank"] - e["hbm_gb_per_rank"] - 4 * 2 * 3075098624 / 1e9) < 1e-6
+    # ZeRO-3 on C5: three exchanges of the padded chunks per iteration
+    c5 = CONFIGS["C5"][1]()
+    z = bench.expected_scaling(c5, 3, "chunk", 8)
+    assert 3 * 8.03 * 2 * 7 / 8 <= z["bus_gb_per_rank"] < 3 * 8.1 * 2 * 7 / 8

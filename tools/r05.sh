@@ -1,0 +1,33 @@
+#!/bin/bash
+# Round-5 GPU session driver: `tools/r05.sh <step> [args]`, each step under its own time limit,
+# outputs under gpurun_out/r05/<step>*.  Steps are chained by the caller with && (a fault, an abort
+# or a time limit ends the call: nothing more runs on the GPU after it).
+set -o pipefail
+R="${GRAFT_REPO_ROOT:-$(pwd)}"; O="$R/gpurun_out/r05"; mkdir -p "$O"
+export TMPDIR=/tmp
+cd "$R" || exit 2
+step="$1"; shift
+fatal() { case $1 in 124|134|137|139) echo "[$step] rc=$1: stop"; exit 1;; esac; }
+case "$step" in
+  tests)  # a subset of the -m gpu suite: tools/r05.sh tests <pytest node ids / files>
+    ZS_FAIL_LOG="$O/failures_tests.txt" timeout -k 10 900 python -u -m pytest "$@" -m gpu -q \
+      --timeout 300 --timeout-method thread > "$O/tests.log" 2>&1; rc=$?
+    tail -30 "$O/tests.log"; fatal $rc; echo "[tests] rc=$rc";;
+  suite)  # the whole -m gpu suite as the driver runs it, then smoke()
+    ZS_FAIL_LOG="$O/failures_suite.txt" timeout -k 10 1000 python -u -m pytest tests -m gpu -q \
+      --timeout 600 --timeout-method thread --durations=40 > "$O/suite.log" 2>&1; rc=$?
+    tail -60 "$O/suite.log"; fatal $rc
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" \
+      > "$O/smoke.log" 2>&1; tail -3 "$O/smoke.log"; echo "[suite] rc=$rc";;
+  bench)  # tools/r05.sh bench <tag> <bench.py args>
+    tag="$1"; shift
+    timeout -k 10 900 python -u bench.py "$@" > "$O/bench_$tag.json" 2> "$O/bench_$tag.err"; rc=$?
+    tail -c 3000 "$O/bench_$tag.json"; tail -5 "$O/bench_$tag.err"; fatal $rc; echo "[bench $tag] rc=$rc";;
+  kstats)  # rocprofv3 kernel trace + stats of a bench command: tools/r05.sh kstats <tag> <args>
+    tag="$1"; shift
+    timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$O/prof_$tag" -o run -- \
+      python3 bench.py "$@" > "$O/kstats_$tag.json" 2> "$O/kstats_$tag.err"; rc=$?
+    tail -c 1500 "$O/kstats_$tag.json"; fatal $rc
+    find "$O/prof_$tag" -name '*kernel_stats.csv' -exec head -12 {} \; ; echo "[kstats $tag] rc=$rc";;
+  *) echo "unknown step $step"; exit 2;;
+esac
