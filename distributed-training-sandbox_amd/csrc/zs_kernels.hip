@@ -866,6 +866,17 @@ DqTune& dq_tune() {
   return t;
 }
 
+// Adam grid (zs_tune "adam_wg_per_cu", diagnostic A/B): 0 = grid_cap() (128 workgroups per CU),
+// k = at most k workgroups per CU striding over the chunks
+int& adam_wg_per_cu() {
+  static int v = 0;
+  return v;
+}
+int64_t adam_grid_cap() {
+  const int k = adam_wg_per_cu();
+  return k > 0 ? int64_t(grid_cap() / 128) * k : int64_t(grid_cap());
+}
+
 // zs_scale's / zs_convert's / zs_copyset_run's cache policy: -1 by size (kMallBytes), 0 default
 // policy, 1 non-temporal
 int& scale_nt_mode() {
@@ -1046,7 +1057,7 @@ static int launch_adam_tables(const AdamSeg* vec, const int64_t* vpre, int64_t n
                               int g_dtype, bool split, bool ams, bool carry, const HP& hp,
                               hipStream_t st) {
 #define ZS_LAUNCH(KERNEL, GT, A, C, S, TAB, PRE, NS, NCH)                                     \
-  hipLaunchKernelGGL((KERNEL<GT, A, C, S>), dim3(int(std::min<int64_t>(NCH, grid_cap()))),   \
+  hipLaunchKernelGGL((KERNEL<GT, A, C, S>), dim3(int(std::min<int64_t>(NCH, adam_grid_cap()))), \
                      dim3(kThreads), 0, st, TAB, PRE, NS, NCH, hp)
 #define ZS_DISPATCH_AC(KERNEL, GT, S, TAB, PRE, NS, NCH)                                      \
   do {                                                                                        \
@@ -1756,6 +1767,9 @@ int zs_tune(const char* key, int64_t value, int64_t* previous) {
   } else if (std::strcmp(key, "copy_nt") == 0) {
     slot = &copy_nt_mode();
     ok = value >= -1 && value <= 1;
+  } else if (std::strcmp(key, "adam_wg_per_cu") == 0) {
+    slot = &adam_wg_per_cu();
+    ok = value >= 0 && value <= 1024;
   } else {
     return zs::fail(ZS_ERR_INVALID, "zs_tune: unknown key '%s'", key);
   }

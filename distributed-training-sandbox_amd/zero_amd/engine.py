@@ -96,14 +96,37 @@ PROBE_MIN_BYTES = 1 << 30
 PROBE_ACCEPT_GBS = 5950.0
 
 
-_PLACED = {"bytes": 0, "buffers": 0}  # device memory held by placed buffers (outside torch's cache)
+# device memory held by placed buffers (outside torch's cache), per device index: bytes and buffers
+# held now, and the high-water mark of bytes — probe candidates included while they are held
+_PLACED = {}
 
 
-def placed_bytes() -> int:
-    """Bytes of device memory currently held by placed buffers (``probed_zeros``).  They are
-    hipMalloc allocations outside torch's caching allocator, so ``torch.cuda.memory_allocated``
-    does not count them; the harness memory report adds them (training_utils/memory.py)."""
-    return _PLACED["bytes"]
+def _placed(dev_index: int) -> dict:
+    return _PLACED.setdefault(int(dev_index), {"bytes": 0, "buffers": 0, "peak": 0})
+
+
+def placed_bytes(device=None) -> int:
+    """Bytes of device memory currently held by placed buffers (``probed_zeros``) on ``device``
+    (None: every device).  They are hipMalloc allocations outside torch's caching allocator, so
+    ``torch.cuda.memory_allocated`` does not count them; the harness memory report prints them
+    beside torch's figures (training_utils/memory.py)."""
+    if device is None:
+        return sum(d["bytes"] for d in _PLACED.values())
+    return _placed(torch.device(device).index or 0)["bytes"]
+
+
+def placed_peak_bytes(device=None) -> int:
+    """High-water mark of ``placed_bytes`` on ``device`` (None: the largest over devices),
+    counting the placement probe's candidates while they are held."""
+    if device is None:
+        return max((d["peak"] for d in _PLACED.values()), default=0)
+    return _placed(torch.device(device).index or 0)["peak"]
+
+
+def reset_placed_peak(device=None) -> None:
+    for k, d in _PLACED.items():
+        if device is None or k == (torch.device(device).index or 0):
+            d["peak"] = d["bytes"]
 
 
 class _DeviceBuffer:
@@ -119,8 +142,10 @@ class _DeviceBuffer:
         with torch.cuda.device(self.device):
             _lib.call("zs_device_alloc", self.nbytes, ctypes.byref(ptr))
         self.ptr = int(ptr.value)
-        _PLACED["bytes"] += self.nbytes
-        _PLACED["buffers"] += 1
+        acc = _placed(self.device.index or 0)
+        acc["bytes"] += self.nbytes
+        acc["buffers"] += 1
+        acc["peak"] = max(acc["peak"], acc["bytes"])
 
     @property
     def __cuda_array_interface__(self):
@@ -140,8 +165,9 @@ class _DeviceBuffer:
     def free(self):
         if self.ptr:
             ptr, self.ptr = self.ptr, 0
-            _PLACED["bytes"] -= self.nbytes
-            _PLACED["buffers"] -= 1
+            acc = _placed(self.device.index or 0)
+            acc["bytes"] -= self.nbytes
+            acc["buffers"] -= 1
             try:
                 _lib.lib.zs_device_free(ptr)
             except Exception:  # noqa: BLE001 — interpreter shutdown: the runtime may be gone

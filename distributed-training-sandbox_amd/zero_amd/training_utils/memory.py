@@ -6,9 +6,11 @@ logical (numel Ã— element size, in MiB) â€” the quantity the reference reports â
 physical: the distinct storages behind those tensors.  The two differ for the drop-ins on purpose:
 ``optimizer.optimizer.state[p]`` holds *views* of one flat fp32 shard buffer, and ZeRO-3 parameters
 are views of one flat chunk arena, so the physical column shows what is really resident.
-"Total allocated" / "Max allocated" are torch's allocator figures plus the placed buffers of 1 GiB
-or more (optimizer state, parameter / gradient arenas: ``engine.probed_zeros``), which are device
-allocations of their own outside torch's cache.
+"Total allocated" / "Max allocated" are torch's allocator figures, as the reference prints them.
+The placed buffers of 1 GiB or more (optimizer state, parameter / gradient arenas:
+``engine.probed_zeros``) are device allocations of their own outside torch's cache; they get a
+line of their own â€” held now and the device's high-water mark, the placement probe's candidates
+included â€” rather than being added to torch's peak (the two peaks need not coincide in time).
 """
 from __future__ import annotations
 
@@ -50,15 +52,20 @@ class MemoryReport:
     optimizer_physical_mb: float
     allocated_mb: float
     max_allocated_mb: float
+    placed_mb: float = 0.0
+    placed_peak_mb: float = 0.0
 
     def lines(self, prefix: str, rank: int):
-        return [f"\nGPU {rank} - {prefix}:",
-                f"  Model parameters: {self.params_mb:.2f} MB",
-                f"  Gradients: {self.grads_mb:.2f} MB",
-                f"  Optimizer states: {self.optimizer_mb:.2f} MB",
-                f"  Total allocated: {self.allocated_mb:.2f} MB",
-                f"  Max allocated: {self.max_allocated_mb:.2f} MB",
-                "-" * 40]
+        out = [f"\nGPU {rank} - {prefix}:",
+               f"  Model parameters: {self.params_mb:.2f} MB",
+               f"  Gradients: {self.grads_mb:.2f} MB",
+               f"  Optimizer states: {self.optimizer_mb:.2f} MB",
+               f"  Total allocated: {self.allocated_mb:.2f} MB",
+               f"  Max allocated: {self.max_allocated_mb:.2f} MB"]
+        if self.placed_peak_mb:
+            out.append(f"  Placed outside torch's allocator: {self.placed_mb:.2f} MB "
+                       f"(peak {self.placed_peak_mb:.2f} MB incl. placement-probe candidates)")
+        return out + ["-" * 40]
 
 
 def memory_report(model, optimizer, device) -> MemoryReport:
@@ -67,12 +74,13 @@ def memory_report(model, optimizer, device) -> MemoryReport:
     g_l, g_p = _walk(p.grad for p in params)
     o_l, o_p = _walk(_state_tensors(optimizer))
     on_gpu = torch.cuda.is_available() and torch.device(device).type == "cuda"
-    from ..engine import placed_bytes
+    from ..engine import placed_bytes, placed_peak_bytes
 
-    placed = placed_bytes() / _MIB if on_gpu else 0.0
-    alloc = torch.cuda.memory_allocated(device) / _MIB + placed if on_gpu else 0.0
-    peak = torch.cuda.max_memory_allocated(device) / _MIB + placed if on_gpu else 0.0
-    return MemoryReport(p_l, g_l, o_l, p_p, g_p, o_p, alloc, peak)
+    placed = placed_bytes(device) / _MIB if on_gpu else 0.0
+    placed_peak = placed_peak_bytes(device) / _MIB if on_gpu else 0.0
+    alloc = torch.cuda.memory_allocated(device) / _MIB if on_gpu else 0.0
+    peak = torch.cuda.max_memory_allocated(device) / _MIB if on_gpu else 0.0
+    return MemoryReport(p_l, g_l, o_l, p_p, g_p, o_p, alloc, peak, placed, placed_peak)
 
 
 def print_memory_stats(prefix: str, model, optimizer, rank, device):

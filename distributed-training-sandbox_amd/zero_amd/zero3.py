@@ -143,7 +143,7 @@ class _GatherRuntime:
     that polls while a cross-stream dependency is pending (≈ one core for as long as the host runs
     ahead of the GPU: profiles/r04_hip_event_cost.jsonl)."""
 
-    def __init__(self, ws, rank, comm, device, wave: int = 2, side_stream: bool = True):
+    def __init__(self, ws, rank, comm, device, wave: int = 1, side_stream: bool = True):
         self.ws, self.rank, self.comm, self.device = ws, rank, comm, device
         if int(wave) < 1:
             raise ValueError(f"gather wave must be >= 1 (got {wave})")
@@ -564,8 +564,10 @@ class Zero3ParamManager:
         self.send_slot = send_slot
         if gather_dtype not in (None, "fp8"):
             raise ValueError(f"gather_dtype must be None or 'fp8' (got {gather_dtype!r})")
-        # fp8 only for matrices (row-wise scales); vectors (biases, norms) gather as they are
-        self.fp8 = gather_dtype == "fp8" and len(self.full_shape) >= 2
+        # fp8 only for matrices (row-wise scales) whose rows are a multiple of 8 elements (the
+        # vector kernels' 8-B fp8 accesses); vectors (biases, norms) and other matrices gather as
+        # they are
+        self.fp8 = gather_dtype == "fp8" and len(self.full_shape) >= 2 and self.row % 8 == 0
 
     def gather_bytes(self) -> int:
         """Bytes this rank contributes to one all-gather of the parameter."""
@@ -578,13 +580,20 @@ class Zero3ParamManager:
         dev, ws = self.shard.device, self.world_size
         rows = self.r1 - self.r0
         if self.fp8:  # 1 byte per element + one fp32 scale per row
-            q = torch.zeros(self.S, dtype=torch.uint8, device=dev)
-            sc = torch.ones(self.cs, dtype=torch.float32, device=dev)
-            if rows:
-                _lib.call("zs_fp8_quantize_rows", self.shard.data_ptr(), zs_dtype(self.shard.dtype),
-                          q.data_ptr(), sc.data_ptr(), rows, self.row, stream_handle(stream))
+            # the module path's rowset kernel as a one-matrix set: it writes the chunk's padding
+            # rows itself (q = 0, scale = 1), so nothing is pre-filled
+            src = self.shard
+            if rows and src.data_ptr() % 16:  # (a standalone shard at an odd offset)
+                src = src.contiguous().clone()
+            q = torch.empty(self.S, dtype=torch.uint8, device=dev)
+            sc = torch.empty(self.cs, dtype=torch.float32, device=dev)
+            ptrs = np.array([src.data_ptr() if rows else 0, q.data_ptr(), sc.data_ptr()], np.uint64)
+            geom = np.array([rows, self.cs, self.row], np.int64)  # real rows, chunk rows, row length
+            _lib.call("zs_fp8_quantize_rowset", 1, ptrs[0:].ctypes.data, ptrs[1:].ctypes.data,
+                      ptrs[2:].ctypes.data, geom[0:].ctypes.data, geom[1:].ctypes.data,
+                      geom[2:].ctypes.data, zs_dtype(self.shard.dtype), stream_handle(stream))
             return (q, sc, torch.empty(ws * self.S, dtype=torch.uint8, device=dev),
-                    torch.empty(ws * self.cs, dtype=torch.float32, device=dev))
+                    torch.empty(ws * self.cs, dtype=torch.float32, device=dev), src)
         if self.send_slot is not None:
             send = self.send_slot
         else:
@@ -599,7 +608,7 @@ class Zero3ParamManager:
 
     def _gather_issue(self, comm, stream, st):
         if self.fp8:
-            q, sc, full_q, full_sc = st
+            q, sc, full_q, full_sc, _ = st
             comm.all_gather(q, full_q, stream)
             comm.all_gather(sc, full_sc, stream)
         else:
@@ -610,10 +619,16 @@ class Zero3ParamManager:
     def _gather_finish(self, stream, st):
         if not self.fp8:
             return st[1]
-        _, _, full_q, full_sc = st
-        full = torch.empty(self.world_size * self.S, dtype=self.shard.dtype, device=self.shard.device)
-        _lib.call("zs_fp8_dequantize_rows", full_q.data_ptr(), full_sc.data_ptr(), full.data_ptr(),
-                  zs_dtype(full.dtype), self.world_size * self.cs, self.row, stream_handle(stream))
+        _, _, full_q, full_sc, _ = st
+        ws = self.world_size
+        full = torch.empty(ws * self.S, dtype=self.shard.dtype, device=self.shard.device)
+        # the module path's gathered kernel as a one-matrix set: rank k's rows at k * S bytes of
+        # the gathered q, its scales at k * cs
+        geom = np.array([0, 0, self.cs, self.row], np.int64)  # q_off, sc_off, cs, row_len
+        dst = np.array([full.data_ptr()], np.uint64)
+        _lib.call("zs_fp8_dequantize_gathered", 1, full_q.data_ptr(), full_sc.data_ptr(), ws, self.S,
+                  self.cs, geom[0:].ctypes.data, geom[1:].ctypes.data, geom[2:].ctypes.data,
+                  geom[3:].ctypes.data, dst.ctypes.data, zs_dtype(full.dtype), stream_handle(stream))
         return full
 
     def _install_full(self, full):
@@ -1190,10 +1205,13 @@ class _GradReducer:
 # gradients waiting for their collective — nothing against 288 GB of HBM.
 RS_BUCKET_MB = 512.0
 # Module gathers ordered (and prefetched) as waves of this many consecutive groups: one ready and
-# one done event, and one consumer wait, per wave (see _GatherRuntime).  2 halves the cross-stream
-# waits of the per-module ordering; the compute of a wave's first module waits for the whole wave
-# (both gathers were launched one wave earlier, while the previous wave computed).
-GATHER_WAVE = 2
+# one done event, and one consumer wait, per wave (see _GatherRuntime).  1 (per-module ordering,
+# the next module prefetched while this one computes) is the default: at most two modules' full
+# parameters are resident.  ``gather_wave=2`` halves the cross-stream waits, but when wave w starts
+# wave w + 1 is already in flight — up to four modules' full parameters resident — and the first
+# module of a wave waits for both of its gathers; its host-time win was measured on the
+# compute-free parameter-set model only, which the bench now runs single-stream.
+GATHER_WAVE = 1
 
 
 class ShardedOptimizer:

@@ -319,7 +319,9 @@ int zs_device_free(void* p);
  * "dq_nt_store" (0 / 1: non-temporal stores), "dq_wg_per_cu" (0 = one wave per row; k = at most k
  * workgroups per CU walking several rows each), "scale_nt" (zs_scale's cache policy: -1 by size,
  * non-temporal above 256 MiB; 0 default policy; 1 non-temporal), "convert_nt" (zs_convert's, the
- * same by source + destination bytes), "copy_nt" (zs_copyset_run's, by 2 x the set's bytes).  *previous (may be NULL) gets the
+ * same by source + destination bytes), "copy_nt" (zs_copyset_run's, by 2 x the set's bytes),
+ * "adam_wg_per_cu" (0 = 128 workgroups per CU, the default grid of the fused Adam; k = at most k
+ * per CU).  *previous (may be NULL) gets the
  * old value;
  * ZS_ERR_INVALID for an unknown key or value. */
 int zs_tune(const char* key, int64_t value, int64_t* previous);

@@ -191,3 +191,42 @@ def _mr(rank, ws, port, reshard=True):
 @pytest.mark.parametrize("ws,reshards", [(2, (True, False)), (3, (True,))])
 def test_zero3_fp8_gather_multirank(gpu, ws, reshards):
     spawn_batch(ws, [(_mr, (r,)) for r in reshards])
+
+
+@pytest.mark.parametrize("ws", [1, 3])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_zero3_fp8_standalone_manager_uses_set_kernels(gpu, ws, dtype, monkeypatch):
+    """a standalone Zero3ParamManager's fp8 gather runs the module path's set
+    kernels as a one-matrix set (zs_fp8_quantize_rowset / zs_fp8_dequantize_gathered), never the
+    per-matrix zs_fp8_*_rows forms.  Every rank's send side is built by the manager itself; the
+    all-gather is emulated by concatenating them rank-major; the full tensor equals the row oracle
+    (uneven chunks: the last rank's padding rows).  A matrix whose rows are not a multiple of 8
+    elements gathers unquantised."""
+    from zero_amd import _lib, zero3
+
+    called = []
+    real_call = _lib.call
+    monkeypatch.setattr(_lib, "call", lambda name, *a: (called.append(name), real_call(name, *a))[1])
+    g = torch.Generator().manual_seed(ws)
+    full = (torch.randn(37, 64, generator=g) * 10.0 ** torch.randint(-3, 3, (37, 1), generator=g)).to(dtype)
+    full[5] = 0
+    cs = -(-37 // ws)
+    st = torch.cuda.current_stream()
+    states, mans = [], []
+    for k in range(ws):
+        p = torch.nn.Parameter(full[k * cs:(k + 1) * cs].contiguous().to(gpu))
+        m = zero3.Zero3ParamManager(p, k, ws, gather_dtype="fp8")
+        assert m.fp8
+        states.append(m._gather_prepare(st))
+        mans.append(m)
+    fq = torch.cat([s[0] for s in states])
+    fsc = torch.cat([s[1] for s in states])
+    out = mans[0]._gather_finish(st, (None, None, fq, fsc, None))
+    torch.cuda.synchronize()
+    want = torch.from_numpy(fp8_rows_oracle(full)[2]).to(dtype)
+    assert torch.equal(out[:full.numel()].view(37, 64).cpu(), want)
+    assert "zs_fp8_quantize_rows" not in called and "zs_fp8_dequantize_rows" not in called
+    assert called.count("zs_fp8_quantize_rowset") == ws and called.count("zs_fp8_dequantize_gathered") == 1
+    odd = zero3.Zero3ParamManager(torch.nn.Parameter(torch.zeros(5, 12, device=gpu, dtype=dtype)), 0, 1,
+                                  gather_dtype="fp8")
+    assert not odd.fp8  # row of 12 elements: gathered as it is

@@ -2,8 +2,10 @@
 
 Single-process cases run the product path end to end (RCCL communicator included at ws=1).
 Multi-rank cases run ws processes on the one GPU of the box: pack / fused Adam / unpack are the
-real HIP kernels, the exchange goes through tests/_gloo_comm.py (RCCL cannot put two ranks of a
-communicator on one device).  Tolerance: 1e-6 normwise relative (north star), every step.
+real HIP kernels, and the exchange goes through tests/_gloo_comm.py's gloo-staged communicator
+here; tests/test_gpu_rccl.py re-runs the same workers through the product's RCCL communicator
+between ranks that share the device (each rank its own RCCL node, NCCL_HOSTID).
+Tolerance: 1e-6 normwise relative (north star), every step.
 """
 
 import os

@@ -262,7 +262,7 @@ def _bench_rank(rank, ws, port, argv):
 def test_bench_share_gpu_n8_both_arenas(gpu):
     """The driver's default N=8 run (C4 ZeRO-2, ``--arena auto``) rehearsed through real RCCL on a
     4-layer copy of the SmolLM3-3B set (the full set at N = 8 takes minutes over sockets:
-    tools/r04_rehearsal8.sh, profiles/r04_rccl_net/c4_n8_full.json): communicator
+    tools/r05.sh rehearsal8, profiles/r04_rccl_net/c4_n8_full.json): communicator
     self-check, then BOTH arenas the calibration can pick — the flat arena's grouped reduce /
     broadcast rounds and the bucket arena's pack / RS / AG / unpack — each exchange-checked (reduced
     grads within the ring bound, Adam within 1 bf16 ulp of the restatement, ranks bit-identical),

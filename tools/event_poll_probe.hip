@@ -7,6 +7,10 @@
 // runtime's own threads show up beside the main thread.  Variants: event flags (timing / disable
 // timing / disable system fence), stream flags (default / non-blocking), host wait by
 // hipEventSynchronize vs a hipEventQuery sleep loop, and no cross-stream wait at all.
+// Round 5: stream memory operations as the ordering — hipStreamWriteValue32 of an
+// epoch on stream A after the busy kernel, hipStreamWaitValue32(>= epoch) on stream B — with the
+// flag word in device memory (hipMalloc), in signal memory (hipExtMallocWithFlags
+// hipMallocSignalMemory) and in pinned host memory (hipHostMalloc).
 //
 // build: hipcc --offload-arch=gfx950 -O2 tools/event_poll_probe.hip -o tools/event_poll_probe
 // run:   tools/event_poll_probe [ms]
@@ -72,12 +76,15 @@ static std::map<long, long> thread_ticks() {
   return out;
 }
 
+enum Flag { kNoFlag = 0, kDeviceFlag, kSignalFlag, kHostFlag };
+
 struct Variant {
   const char* name;
   unsigned ev_flags;
   unsigned st_flags;
   bool cross_wait;
   bool query_loop;
+  Flag flag = kNoFlag;  // != kNoFlag: the cross-stream ordering is a write / wait of this word
 };
 
 int main(int argc, char** argv) {
@@ -110,9 +117,32 @@ int main(int argc, char** argv) {
       {"cross wait, non-blocking streams", hipEventDisableTiming, hipStreamNonBlocking, true, false},
       {"cross wait, host polls hipEventQuery + sleep", hipEventDisableTiming, hipStreamDefault, true, true},
       {"no cross wait, host polls hipEventQuery + sleep", hipEventDisableTiming, hipStreamDefault, false, true},
+      {"stream write/wait value32, flag in hipMalloc memory", hipEventDisableTiming, hipStreamDefault, true,
+       false, kDeviceFlag},
+      {"stream write/wait value32, flag in signal memory", hipEventDisableTiming, hipStreamDefault, true,
+       false, kSignalFlag},
+      {"stream write/wait value32, flag in pinned host memory", hipEventDisableTiming, hipStreamDefault, true,
+       false, kHostFlag},
+      {"stream write/wait value32 (hipMalloc), host polls hipEventQuery + sleep", hipEventDisableTiming,
+       hipStreamDefault, true, true, kDeviceFlag},
   };
+  // the flag words (one per kind); epochs only grow, so a wait never sees a stale value as done
+  uint32_t* flags[4] = {nullptr, nullptr, nullptr, nullptr};
+  CHECK(hipMalloc(&flags[kDeviceFlag], 64));
+  CHECK(hipMemset(flags[kDeviceFlag], 0, 64));
+  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&flags[kSignalFlag]), 64, hipMallocSignalMemory) != hipSuccess) {
+    (void)hipGetLastError();
+    flags[kSignalFlag] = nullptr;
+    std::printf("{\"note\": \"hipMallocSignalMemory refused: signal-memory variant skipped\"}\n");
+  } else {
+    CHECK(hipMemset(flags[kSignalFlag], 0, 8));
+  }
+  CHECK(hipHostMalloc(reinterpret_cast<void**>(&flags[kHostFlag]), 64, hipHostMallocCoherent));
+  std::memset(flags[kHostFlag], 0, 64);
+  uint32_t epoch = 0;
   const long self_tid = long(gettid());
   for (const Variant& v : vs) {
+    if (v.flag != kNoFlag && flags[v.flag] == nullptr) continue;
     for (int rep = 0; rep < 2; ++rep) {
       hipStream_t a, b;
       CHECK(hipStreamCreateWithFlags(&a, v.st_flags));
@@ -126,7 +156,13 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL(busy_kernel, dim3(1), dim3(64), 0, a, iters, out);
       CHECK(hipEventRecord(ea, a));
       hipEvent_t last = ea;
-      if (v.cross_wait) {
+      if (v.cross_wait && v.flag != kNoFlag) {
+        ++epoch;
+        CHECK(hipStreamWriteValue32(a, flags[v.flag], epoch, 0));
+        CHECK(hipStreamWaitValue32(b, flags[v.flag], epoch, hipStreamWaitValueGte, 0xFFFFFFFFu));
+        CHECK(hipEventRecord(eb, b));
+        last = eb;
+      } else if (v.cross_wait) {
         CHECK(hipStreamWaitEvent(b, ea, 0));
         CHECK(hipEventRecord(eb, b));
         last = eb;
@@ -157,6 +193,10 @@ int main(int argc, char** argv) {
       CHECK(hipStreamDestroy(b));
     }
   }
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipFree(flags[kDeviceFlag]));
+  if (flags[kSignalFlag]) CHECK(hipFree(flags[kSignalFlag]));
+  CHECK(hipHostFree(flags[kHostFlag]));
   CHECK(hipFree(out));
   return 0;
 }

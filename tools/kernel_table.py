@@ -6,9 +6,13 @@ events on the launch stream, achieved GB/s and the fraction of the 8 TB/s HBM pe
   convert_kernel<true>   fp32 -> bf16 RNE, C3-size gradient (983,116,800 elements): the
                          grad_comm="bf16" conversion before the exchange; 4 + 2 B/element
   convert_kernel<false>  bf16 -> fp32, same size; 2 + 4 B/element
-  fp8_quantize_rows      one C5 decoder layer's matrices (bf16, row-scaled E4M3, the ZeRO-3
-                         gather_dtype="fp8" send side): 2 + 1 B/element + 4 B/row
-  fp8_dequantize_rows    the same layer gathered (receive side): 1 + 2 B/element + 4 B/row
+  fp8_quantize_rowset    one C5 decoder layer's matrices (bf16, row-scaled E4M3, the ZeRO-3
+                         gather_dtype="fp8" send side, one launch per register class):
+                         2 + 1 B/element + 4 B/row
+  fp8_dequantize_gathered  the same layer gathered (receive side, one launch): 1 + 2 B/element
+                         + 4 B/row.  (Round 5: the per-matrix zs_fp8_*_rows forms are off the
+                         product path — a standalone Zero3ParamManager runs these two kernels as a
+                         one-matrix set — so they are not in the table.)
   scale_kernel           DDP's grad /= ws, in place, bf16 and fp32: a 256 MiB bucket (MALL-sized)
                          and a 4 GiB buffer (HBM): 2 x element size per element
   copy_segments_kernel   pack of the C4 set's grads into one rank-major arena (every tensor a
@@ -102,25 +106,9 @@ def main():
     for x in mats:
         x.normal_()
 
-    def quant():
-        for x, q, sc in zip(mats, qs, scs):
-            _lib.call("zs_fp8_quantize_rows", x.data_ptr(), _lib.ZS_BF16, q.data_ptr(), sc.data_ptr(),
-                      x.shape[0], x.shape[1], stream_handle(st))
-
-    def dequant():
-        for q, sc, y in zip(qs, scs, outs):
-            _lib.call("zs_fp8_dequantize_rows", q.data_ptr(), sc.data_ptr(), y.data_ptr(),
-                      _lib.ZS_BF16, q.shape[0], q.shape[1], stream_handle(st))
-
-    timed("fp8_quantize_rows_kernel<bf16> (7 launches, one per matrix)", quant,
-          3 * elems + 4 * nrows, f"one C5 decoder layer, {elems:,} bf16 elements",
-          "fp8_quantize_rows_wave_kernel<unsigned short,", len(layer))
-    timed("fp8_dequantize_rows (7 launches, one per matrix; the gathered kernel at ws = 1)", dequant,
-          3 * elems + 4 * nrows, f"one C5 decoder layer, {elems:,} elements",
-          "fp8_dequantize_gathered_kernel<unsigned short,", len(layer))
-    # the same layer through the gather group's fused forms: one quantise launch per register
-    # class into one concatenated send buffer, one dequantise launch from it (ws = 1 layout: the
-    # gathered buffer is the send buffer)
+    # the gather group's fused forms: one quantise launch per register class into one
+    # concatenated send buffer, one dequantise launch from it (ws = 1 layout: the gathered buffer
+    # is the send buffer)
     shp = [tuple(x.shape) for x in mats]
     q_off = np.cumsum([0] + [r * c for r, c in shp])[:-1].astype(np.int64)
     sc_off = np.cumsum([0] + [r for r, _ in shp])[:-1].astype(np.int64)

@@ -29,5 +29,21 @@ case "$step" in
       python3 bench.py "$@" > "$O/kstats_$tag.json" 2> "$O/kstats_$tag.err"; rc=$?
     tail -c 1500 "$O/kstats_$tag.json"; fatal $rc
     find "$O/prof_$tag" -name '*kernel_stats.csv' -exec head -12 {} \; ; echo "[kstats $tag] rc=$rc";;
+  pmc)  # separate FETCH_SIZE / WRITE_SIZE passes + summary: tools/r05.sh pmc <tag> <alg bytes> <config json> <bench args>
+    tag="$1"; alg="$2"; cfg="$3"; shift 3
+    for c in FETCH_SIZE WRITE_SIZE; do
+      (cd /tmp && timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_${tag}_$c" -o run -- \
+        python3 "$R/bench.py" "$@" > "$O/pmc_${tag}_$c.json" 2> "$O/pmc_${tag}_$c.err"); rc=$?
+      tail -c 300 "$O/pmc_${tag}_$c.json"; fatal $rc
+      [ $rc -eq 0 ] || { echo "[pmc $c] rc=$rc"; tail -5 "$O/pmc_${tag}_$c.err"; exit 1; }
+    done
+    python3 tools/pmc_summary.py "$O/pmc_${tag}_FETCH_SIZE" "$O/pmc_${tag}_WRITE_SIZE" "adam_segments_kernel<unsigned short, false, false, true>" \
+      "$O/${tag}_pmc.json" "$alg" "$cfg" "python3 bench.py $*" | tail -8; echo "[pmc $tag] done";;
+  rehearsal8)  # the driver's default N = 8 line (C4 ZeRO-2, arena auto) on the ONE GPU through real
+    # RCCL (--share-gpu: 8 ranks on one card, sockets between them), as plain `python bench.py --gpus 8`
+    GPU_MAX_HW_QUEUES=2 timeout -k 10 840 python3 bench.py --share-gpu --no-cpu-baseline --watchdog-s 800 \
+      --gpus 8 --steps 2 --warmup 1 --no-comm-sweep "$@" > "$O/c4_n8_full.json" 2> "$O/c4_n8_full.err"; rc=$?
+    tail -1 "$O/c4_n8_full.json" | cut -c1-600; fatal $rc
+    [ $rc -eq 0 ] || { tail -20 "$O/c4_n8_full.err"; exit 1; }; echo "[rehearsal8] done";;
   *) echo "unknown step $step"; exit 2;;
 esac

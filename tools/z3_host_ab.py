@@ -1,5 +1,6 @@
-"""Host-time A/B of the hooked ZeRO-3 iteration: the round-2 ZeRO-3 runtime
-(tools/_zero3_r02.py, loaded as a module of the zero_amd package) against the current one, in ONE
+"""Host-time A/B of the hooked ZeRO-3 iteration: an earlier round's ZeRO-3 runtime
+(zero_amd/zero3.py at that round's commit, loaded as a module of the zero_amd package) against the
+current one, in ONE
 process, alternating blocks of iterations, each on its own copy of the configs[4] parameter set as
 rank 0 of a simulated ws-rank job (collectives no-ops, so the GPU runs only Adam and the rest is
 host time).  Wall time per iteration and process CPU time (all threads: the backward hooks run on
@@ -7,7 +8,10 @@ autograd's device thread) per block — the box's host speed drifts by 30 % over
 the interleaved comparison means anything.
 
 Usage: python tools/z3_host_ab.py [--config C5] [--ws 8] [--iters 20] [--blocks 6] [--baseline r02|r03]
-(--baseline r03: tools/_zero3_r03.py, the round-3 runtime, against the current one)
+The baseline module is ``git show <rev>:distributed-training-sandbox_amd/zero_amd/zero3.py`` (r02:
+1653aab, r03: 3d19026 — the runtimes profiles/r03_z3_host_ab*.json and r04_z3_host_ab.json compare),
+written to tools/.baselines/ (git-ignored, so it travels to the GPU box, which has no git history):
+run ``python tools/z3_host_ab.py --baseline r03 --extract-only`` here before the gpurun call.
 """
 from __future__ import annotations
 
@@ -22,6 +26,22 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO / "distributed-training-sandbox_amd"))
 sys.path.insert(0, str(REPO))
+BASELINE_REVS = {"r02": "1653aab", "r03": "3d19026"}
+ZERO3_PATH = "distributed-training-sandbox_amd/zero_amd/zero3.py"
+
+
+def baseline_file(tag: str) -> Path:
+    """tools/.baselines/_zero3_<tag>.py, extracted from git history when it is not there yet."""
+    import subprocess
+
+    out = REPO / "tools" / ".baselines" / f"_zero3_{tag}.py"
+    if not out.exists():
+        src = subprocess.run(["git", "-C", str(REPO), "show", f"{BASELINE_REVS[tag]}:{ZERO3_PATH}"],
+                             check=True, capture_output=True, text=True).stdout
+        out.parent.mkdir(exist_ok=True)
+        out.write_text(f"# {ZERO3_PATH} at {BASELINE_REVS[tag]} ({tag}); extracted by "
+                       "tools/z3_host_ab.py, not part of the product\n" + src)
+    return out
 
 
 def main():
@@ -31,11 +51,17 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--baseline", default="r02", choices=["r02", "r03"])
+    ap.add_argument("--baseline", default="r03", choices=sorted(BASELINE_REVS))
+    ap.add_argument("--extract-only", action="store_true",
+                    help="write the baseline module under tools/.baselines/ and exit (no GPU)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--single", action="store_true",
                     help="also time the current runtime with side_stream=False")
     args = ap.parse_args()
+    path = baseline_file(args.baseline)
+    if args.extract_only:
+        print(path)
+        return
 
     import torch
     import torch.distributed as dist
@@ -47,8 +73,7 @@ def main():
     from zero_amd.shapes import CONFIGS
 
     base = "round2" if args.baseline == "r02" else "round3"
-    spec = importlib.util.spec_from_file_location(f"zero_amd._zero3_{args.baseline}",
-                                                  REPO / "tools" / f"_zero3_{args.baseline}.py")
+    spec = importlib.util.spec_from_file_location(f"zero_amd._zero3_{args.baseline}", path)
     z3_old = importlib.util.module_from_spec(spec)
     sys.modules[spec.name] = z3_old
     spec.loader.exec_module(z3_old)
