@@ -316,6 +316,101 @@ int zs_stream_wait_event(uintptr_t stream, uint64_t event) {
   return ZS_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Sync objects (ABI v12): the cross-stream ordering of the ZeRO-3 gathers as either a HIP event or
+// a stream memory operation on a flag word (hipStreamWriteValue32 after the producer's work,
+// hipStreamWaitValue32 >= the recorded epoch before the consumer's).  A record bumps the object's
+// epoch on the host and enqueues its write; a wait enqueues a wait for the epoch of the latest
+// record, the semantics of hipStreamWaitEvent.  A flag object must be recorded from one stream at a
+// time (its epochs then reach the word in order).
+struct zs_sync {
+  int kind = ZS_SYNC_EVENT;
+  hipEvent_t event = nullptr;
+  uint32_t* flag = nullptr;
+  uint32_t epoch = 0;
+};
+
+int zs_sync_create(int kind, zs_sync** out) {
+  ZS_REQUIRE(out != nullptr, "zs_sync_create: out is NULL");
+  ZS_REQUIRE(kind == ZS_SYNC_EVENT || kind == ZS_SYNC_FLAG, "zs_sync_create: bad kind %d", kind);
+  *out = nullptr;
+  zs_sync* s = new (std::nothrow) zs_sync();
+  if (!s) return zs::fail(ZS_ERR_NOMEM, "zs_sync_create: out of memory");
+  s->kind = kind;
+  hipError_t e = kind == ZS_SYNC_EVENT
+                     ? hipEventCreateWithFlags(&s->event, hipEventDisableTiming)
+                     : hipMalloc(reinterpret_cast<void**>(&s->flag), 64);
+  if (e == hipSuccess && s->flag) e = hipMemset(s->flag, 0, 64);
+  if (e != hipSuccess) {
+    zs_sync_destroy(s);
+    return zs::fail(ZS_ERR_HIP, "zs_sync_create: %s", hipGetErrorString(e));
+  }
+  *out = s;
+  return ZS_OK;
+}
+
+int zs_sync_destroy(zs_sync* s) {
+  if (!s) return ZS_OK;
+  if (s->event) (void)hipEventDestroy(s->event);
+  if (s->flag) (void)hipFree(s->flag);
+  delete s;
+  return ZS_OK;
+}
+
+int zs_sync_record(zs_sync* s, uintptr_t stream) {
+  ZS_REQUIRE(s != nullptr, "zs_sync_record: NULL sync");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (s->kind == ZS_SYNC_EVENT) {
+    ZS_HIP(hipEventRecord(s->event, st));
+  } else {
+    ZS_HIP(hipStreamWriteValue32(st, s->flag, s->epoch + 1, 0));
+    ++s->epoch;
+  }
+  return ZS_OK;
+}
+
+int zs_sync_wait(zs_sync* s, uintptr_t stream) {
+  ZS_REQUIRE(s != nullptr, "zs_sync_wait: NULL sync");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (s->kind == ZS_SYNC_EVENT) {
+    ZS_HIP(hipStreamWaitEvent(st, s->event, 0));
+  } else if (s->epoch > 0) {  // never recorded: nothing to wait for (as an unrecorded event)
+    ZS_HIP(hipStreamWaitValue32(st, s->flag, s->epoch, hipStreamWaitValueGte, 0xFFFFFFFFu));
+  }
+  return ZS_OK;
+}
+
+static int synced_prologue(uintptr_t after_stream, zs_sync* ready, uintptr_t stream) {
+  if (ready) {
+    int rc = zs_sync_record(ready, after_stream);
+    if (rc == ZS_OK) rc = zs_sync_wait(ready, stream);
+    return rc;
+  }
+  return ZS_OK;
+}
+
+int zs_all_gather_group_synced(zs_comm* c, int64_t n, const uint64_t* send, const uint64_t* recv,
+                               const int64_t* send_count, int dtype, uintptr_t after_stream,
+                               zs_sync* ready, uintptr_t stream, zs_sync* done) {
+  ZS_REQUIRE(n == 0 || (c && c->comm), "zs_all_gather_group_synced: NULL communicator");
+  int rc = synced_prologue(after_stream, ready, stream);
+  if (rc == ZS_OK && n > 0) rc = zs_all_gather_group(c, n, send, recv, send_count, dtype, stream);
+  if (rc == ZS_OK && done) rc = zs_sync_record(done, stream);
+  return rc;
+}
+
+int zs_reduce_scatter_group_synced(zs_comm* c, int64_t n, const uint64_t* send,
+                                   const uint64_t* recv, const int64_t* recv_count, int dtype,
+                                   uintptr_t after_stream, zs_sync* ready, uintptr_t stream,
+                                   zs_sync* done) {
+  ZS_REQUIRE(n == 0 || (c && c->comm), "zs_reduce_scatter_group_synced: NULL communicator");
+  int rc = synced_prologue(after_stream, ready, stream);
+  if (rc == ZS_OK && n > 0)
+    rc = zs_reduce_scatter_group(c, n, send, recv, recv_count, dtype, stream);
+  if (rc == ZS_OK && done) rc = zs_sync_record(done, stream);
+  return rc;
+}
+
 int zs_group_start(void) {
   ZS_NCCL(ncclGroupStart());
   return ZS_OK;

@@ -551,6 +551,10 @@ class Zero3ParamManager:
         self.shard_dim = shard_dim
         self.full_data = None
         self.runtime = runtime
+        if full_shape is None and shard is None and param.dim() > 0:
+            # the reference's standalone manager: param.data is this rank's dim-0 shard and the
+            # full tensor is the rank-ordered concatenation of ws equal shards (zero3.py:36-41)
+            full_shape = (world_size * param.shape[0],) + tuple(param.shape[1:])
         self.full_shape = tuple(full_shape if full_shape is not None else param.shape)
         self.shard = shard if shard is not None else param.data
         self.keep_full_grad = keep_full_grad

@@ -199,24 +199,25 @@ def test_zero3_fp8_standalone_manager_uses_set_kernels(gpu, ws, dtype, monkeypat
     """a standalone Zero3ParamManager's fp8 gather runs the module path's set
     kernels as a one-matrix set (zs_fp8_quantize_rowset / zs_fp8_dequantize_gathered), never the
     per-matrix zs_fp8_*_rows forms.  Every rank's send side is built by the manager itself; the
-    all-gather is emulated by concatenating them rank-major; the full tensor equals the row oracle
-    (uneven chunks: the last rank's padding rows).  A matrix whose rows are not a multiple of 8
-    elements gathers unquantised."""
+    all-gather is emulated by concatenating them rank-major; the full tensor (the reference's
+    torch.cat of ws equal shards, zero3.py:36-41) equals the row oracle.  A matrix whose rows are
+    not a multiple of 8 elements gathers unquantised."""
     from zero_amd import _lib, zero3
 
     called = []
     real_call = _lib.call
     monkeypatch.setattr(_lib, "call", lambda name, *a: (called.append(name), real_call(name, *a))[1])
     g = torch.Generator().manual_seed(ws)
-    full = (torch.randn(37, 64, generator=g) * 10.0 ** torch.randint(-3, 3, (37, 1), generator=g)).to(dtype)
+    d0 = 13 * ws
+    full = (torch.randn(d0, 64, generator=g) * 10.0 ** torch.randint(-3, 3, (d0, 1), generator=g)).to(dtype)
     full[5] = 0
-    cs = -(-37 // ws)
+    cs = 13
     st = torch.cuda.current_stream()
     states, mans = [], []
     for k in range(ws):
         p = torch.nn.Parameter(full[k * cs:(k + 1) * cs].contiguous().to(gpu))
         m = zero3.Zero3ParamManager(p, k, ws, gather_dtype="fp8")
-        assert m.fp8
+        assert m.fp8 and m.full_shape == (d0, 64) and m.cs == cs
         states.append(m._gather_prepare(st))
         mans.append(m)
     fq = torch.cat([s[0] for s in states])
@@ -224,7 +225,7 @@ def test_zero3_fp8_standalone_manager_uses_set_kernels(gpu, ws, dtype, monkeypat
     out = mans[0]._gather_finish(st, (None, None, fq, fsc, None))
     torch.cuda.synchronize()
     want = torch.from_numpy(fp8_rows_oracle(full)[2]).to(dtype)
-    assert torch.equal(out[:full.numel()].view(37, 64).cpu(), want)
+    assert torch.equal(out[:full.numel()].view(d0, 64).cpu(), want)
     assert "zs_fp8_quantize_rows" not in called and "zs_fp8_dequantize_rows" not in called
     assert called.count("zs_fp8_quantize_rowset") == ws and called.count("zs_fp8_dequantize_gathered") == 1
     odd = zero3.Zero3ParamManager(torch.nn.Parameter(torch.zeros(5, 12, device=gpu, dtype=dtype)), 0, 1,

@@ -25,7 +25,7 @@ case "$step" in
     tail -c 3000 "$O/bench_$tag.json"; tail -5 "$O/bench_$tag.err"; fatal $rc; echo "[bench $tag] rc=$rc";;
   kstats)  # rocprofv3 kernel trace + stats of a bench command: tools/r05.sh kstats <tag> <args>
     tag="$1"; shift
-    timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$O/prof_$tag" -o run -- \
+    timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$tag" -o run -- \
       python3 bench.py "$@" > "$O/kstats_$tag.json" 2> "$O/kstats_$tag.err"; rc=$?
     tail -c 1500 "$O/kstats_$tag.json"; fatal $rc
     find "$O/prof_$tag" -name '*kernel_stats.csv' -exec head -12 {} \; ; echo "[kstats $tag] rc=$rc";;
