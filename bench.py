@@ -550,8 +550,15 @@ class _NoComm:
     def reduce_scatter_group(self, send, recv, count, dtype, stream):
         pass
 
-    # the ordered forms keep the product's host path (events and stream waits in one library
-    # call) with the collective left out: zs_*_group_ordered with no communicator and n = 0
+    # the synced forms keep the product's host path (sync records and stream waits in one
+    # library call) with the collective left out: zs_*_group_synced with no communicator, n = 0
+    def all_gather_group_synced_bound(self, send, recv, count, dtype):
+        return self._ordered("zs_all_gather_group_synced", dtype)
+
+    def reduce_scatter_group_synced_bound(self, send, recv, count, dtype):
+        return self._ordered("zs_reduce_scatter_group_synced", dtype)
+
+    # (the event-ordered forms, which earlier rounds' runtimes bind: tools/z3_host_ab.py)
     def all_gather_group_ordered_bound(self, send, recv, count, dtype):
         return self._ordered("zs_all_gather_group_ordered", dtype)
 

@@ -11,7 +11,10 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <new>
+#include <vector>
 
 #include "zs_common.h"
 
@@ -325,10 +328,40 @@ int zs_stream_wait_event(uintptr_t stream, uint64_t event) {
 // time (its epochs then reach the word in order).
 struct zs_sync {
   int kind = ZS_SYNC_EVENT;
+  int device = 0;
   hipEvent_t event = nullptr;
   uint32_t* flag = nullptr;
   uint32_t epoch = 0;
 };
+
+namespace {
+// Flag words come from per-device slabs (one hipMalloc per 4096 flags, 64 B apart: one cache line
+// each): engines create a few hundred syncs, not a few hundred tiny device allocations.
+constexpr int kFlagsPerSlab = 4096;
+constexpr size_t kFlagStride = 64;
+std::mutex g_flag_mu;
+std::map<int, std::vector<uint32_t*>> g_flag_free;
+
+hipError_t flag_take(int device, uint32_t** out) {
+  std::lock_guard<std::mutex> lk(g_flag_mu);
+  auto& fl = g_flag_free[device];
+  if (fl.empty()) {
+    unsigned char* slab = nullptr;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&slab), kFlagsPerSlab * kFlagStride);
+    if (e != hipSuccess) return e;
+    // zeroed and COMPLETE before any word is handed out: a record on another stream must never
+    // be overtaken by the zero fill
+    e = hipMemsetAsync(slab, 0, kFlagsPerSlab * kFlagStride, nullptr);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    if (e != hipSuccess) return e;
+    for (int i = kFlagsPerSlab - 1; i >= 0; --i)
+      fl.push_back(reinterpret_cast<uint32_t*>(slab + size_t(i) * kFlagStride));
+  }
+  *out = fl.back();
+  fl.pop_back();
+  return hipSuccess;
+}
+}  // namespace
 
 int zs_sync_create(int kind, zs_sync** out) {
   ZS_REQUIRE(out != nullptr, "zs_sync_create: out is NULL");
@@ -337,10 +370,14 @@ int zs_sync_create(int kind, zs_sync** out) {
   zs_sync* s = new (std::nothrow) zs_sync();
   if (!s) return zs::fail(ZS_ERR_NOMEM, "zs_sync_create: out of memory");
   s->kind = kind;
-  hipError_t e = kind == ZS_SYNC_EVENT
-                     ? hipEventCreateWithFlags(&s->event, hipEventDisableTiming)
-                     : hipMalloc(reinterpret_cast<void**>(&s->flag), 64);
-  if (e == hipSuccess && s->flag) e = hipMemset(s->flag, 0, 64);
+  hipError_t e = hipGetDevice(&s->device);
+  if (e == hipSuccess) {
+    if (kind == ZS_SYNC_EVENT) {
+      e = hipEventCreateWithFlags(&s->event, hipEventDisableTiming);
+    } else {
+      e = flag_take(s->device, &s->flag);  // (zeroed with its slab: epoch 0)
+    }
+  }
   if (e != hipSuccess) {
     zs_sync_destroy(s);
     return zs::fail(ZS_ERR_HIP, "zs_sync_create: %s", hipGetErrorString(e));
@@ -352,7 +389,9 @@ int zs_sync_create(int kind, zs_sync** out) {
 int zs_sync_destroy(zs_sync* s) {
   if (!s) return ZS_OK;
   if (s->event) (void)hipEventDestroy(s->event);
-  if (s->flag) (void)hipFree(s->flag);
+  // a flag word may still be written by a queued record or read by a queued wait, and finding
+  // out would synchronise the device from a destructor: the word is abandoned, not recycled
+  // (64 B; a destroyed sync is rare — an engine going away)
   delete s;
   return ZS_OK;
 }

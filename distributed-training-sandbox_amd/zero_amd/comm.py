@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import os
 
 import torch
 import torch.distributed as dist
@@ -198,6 +199,18 @@ class RcclComm:
         all_gather_group_ordered_bound)."""
         return self._ordered(_lib.lib.zs_reduce_scatter_group_ordered, send, recv, count, dtype)
 
+    def all_gather_group_synced_bound(self, send, recv, count, dtype: int):
+        """all_gather_group_bound with the ordering in the same call through sync objects
+        (zs_all_gather_group_synced): ``run(after_stream, ready_sync, stream, done_sync)`` on raw
+        handles (a sync may be 0) — record ``ready_sync`` on ``after_stream``, make ``stream`` wait
+        for it, the group, record ``done_sync`` on ``stream``.  A sync is a HIP event or a stream
+        flag (``Sync``)."""
+        return self._ordered(_lib.lib.zs_all_gather_group_synced, send, recv, count, dtype)
+
+    def reduce_scatter_group_synced_bound(self, send, recv, count, dtype: int):
+        """reduce_scatter_group_bound with sync-object ordering (see all_gather_group_synced_bound)."""
+        return self._ordered(_lib.lib.zs_reduce_scatter_group_synced, send, recv, count, dtype)
+
     def _ordered(self, fn, send, recv, count, dtype):
         n = len(count)
         sp, rp, cp = send.ctypes.data_as(_PU64), recv.ctypes.data_as(_PU64), count.ctypes.data_as(_PI64)
@@ -224,6 +237,83 @@ class RcclComm:
         _lib.call("zs_broadcast_group", self._h, len(count), buf.ctypes.data_as(_PU64),
                   count.ctypes.data_as(_PI64), root.ctypes.data_as(_PI32), int(dtype),
                   stream_handle(stream))
+
+
+class Sync:
+    """A cross-stream ordering point (``zs_sync``, include/zero_amd.h): a HIP event
+    (``kind=_lib.ZS_SYNC_EVENT``) or a stream memory operation on a device flag word
+    (``_lib.ZS_SYNC_FLAG``: hipStreamWriteValue32 of an epoch on the producer stream,
+    hipStreamWaitValue32 >= it on the consumer).  A wait on a pending HIP event keeps one HIP
+    runtime thread polling for as long as it is pending; a flag wait is resolved by the GPU and
+    costs the host nothing (profiles/r05_event_poll_probe.jsonl).  ``record(stream_h)`` /
+    ``wait(stream_h)`` take raw stream handles; ``h`` is the raw handle the synced group calls
+    take.  A flag sync is recorded from one stream at a time (its epochs reach the word in order)."""
+
+    __slots__ = ("h", "kind")
+
+    def __init__(self, kind: int):
+        h = ctypes.c_void_p()
+        _lib.call("zs_sync_create", int(kind), ctypes.byref(h))
+        self.h, self.kind = int(h.value), int(kind)
+
+    def record(self, stream_h: int) -> None:
+        rc = _lib.lib.zs_sync_record(self.h, stream_h)
+        if rc:
+            _lib.check(rc, "zs_sync_record")
+
+    def wait(self, stream_h: int) -> None:
+        rc = _lib.lib.zs_sync_wait(self.h, stream_h)
+        if rc:
+            _lib.check(rc, "zs_sync_wait")
+
+    def __del__(self):
+        h = getattr(self, "h", 0)
+        if h and _lib is not None:
+            try:
+                _lib.lib.zs_sync_destroy(h)
+            except Exception:  # interpreter teardown
+                pass
+            self.h = 0
+
+
+# Cross-stream ordering of every engine's collective stream (ZeRO-1/2 rounds, overlap buckets, DDP
+# buckets, ZeRO-3 gathers and reduce-scatters): "flag" (stream memory operations, resolved by the
+# GPU) or "event" (HIP events: a pending cross-stream wait keeps one HIP runtime thread polling —
+# about one core for as long as the host runs ahead of the GPU, profiles/r05_event_poll_probe.jsonl).
+# ``ZERO_AMD_STREAM_SYNC`` overrides the default (A/B runs).
+STREAM_SYNC = os.environ.get("ZERO_AMD_STREAM_SYNC", "flag")
+
+
+def _stream_h(stream) -> int:
+    if stream is None:
+        return torch._C._cuda_getCurrentRawStream(torch.cuda.current_device())
+    return stream if isinstance(stream, int) else int(stream.cuda_stream)
+
+
+class StreamEvent:
+    """The ordering surface of a non-timing ``torch.cuda.Event`` — ``record(stream=None)``,
+    ``wait(stream=None)``, so ``torch.cuda.Stream.wait_event(ev)`` takes it — over a ``Sync`` of
+    the process default kind (``STREAM_SYNC``): the engines' cross-stream ordering without a HIP
+    runtime thread polling.  Recorded from one stream at a time (see ``Sync``)."""
+
+    __slots__ = ("sync",)
+
+    def __init__(self, kind: str | None = None):
+        self.sync = Sync(sync_kind(kind or STREAM_SYNC))
+
+    def record(self, stream=None) -> None:
+        self.sync.record(_stream_h(stream))
+
+    def wait(self, stream=None) -> None:
+        self.sync.wait(_stream_h(stream))
+
+
+def sync_kind(name: str) -> int:
+    """"flag" / "event" -> the zs_sync kind."""
+    kinds = {"flag": _lib.ZS_SYNC_FLAG, "event": _lib.ZS_SYNC_EVENT}
+    if name not in kinds:
+        raise ValueError(f"stream_sync must be 'flag' or 'event' (got {name!r})")
+    return kinds[name]
 
 
 _PU64 = ctypes.POINTER(ctypes.c_uint64)

@@ -36,7 +36,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .comm import comm_stream, zs_dtype
+from .comm import StreamEvent, comm_stream, zs_dtype
 from .kernels import AdamSet, CopySet, adam_hparams
 from .plan import Plan
 
@@ -328,7 +328,7 @@ class ShardEngine:
             self.buckets = [self.plan.bucket(k) for k in range(self.K)]
             self.segs = [self.plan.segments(k) for k in range(self.K)]
             self.comm_stream = comm_stream(dev)
-            mk = lambda: [torch.cuda.Event() for _ in range(self.K)]  # noqa: E731
+            mk = lambda: [StreamEvent() for _ in range(self.K)]  # noqa: E731
             self.ev_pack, self.ev_rs, self.ev_adam, self.ev_ag = mk(), mk(), mk(), mk()
         self.ev_c0 = torch.cuda.Event(enable_timing=True)
         self.ev_c1 = torch.cuda.Event(enable_timing=True)
@@ -644,7 +644,7 @@ class ShardEngine:
         self.gb = GradBuckets(self.params, owner, bucket_bytes, self._overlap_reduce)
         pc = self.pieces
         self._so_of = {int(i): int(so) for i, so, n in zip(pc.param, pc.stream_off, pc.length)}
-        mk = lambda: [torch.cuda.Event() for _ in range(self.gb.K)]  # noqa: E731
+        mk = lambda: [StreamEvent() for _ in range(self.gb.K)]  # noqa: E731
         self.ev_oadam, self.ev_obc = mk(), mk()
         return self.gb
 

@@ -42,6 +42,7 @@ import torch
 
 from . import _lib
 from ._hooks import WeakCall
+from .comm import StreamEvent
 from .engine import ALIGN_ELEMS, ShardEngine, _ptr
 from .kernels import check_extents, check_extents_enabled, copy_direct
 
@@ -131,9 +132,10 @@ class FlatEngine(ShardEngine):
         self.K = max(1, -(-int(self.Ls.max()) // W))
         self.rounds = [self._make_round(j) for j in range(self.K)]
         self._views = [None] * n  # the grad views handed out (identity = "still the view")
-        mk = lambda: [torch.cuda.Event() for _ in range(self.K)]  # noqa: E731
+        # cross-stream ordering points (comm.StreamEvent: stream flags unless ZERO_AMD_STREAM_SYNC)
+        mk = lambda: [StreamEvent() for _ in range(self.K)]  # noqa: E731
         self.ev_red, self.ev_adam, self.ev_bc = mk(), mk(), mk()
-        self.ev_grads = torch.cuda.Event()
+        self.ev_grads = StreamEvent()
         self.ev_c0 = torch.cuda.Event(enable_timing=True)
         self.ev_c1 = torch.cuda.Event(enable_timing=True)
         self.capture_reduced = None  # optional tensor: a copy of R after the reduces (checks)
@@ -158,6 +160,7 @@ class FlatEngine(ShardEngine):
         # set of fresh gradients (the reference holds one set)
         self.land_batch_bytes = LAND_BATCH_BYTES
         self.land_pending, self.land_pending_bytes = [], 0
+        self.land_marked = np.zeros(n, bool)
         self.inplace_reads = 0  # gradients the last step's Adam read in place (ws == 1)
 
     # ------------------------------------------------------------------------------------------
@@ -250,6 +253,7 @@ class FlatEngine(ShardEngine):
             self.dirty[:] = False
             self.install_views()
         self.land_pending, self.land_pending_bytes = [], 0
+        self.land_marked[:] = False
         self.zero_grad_calls += 1
         self.touched[:] = False
         self.any_touched = False
@@ -339,7 +343,8 @@ class FlatEngine(ShardEngine):
         if self.inplace or not self.adopt_fresh:
             return  # ws == 1 reads fresh grads in place; ZeRO-1's carry needs the caller's tensors
         g = self.params[i].grad
-        if g is not None and not self.is_view(i, g):  # fresh: land with the next batch
+        if g is not None and not self.is_view(i, g) and not self.land_marked[i]:  # fresh: land
+            self.land_marked[i] = True  # with the next batch (once, however often accumulated)
             self.land_pending.append(i)
             self.land_pending_bytes += g.numel() * g.element_size()
             if self.land_pending_bytes >= self.land_batch_bytes:
@@ -353,6 +358,7 @@ class FlatEngine(ShardEngine):
         if not idx:
             return
         self.land_pending, self.land_pending_bytes = [], 0
+        self.land_marked[idx] = False
         cur = torch.cuda.current_stream(self.device) if stream is None else stream
         live = [i for i in idx if self.params[i].grad is not None
                 and not self.is_view(i, self.params[i].grad)]
@@ -439,7 +445,8 @@ class FlatEngine(ShardEngine):
         # re-counted at the first hook of a backward if requires_grad changed since
         self.ov_req = self._requires_grad()
         self.ov_size = np.array([int(self.ov_req[g].sum()) for g in groups], np.int64)
-        self.ov_ev = [torch.cuda.Event() for _ in range(self.ov_K)]
+        self.ov_ev = [StreamEvent() for _ in range(self.ov_K)]
+        self.ov_ev_ready = [StreamEvent() for _ in range(self.ov_K)]  # recorded where backward ran
         own = np.nonzero(self.ov_owner == self.rank)[0]
         self.ov_last_own = int(own[-1]) if len(own) else -1
         self.overlap = True
@@ -514,7 +521,7 @@ class FlatEngine(ShardEngine):
         if self.ws == 1:  # nothing to exchange: Adam reads Gc (= G unless converted)
             self.ov_ev[k].record(cur)
             return
-        ev = torch.cuda.Event()
+        ev = self.ov_ev_ready[k]
         ev.record(cur)
         cs = self.comm_stream
         cs.wait_event(ev)
@@ -656,6 +663,7 @@ class FlatEngine(ShardEngine):
                                        gptr=None if gptr is None else gptr[idx])
             if self.inplace:
                 if self.overlap:
+                    self.launched_in_backward = self.ov_launched
                     self._ov_reset()
                 return  # fresh gradients stay the caller's p.grad (read in place)
             self._reinstall(has, view)

@@ -29,7 +29,7 @@ import numpy as np
 import torch
 
 from ._hooks import WeakCall
-from .comm import comm_stream
+from .comm import StreamEvent, comm_stream
 from .kernels import CopySet
 
 ALIGN = 64  # elements: every slot 16-byte aligned for the vector kernels
@@ -93,8 +93,8 @@ class GradBuckets:
 
         self.buf, self.placement = probed_zeros(max(off, align), self.dtype, self.device)
         self.comm_stream = comm_stream(self.device)
-        self.ev_ready = [torch.cuda.Event() for _ in range(self.K)]
-        self.ev_done = [torch.cuda.Event() for _ in range(self.K)]
+        self.ev_ready = [StreamEvent() for _ in range(self.K)]  # (comm.StreamEvent: stream flags)
+        self.ev_done = [StreamEvent() for _ in range(self.K)]
         self._size = np.array([len(g) for g in self.groups], np.int64)
         self._cache = {}
         self.retired = []

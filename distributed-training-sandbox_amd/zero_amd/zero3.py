@@ -50,7 +50,7 @@ from ._lib import ZS_BF16, ZS_BF16_SPLIT, ZS_F32
 from . import checkpoint as ckpt
 from ._hooks import WeakCall
 from ._sharded import adam_group_hparams
-from .comm import RcclComm, comm_stream, zs_dtype
+from .comm import STREAM_SYNC, RcclComm, Sync, comm_stream, sync_kind, zs_dtype
 from .engine import ALIGN_ELEMS, probed_zeros
 from .kernels import AdamSet, adam_hparams, stream_handle
 from .training_utils.utils import get
@@ -143,8 +143,12 @@ class _GatherRuntime:
     that polls while a cross-stream dependency is pending (≈ one core for as long as the host runs
     ahead of the GPU: profiles/r04_hip_event_cost.jsonl)."""
 
-    def __init__(self, ws, rank, comm, device, wave: int = 1, side_stream: bool = True):
+    def __init__(self, ws, rank, comm, device, wave: int = 1, side_stream: bool = True,
+                 stream_sync: str | None = None):
         self.ws, self.rank, self.comm, self.device = ws, rank, comm, device
+        # the cross-stream ordering: stream flags (the GPU resolves the wait; no HIP runtime
+        # thread polls while one is pending) or HIP events (comm.Sync)
+        self.sync_kind = sync_kind(stream_sync or STREAM_SYNC)
         if int(wave) < 1:
             raise ValueError(f"gather wave must be >= 1 (got {wave})")
         self.wave = int(wave)
@@ -167,20 +171,28 @@ class _GatherRuntime:
         self.gather_events = None  # optional list of (start, end, bus_bytes) per gather group
         self._tables = {}          # key -> grouped all-gather pointer table (see _table)
         self._fp8_tables = {}      # key -> fp8 gather tables (see _fp8_plan)
-        # key -> (ready, done) events, re-recorded every iteration: a wait enqueued on an event
-        # keeps the record it saw, and a key's next launch comes after its materialise has
-        # enqueued that wait (creating two HIP events per gather cost host time every iteration)
-        self._events = {}
+        # (key, producing stream) -> ready sync and key -> done sync, re-recorded every iteration:
+        # a wait enqueued on a sync keeps the record it saw, and a key's next launch comes after
+        # its materialise has enqueued that wait (creating them per gather cost host time)
+        self._syncs = {}
         self.iteration_callbacks = []  # called by end_iteration (hook bookkeeping resets)
 
-    def _key_events(self, key):
-        ev = self._events.get(key)
-        if ev is None:
-            a, b = torch.cuda.Event(), torch.cuda.Event()
-            a.record(self.stream)  # torch creates the HIP event at its first record: the raw
-            b.record(self.stream)  # handles below are what the ordered library calls record
-            ev = self._events[key] = (a, b, a.cuda_event, b.cuda_event)
-        return ev
+    def _ready_sync(self, key, cur_h) -> Sync:
+        """The sync the consumer stream ``cur_h`` records before ``key``'s gather (one per stream:
+        a flag is recorded from one stream at a time)."""
+        k = ("ready", key, cur_h)
+        sy = self._syncs.get(k)
+        if sy is None:
+            sy = self._syncs[k] = Sync(self.sync_kind)
+        return sy
+
+    def _done_sync(self, key) -> Sync:
+        """The sync the side stream records after ``key``'s gather, its consumers wait on."""
+        k = ("done", key)
+        sy = self._syncs.get(k)
+        if sy is None:
+            sy = self._syncs[k] = Sync(self.sync_kind)
+        return sy
 
     def _cur_h(self) -> int:
         return torch._C._cuda_getCurrentRawStream(self._dev_idx)
@@ -201,10 +213,11 @@ class _GatherRuntime:
                                  None)
             self.n_gathers += 1
             return
-        ev_ready, ev, ready_h, ev_h = self._key_events(key)
-        self._waited.pop(ev_h, None)  # re-recorded below: no consumer has waited on this record
         if cur_h is None:
             cur_h = self._cur_h()
+        ready, done = self._ready_sync(key, cur_h), self._done_sync(key)
+        ready_h, ev_h = ready.h, done.h
+        self._waited.pop(ev_h, None)  # re-recorded below: no consumer has waited on this record
         timed = self.gather_events is not None and self.ws > 1
         plan = self._tables[key] if key in self._tables else self._table(key, managers)
         if plan is not None and plan[-1] is not None and not timed and self.stream is None:
@@ -219,21 +232,21 @@ class _GatherRuntime:
             return
         side = self.side()
         if plan is not None and plan[-1] is not None and not timed:
-            # one allocation for the module's full tensors and ONE library call: ready event on
+            # one allocation for the module's full tensors and ONE library call: ready sync on
             # the compute stream (the shards may just have been updated), the side stream's wait,
-            # the RCCL group of all-gathers (zero-copy from the chunk-arena slots), the done event
+            # the RCCL group of all-gathers (zero-copy from the chunk-arena slots), the done sync
             send, count, offs, total, dt, es, views, recv, raw, ordered = plan
             hold = torch.empty(total, dtype=managers[0].shard.dtype, device=self.device)
             hold.record_stream(side)
             np.add(offs, np.uint64(hold.data_ptr()), out=recv)
             ordered(cur_h, ready_h, self._side_h, ev_h)
             self.pending[key] = ([(m, hold.as_strided(shape, stride, off)) for m, (shape, stride, off)
-                                  in zip(managers, views)], ev, hold, cur_h, ev_h)
+                                  in zip(managers, views)], done, hold, cur_h, ev_h)
             self.n_gathers += 1
             return
-        cur = torch.cuda.current_stream(self.device)
-        ev_ready.record(cur)  # shards may just have been updated
-        side.wait_event(ev_ready)
+        side_h = self._side_h if self.stream is not None else cur_h
+        ready.record(cur_h)  # shards may just have been updated
+        ready.wait(side_h)
         if timed:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record(side)
@@ -274,11 +287,11 @@ class _GatherRuntime:
                     for m, st in zip(managers, states):
                         m._gather_issue(self.comm, side, st)
                 out = [(m, m._gather_finish(side, st)) for m, st in zip(managers, states)]
-        ev.record(side)
+        done.record(side_h)
         if timed:  # ring all-gather bus bytes: (ws-1)/ws of the gathered tensor, per rank
             bus = sum(m.gather_bytes() for m in managers) * (self.ws - 1)
             self.gather_events.append((e0, _timed_after(side), bus))
-        self.pending[key] = (out, ev, hold, cur_h, ev_h)
+        self.pending[key] = (out, done, hold, cur_h, ev_h)
         self.n_gathers += 1
 
     def _table(self, key, managers):
@@ -315,8 +328,8 @@ class _GatherRuntime:
             bind = getattr(self.comm, "all_gather_group_bound", None)
             if bind is not None:
                 raw = bind(send, recv, count, dt)
-            bind = getattr(self.comm, "all_gather_group_ordered_bound", None)
-            if bind is not None:
+            bind = getattr(self.comm, "all_gather_group_synced_bound", None)
+            if bind is not None:  # ordering through sync objects (ready / done), one call
                 ordered = bind(send, recv, count, dt)
             plan = (send, count, np.array(offs, np.uint64) * np.uint64(es), max(o, 1), dt, es,
                     views, recv, raw, ordered)
@@ -429,12 +442,13 @@ class _GatherRuntime:
                 self.launch(k, ms, cur_h)
             return
         single = self.stream is None
-        if single:  # everything on the consumer's stream: no events
+        if single:  # everything on the consumer's stream: nothing to order
             ready_h = done_h = 0
             done_ev = None
         else:
-            ready_h = self._key_events(todo[0][0])[2]
-            _, done_ev, _, done_h = self._key_events(todo[-1][0])
+            ready_h = self._ready_sync(todo[0][0], cur_h).h
+            done_ev = self._done_sync(todo[-1][0])
+            done_h = done_ev.h
             self._waited.pop(done_h, None)
         last = len(todo) - 1
         side, side_h = self.stream, (cur_h if single else self._side_h)
@@ -493,9 +507,9 @@ class _GatherRuntime:
             return
         if wait_h is not None:
             if self._waited.get(wait_h) != cur_h:  # once per wave and consuming stream
-                rc = _lib.lib.zs_stream_wait_event(cur_h, wait_h)
+                rc = _lib.lib.zs_sync_wait(wait_h, cur_h)
                 if rc:
-                    _lib.check(rc, "zs_stream_wait_event")
+                    _lib.check(rc, "zs_sync_wait")
                 self._waited[wait_h] = cur_h
         elif alloc_h is not None and alloc_h != cur_h:
             # single-stream mode, gathered on another stream than this one: order the two
@@ -650,10 +664,10 @@ class Zero3ParamManager:
         rt = self._runtime()
         key = ("param", id(self))
         rt.launch(key, [self])
-        out, ev, hold, _, _ = rt.pending.pop(key)
+        out, done, hold, _, _ = rt.pending.pop(key)
         cur = torch.cuda.current_stream(self.shard.device)
-        if ev is not None:
-            cur.wait_event(ev)
+        if done is not None:
+            done.wait(cur.cuda_stream)
         if hold is not None:
             hold.record_stream(cur)
         for m, full in out:
@@ -1003,18 +1017,25 @@ class _GradReducer:
         self._S_l = [int(x) for x in arena.S]
         self._N_l = [int(x) for x in arena.numel]
         self._shard_grad = [None] * n  # cached grad-arena views handed out as shard grads
-        self.ev_done = [torch.cuda.Event() for _ in range(self.K)]
-        self.ev_ready = [torch.cuda.Event() for _ in range(self.K)]
+        # per bucket: the sync the side stream records after its reduce-scatter (step() and the
+        # shard grads wait on the last one) and, per producing stream, the one recorded before it
+        kind = opt.runtime.sync_kind
+        self.ev_done = [Sync(kind) for _ in range(self.K)]
+        self._done_h = [e.h for e in self.ev_done]
+        self._ready = {}  # (bucket, stream handle) -> Sync
+        self._sync_kind = kind
         cs = opt.runtime.stream if opt.world_size > 1 else None  # (None: single-stream mode)
-        if cs is not None:  # torch creates a HIP event at its first record: the raw handles are
-            for e in self.ev_done + self.ev_ready:  # what the ordered library calls record
-                e.record(cs)
-            self._done_h = [e.cuda_event for e in self.ev_done]
-            self._ready_h = [e.cuda_event for e in self.ev_ready]
+        if cs is not None:
             self._cs_h = cs.cuda_stream
         self.timing = None  # optional list of (start, end, bus_bytes) per launched bucket
         self._rs_tables = {}
         self.reset()
+
+    def _ready_sync(self, k: int, cur_h: int) -> Sync:
+        sy = self._ready.get((k, cur_h))
+        if sy is None:
+            sy = self._ready[(k, cur_h)] = Sync(self._sync_kind)
+        return sy
 
     def reset(self):
         n = len(self.opt.params)
@@ -1065,9 +1086,8 @@ class _GradReducer:
         opt = self.opt
         if opt.world_size == 1:
             return
-        cur = torch.cuda.current_stream(opt._arena.device)
         if self.K and opt.runtime.stream is not None:
-            cur.wait_event(self.ev_done[self.K - 1])
+            self.ev_done[self.K - 1].wait(opt.runtime._cur_h())
         if opt._G.dtype != opt.params[0].dtype:  # a bf16 exchange's chunks stay internal
             return
         shapes, views = opt._arena.shard_shapes, self._shard_grad
@@ -1093,7 +1113,7 @@ class _GradReducer:
             send = np.zeros(len(idx), np.uint64)  # refilled per launch with the grads' addresses
             bind = getattr(opt.comm, "reduce_scatter_group_bound", None)
             raw = bind(send, recv, count, zs_dtype(G.dtype)) if bind is not None else None
-            bind = getattr(opt.comm, "reduce_scatter_group_ordered_bound", None)
+            bind = getattr(opt.comm, "reduce_scatter_group_synced_bound", None)
             ordered = bind(send, recv, count, zs_dtype(G.dtype)) if bind is not None else None
             t = (recv, count, zs_dtype(G.dtype), send, raw, ordered)
             self._rs_tables[k] = t
@@ -1162,19 +1182,20 @@ class _GradReducer:
             cur = torch.cuda.current_stream(dev)
         cs = cur if single else opt.runtime.stream
         if tab is not None and tab[5] is not None and self.timing is None:
-            # ONE library call: ready event on the stream that produced the grads, the side
-            # stream's wait, the bucket's RCCL group of reduce-scatters, the done event
+            # ONE library call: ready sync on the stream that produced the grads, the side
+            # stream's wait, the bucket's RCCL group of reduce-scatters, the done sync
             recv, count, dt, sp, raw, ordered = tab
             for j, (_, t) in enumerate(sends):
                 sp[j] = t.data_ptr()
-            ordered(cur_h, self._ready_h[k], self._cs_h, self._done_h[k])
+            ordered(cur_h, self._ready_sync(k, cur_h).h, self._cs_h, self._done_h[k])
             for i, send in sends:
                 send.record_stream(cs)
                 opt.params[i].grad = None
             return
-        ready = self.ev_ready[k]
-        ready.record(cur)
-        cs.wait_event(ready)
+        cs_h = cs.cuda_stream
+        ready = self._ready_sync(k, cur_h)
+        ready.record(cur_h)
+        ready.wait(cs_h)
         if self.timing is not None:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record(cs)
@@ -1195,7 +1216,7 @@ class _GradReducer:
         for i, send in sends:
             send.record_stream(cs)
             opt.params[i].grad = None
-        self.ev_done[k].record(cs)
+        self.ev_done[k].record(cs_h)
         if self.timing is not None:
             bus = sum(int(ar.S[i]) * ws for i, _ in sends) * opt._G.element_size() * (ws - 1) / ws
             self.timing.append((e0, _timed_after(cs), bus))
@@ -1216,6 +1237,9 @@ RS_BUCKET_MB = 512.0
 # module of a wave waits for both of its gathers; its host-time win was measured on the
 # compute-free parameter-set model only, which the bench now runs single-stream.
 GATHER_WAVE = 1
+# Cross-stream ordering of the side-stream collectives: comm.STREAM_SYNC ("flag": stream memory
+# operations on a device word, resolved by the GPU; "event": HIP events, whose pending cross-stream
+# waits keep a HIP runtime thread polling — profiles/r05_event_poll_probe.jsonl)
 
 
 class ShardedOptimizer:
@@ -1223,7 +1247,8 @@ class ShardedOptimizer:
 
     def __init__(self, optimizer: Optimizer, *, update: bool = False, comm=None, sync: bool = True,
                  gather_dtype=None, bucket_mb: float = RS_BUCKET_MB, grad_comm: str | None = None,
-                 gather_wave: int = GATHER_WAVE, side_stream: bool = True):
+                 gather_wave: int = GATHER_WAVE, side_stream: bool = True,
+                 stream_sync: str = STREAM_SYNC):
         if not isinstance(optimizer, torch.optim.Adam):
             raise TypeError("zero_amd ShardedOptimizer wraps torch.optim.Adam / AdamW")
         self.optimizer = optimizer
@@ -1262,6 +1287,7 @@ class ShardedOptimizer:
             comm = RcclComm()
         self.comm = comm
         self.runtime = _GatherRuntime(world_size, rank, comm, dev, wave=gather_wave,
+                                      stream_sync=stream_sync,
                                       side_stream=side_stream)
         # zero3.py:104-110: every param becomes its dim-0 chunk — here a view of the chunk arena
         # (the full tensor is released); one manager per param
@@ -1368,10 +1394,12 @@ class ShardedOptimizer:
                 shards.append((pad, n, g.shape))
             else:
                 shards.append((g.contiguous(), n, g.shape))
-        ready = torch.cuda.Event()
-        ready.record(cur)
         cs = self.runtime.side()
-        cs.wait_event(ready)
+        if getattr(self, "_ref_syncs", None) is None:  # (ready, done): reused every step
+            self._ref_syncs = (Sync(self.runtime.sync_kind), Sync(self.runtime.sync_kind))
+        ready, done_sync = self._ref_syncs
+        ready.record(cur.cuda_stream)
+        ready.wait(cs.cuda_stream)
         with _group_ctx(self.comm):
             for buf, _, _ in shards:
                 self.comm.all_reduce(buf, cs)
@@ -1381,8 +1409,9 @@ class ShardedOptimizer:
                                        for buf, n, shp in shards]
         for buf, _, _ in shards:
             buf.record_stream(cs)
-        done = _timed_after(cs)
-        cur.wait_event(done)
+        done = _timed_after(cs)  # (the communication_time span's end)
+        done_sync.record(cs.cuda_stream)
+        done_sync.wait(cur.cuda_stream)
         for param in self.params:  # zero3.py:150-153 for-else: every grad is dropped
             param.grad = None
         return done
@@ -1422,7 +1451,7 @@ class ShardedOptimizer:
                 done.record(cur)
             else:
                 done = red.ev_done[red.K - 1]
-                cur.wait_event(done)
+                done.wait(cur.cuda_stream)
         idx = np.nonzero(red.had_grad & (ar.ln > 0))[0]
         self._steps[idx] += 1
         hps = {gi: adam_group_hparams(self._groups[gi], self.optimizer) for gi in set(self._group_of)}

@@ -88,38 +88,72 @@ def test_overlap_unused_param_keeps_value(gpu, pg1):
     assert "exp_avg" in opt.optimizer.state[ps[0]]
 
 
+class _NoComm:
+    """Collectives as no-ops: rank 0 of a simulated two-rank job (the landing path only)."""
+
+    def reduce_out(self, send, recv, root, stream):
+        pass
+
+    def broadcast(self, t, root, stream):
+        pass
+
+    def reduce(self, t, root, stream):
+        pass
+
+
+@pytest.mark.parametrize("ws", [1, 2])
 @pytest.mark.parametrize("overlap", [False, True])
-def test_zero2_flat_zero_grad_sets_none_then_adopts(gpu, pg1, overlap):
+def test_zero2_flat_zero_grad_sets_none_then_adopts(gpu, pg1, overlap, ws, monkeypatch):
     """ZeRO-2 on the flat arena: zero_grad() leaves p.grad None (the reference's state after
-    zero_grad); backward's fresh gradient lands in its arena slot — with its bucket during backward
-    (overlap: p.grad becomes the slot's view there) or in step() (one zs_copy_direct launch), a
-    second backward accumulating in the fresh tensor first — and p.grad is the slot's view after
-    step(); zero_grad(set_to_none=False) hands out zeroed views; ZeRO-1 keeps zeroed views."""
+    zero_grad).  ws = 1: step() reads backward's fresh gradient in place — p.grad stays backward's
+    tensor and no gradient arena exists until grad views are asked for.  ws > 1 (rank 0 of a
+    simulated two-rank job): the fresh gradient lands in its arena slot — with its bucket during
+    backward (overlap: p.grad becomes the slot's view there), else from the hooks in batches or at
+    step() — a second backward accumulating in the fresh tensor first — and p.grad is the slot's
+    view after step().  zero_grad(set_to_none=False) hands out zeroed views; ZeRO-1 keeps zeroed
+    views."""
+    import zero_amd._sharded as sh
     from zero_amd import zero1, zero2
 
+    kw = {}
+    if ws > 1:
+        monkeypatch.setattr(sh, "get", lambda what, dm=None: {"ws": ws, "rank": 0}[what])
+        kw["comm"] = _NoComm()
     ps = [torch.nn.Parameter(torch.randn(64, 8, device=gpu)) for _ in range(3)]
     opt = zero2.ShardedOptimizer(torch.optim.Adam(ps, lr=1e-2), overlap=overlap,
-                                 overlap_bucket_mb=1e-3)
+                                 overlap_bucket_mb=1e-3, **kw)
     eng = opt.engine
+    assert eng.inplace == (ws == 1) and (eng.G is None) == (ws == 1)
     opt.zero_grad()
     assert all(p.grad is None for p in ps)
     w = [torch.randn(64, 8, device=gpu) for _ in ps]
     sum((p * x).sum() for p, x in zip(ps, w)).backward()
+    landed = overlap and ws > 1
     for i, (p, x) in enumerate(zip(ps, w)):
-        assert eng.is_view(i, p.grad) == overlap and torch.equal(p.grad, x)
+        assert eng.is_view(i, p.grad) == landed and torch.equal(p.grad, x)
     if not overlap:
         sum((p * x).sum() for p, x in zip(ps, w)).backward()
         for p, x in zip(ps, w):
             assert torch.equal(p.grad, x + x)
+    fresh = [p.grad for p in ps]
     opt.step()
     for i, (p, x) in enumerate(zip(ps, w)):
-        assert eng.is_view(i, p.grad) and torch.equal(p.grad, x if overlap else x + x)
+        assert torch.equal(p.grad, x if overlap else x + x)
+        if ws == 1:  # read in place: still backward's own tensor
+            assert p.grad is fresh[i] and not eng.is_view(i, p.grad)
+        else:
+            assert eng.is_view(i, p.grad)
+    if ws == 1:
+        assert eng.G is None and eng.inplace_reads == len(ps)
     opt.zero_grad(set_to_none=False)
     assert all(eng.is_view(i, p.grad) and not p.grad.any() for i, p in enumerate(ps))
     q = torch.nn.Parameter(torch.randn(8, device=gpu))
-    z1 = zero1.ShardedOptimizer(torch.optim.Adam([q], lr=1e-2))
+    z1 = zero1.ShardedOptimizer(torch.optim.Adam([q], lr=1e-2), **kw)
     z1.zero_grad()
-    assert q.grad is not None and not q.grad.any() and z1.engine.is_view(0, q.grad)
+    if ws > 1:  # the carry needs the views
+        assert q.grad is not None and not q.grad.any() and z1.engine.is_view(0, q.grad)
+    else:  # no carry at ws = 1: None, as the reference's optimizer.zero_grad()
+        assert q.grad is None
 
 
 def test_overlap_double_backward_raises(gpu, pg1):

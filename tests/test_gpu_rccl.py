@@ -101,6 +101,7 @@ def _zero3_cases(ws):
                  ("_update_hooks", "traj_z2_ws2_d16_distinct.npz"),
                  ("_update_hooks_single", "traj_z2_ws2_d16_distinct.npz"),
                  ("_update_hooks_wave3", "traj_z2_ws2_d16_distinct.npz"),
+                 ("_update_hooks_events", "traj_z2_ws2_d16_distinct.npz"),
                  ("_ref_mode_single", "traj_z3_ws2_d16_distinct.npz")],
              3: [("_update_injected", "traj_z2_ws3_d16_distinct.npz"),
                  ("_update_hooks_single", "traj_z2_ws3_d16_distinct.npz")],

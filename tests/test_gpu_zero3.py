@@ -137,7 +137,7 @@ def _update_injected(rank, ws, name, dev, comm=None, dtype=torch.float32):
 
 
 def _update_hooks(rank, ws, name, dev, comm=None, backward_hooks=None, side_stream=True,
-                  gather_wave=None):
+                  gather_wave=None, stream_sync=None):
     """update=True through the real hooks: forward / backward all-gathers, gradients
     reduce-scattered from the post-accumulate-grad hooks during backward, fused Adam on the
     chunks.  Grads come from hipBLAS GEMMs, so the bound vs the CPU reference is 1e-4.  Backward
@@ -150,6 +150,8 @@ def _update_hooks(rank, ws, name, dev, comm=None, backward_hooks=None, side_stre
     kw = {} if comm is None else {"comm": comm}
     if gather_wave is not None:
         kw["gather_wave"] = gather_wave
+    if stream_sync is not None:
+        kw["stream_sync"] = stream_sync
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
                                  bucket_mb=2e-3, side_stream=side_stream,
                                  **kw)  # ~2 KB buckets: several launches in backward
@@ -183,6 +185,11 @@ def _update_hooks_module(rank, ws, name, dev, comm=None):
 def _update_hooks_single(rank, ws, name, dev, comm=None):
     """update mode with every collective on the compute stream (side_stream=False)."""
     _update_hooks(rank, ws, name, dev, comm=comm, side_stream=False)
+
+
+def _update_hooks_events(rank, ws, name, dev, comm=None):
+    """update mode with the side stream ordered by HIP events (the default is stream flags)."""
+    _update_hooks(rank, ws, name, dev, comm=comm, stream_sync="event")
 
 
 def _update_hooks_wave3(rank, ws, name, dev, comm=None):
@@ -237,7 +244,8 @@ Z3_CASES = [("_ref_mode", w, f"traj_z3_ws{w}_d16_distinct.npz") for w in (2, 4, 
     [("_update_injected", w, f"traj_z2_ws{w}_d16_distinct.npz") for w in (2, 3, 4, 8)] + \
     [("_update_hooks", w, f"traj_z2_ws{w}_d16_{m}.npz")
      for w, m in ((2, "distinct"), (3, "distinct"), (4, "distinct"), (8, "ref"), (8, "distinct"))] + \
-    [("_update_hooks_module", w, f"traj_z2_ws{w}_d16_distinct.npz") for w in (2, 4)]
+    [("_update_hooks_module", w, f"traj_z2_ws{w}_d16_distinct.npz") for w in (2, 4)] + \
+    [("_update_hooks_events", w, f"traj_z2_ws{w}_d16_distinct.npz") for w in (2, 3)]
 
 
 @pytest.mark.parametrize("ws", [2, 3, 4, 8])

@@ -10,7 +10,7 @@ step="$1"; shift
 fatal() { case $1 in 124|134|137|139) echo "[$step] rc=$1: stop"; exit 1;; esac; }
 case "$step" in
   tests)  # a subset of the -m gpu suite: tools/r05.sh tests <pytest node ids / files>
-    ZS_FAIL_LOG="$O/failures_tests.txt" timeout -k 10 900 python -u -m pytest "$@" -m gpu -q \
+    ZS_FAIL_LOG="$O/failures_tests.txt" timeout -k 10 900 python -u -m pytest "$@" -m gpu -v \
       --timeout 300 --timeout-method thread > "$O/tests.log" 2>&1; rc=$?
     tail -30 "$O/tests.log"; fatal $rc; echo "[tests] rc=$rc";;
   suite)  # the whole -m gpu suite as the driver runs it, then smoke()

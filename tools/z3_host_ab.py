@@ -55,6 +55,8 @@ def main():
     ap.add_argument("--extract-only", action="store_true",
                     help="write the baseline module under tools/.baselines/ and exit (no GPU)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--events", action="store_true",
+                    help="also time the current runtime with stream_sync='event'")
     ap.add_argument("--single", action="store_true",
                     help="also time the current runtime with side_stream=False")
     args = ap.parse_args()
@@ -109,6 +111,8 @@ def main():
         return step
 
     variants = {base: build(z3_old, 0), "current": build(z3_new, 0)}
+    if args.events:  # the current runtime ordered by HIP events instead of stream flags
+        variants["current_events"] = build(z3_new, 0, stream_sync="event")
     if args.single:  # the current runtime with its collectives on the compute stream
         variants["current_single_stream"] = build(z3_new, 0, side_stream=False)
     for st in variants.values():

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--wave", type=int, default=None, help="gather wave (default: the library's)")
     ap.add_argument("--bucket-mb", type=float, default=None, help="reduce-scatter bucket MB")
+    ap.add_argument("--stream-sync", default=None, choices=["flag", "event"],
+                    help="cross-stream ordering of the side stream (default: the library's)")
     ap.add_argument("--no-events", action="store_true",
                     help="DIAGNOSTIC: the ordered library calls and the consumer's stream wait "
                          "become no-ops (no HIP event record / wait at all): how much of the "
@@ -71,7 +73,13 @@ def main():
 
         comm._ordered = lambda name, dtype: (lambda after, ready, stream, done: None)
         _lib.lib.zs_stream_wait_event = lambda *a: 0
+        _lib.lib.zs_sync_wait = lambda *a: 0
+        from zero_amd.comm import Sync
+
+        Sync.record = Sync.wait = lambda self, h: None
     kw = {}
+    if args.stream_sync is not None:
+        kw["stream_sync"] = args.stream_sync
     if args.wave is not None:
         kw["gather_wave"] = args.wave
     if args.bucket_mb is not None:
@@ -127,6 +135,7 @@ def main():
     med = lambda k: sorted(r[k] for r in rows)[len(rows) // 2]  # noqa: E731
     summ = {"config": args.config, "simulated_ws": ws, "iters_per_block": args.iters,
             "no_events": args.no_events, "gather_wave": opt.runtime.wave,
+            "stream_sync": "flag" if opt.runtime.sync_kind == 1 else "event",
             "bucket_mb": args.bucket_mb,
             "autograd_thread_is_main": bool(bwd_tid and bwd_tid <= {main_tid}),
             "median": {k: med(k) for k in ("wall_ms", "cpu_ms", "main_thread_ms",
