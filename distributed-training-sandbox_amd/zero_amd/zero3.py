@@ -156,6 +156,8 @@ class _GatherRuntime:
         self._waited = {}             # done-event handle -> stream handle that waited on it
         self.stream = comm_stream(device) if side_stream else None
         self._side_h = self.stream.cuda_stream if side_stream else None
+        self._side_ids = ((self.stream.stream_id, self.stream.device_index, self.stream.device_type)
+                          if side_stream else None)
         # the current stream as a raw handle (torch.cuda.current_stream builds a Stream object per
         # call; the hot path only needs the handle for the library's ordered calls)
         self._dev_idx = device.index if device.index is not None else torch.cuda.current_device()
@@ -176,6 +178,8 @@ class _GatherRuntime:
         # its materialise has enqueued that wait (creating them per gather cost host time)
         self._syncs = {}
         self.iteration_callbacks = []  # called by end_iteration (hook bookkeeping resets)
+        self._inputs_dirty = True  # the shards may have changed since the last gather (step)
+        self._streams = {}  # raw handle -> torch stream object (record_stream)
 
     def _ready_sync(self, key, cur_h) -> Sync:
         """The sync the consumer stream ``cur_h`` records before ``key``'s gather (one per stream:
@@ -196,6 +200,27 @@ class _GatherRuntime:
 
     def _cur_h(self) -> int:
         return torch._C._cuda_getCurrentRawStream(self._dev_idx)
+
+    def _side_empty(self, n: int, dtype) -> torch.Tensor:
+        """torch.empty on the side stream (the caching allocator's stream of the block), with the
+        current stream set and restored by id — the stream context manager's host cost, per
+        gather, without its Python objects."""
+        prev = torch._C._cuda_getCurrentStream(self._dev_idx)
+        torch._C._cuda_setStream(*self._side_ids)
+        try:
+            return torch.empty(n, dtype=dtype, device=self.device)
+        finally:
+            torch._C._cuda_setStream(*prev)
+
+    def _stream_obj(self, h: int):
+        """A torch stream object for raw handle ``h`` (cached: record_stream needs one, and
+        building it per gather costs host time)."""
+        st = self._streams.get(h)
+        if st is None:
+            cur = torch.cuda.current_stream(self.device)
+            st = cur if cur.cuda_stream == h else torch.cuda.ExternalStream(h, device=self.device)
+            self._streams[h] = st
+        return st
 
     def side(self):
         """The stream collectives go to: the side stream, or (single-stream mode) the current."""
@@ -232,16 +257,16 @@ class _GatherRuntime:
             return
         side = self.side()
         if plan is not None and plan[-1] is not None and not timed:
-            # one allocation for the module's full tensors and ONE library call: ready sync on
-            # the compute stream (the shards may just have been updated), the side stream's wait,
-            # the RCCL group of all-gathers (zero-copy from the chunk-arena slots), the done sync
+            # one allocation for the module's full tensors and ONE library call: the ready sync
+            # (see _take_ready), the RCCL group of all-gathers (zero-copy from the chunk-arena
+            # slots), the done sync its consumers wait on.  Allocated on the side stream, which
+            # writes it; the consumer records its own use (materialize)
             send, count, offs, total, dt, es, views, recv, raw, ordered = plan
-            hold = torch.empty(total, dtype=managers[0].shard.dtype, device=self.device)
-            hold.record_stream(side)
+            hold = self._side_empty(total, managers[0].shard.dtype)
             np.add(offs, np.uint64(hold.data_ptr()), out=recv)
-            ordered(cur_h, ready_h, self._side_h, ev_h)
+            ordered(cur_h, self._take_ready(ready_h), self._side_h, ev_h)
             self.pending[key] = ([(m, hold.as_strided(shape, stride, off)) for m, (shape, stride, off)
-                                  in zip(managers, views)], done, hold, cur_h, ev_h)
+                                  in zip(managers, views)], done, hold, self._side_h, ev_h)
             self.n_gathers += 1
             return
         side_h = self._side_h if self.stream is not None else cur_h
@@ -335,6 +360,19 @@ class _GatherRuntime:
                     views, recv, raw, ordered)
         self._tables[key] = plan
         return plan
+
+    def _take_ready(self, ready_h: int) -> int:
+        """The ready sync a fast-path gather records on the consumer stream and waits for on the
+        side stream — only the first gather after the shards may have changed (construction, each
+        step(): ``end_iteration`` marks them): the gathers read the chunk-arena slots, which only
+        the compute stream's Adam writes, and the side stream runs its gathers in order, so one
+        wait per iteration orders all of them.  Their buffers are allocated on the side stream
+        (no reuse of a block the compute stream still reads: the caching allocator sees the
+        consumer's recorded use), so no other ordering is needed.  Returns 0 for "no ready"."""
+        if not self._inputs_dirty:
+            return 0
+        self._inputs_dirty = False
+        return ready_h
 
     def _fp8_plan(self, key, managers):
         """The cached tables of a module's fp8 gather: its matrices quantised by ONE launch into
@@ -446,7 +484,7 @@ class _GatherRuntime:
             ready_h = done_h = 0
             done_ev = None
         else:
-            ready_h = self._ready_sync(todo[0][0], cur_h).h
+            ready_h = self._take_ready(self._ready_sync(todo[0][0], cur_h).h)
             done_ev = self._done_sync(todo[-1][0])
             done_h = done_ev.h
             self._waited.pop(done_h, None)
@@ -454,13 +492,14 @@ class _GatherRuntime:
         side, side_h = self.stream, (cur_h if single else self._side_h)
         for j, ((k, ms), plan) in enumerate(zip(todo, plans)):
             send, count, offs, total, dt, es, views, recv, raw, ordered = plan
-            hold = torch.empty(total, dtype=ms[0].shard.dtype, device=self.device)
-            if not single:
-                hold.record_stream(side)
+            if single:
+                hold = torch.empty(total, dtype=ms[0].shard.dtype, device=self.device)
+            else:  # written by the side stream: allocated there (see _take_ready)
+                hold = self._side_empty(total, ms[0].shard.dtype)
             np.add(offs, np.uint64(hold.data_ptr()), out=recv)
             ordered(cur_h, ready_h if j == 0 else 0, side_h, done_h if j == last else 0)
             self.pending[k] = ([(m, hold.as_strided(shape, stride, off)) for m, (shape, stride, off)
-                                in zip(ms, views)], done_ev, hold, cur_h, done_h or None)
+                                in zip(ms, views)], done_ev, hold, side_h, done_h or None)
             self.n_gathers += 1
 
     def _ensure_wave(self, w, cur_h=None):
@@ -519,7 +558,7 @@ class _GatherRuntime:
         if hold is not None and alloc_h is not None and alloc_h != cur_h:
             # prefetched under another current stream (a user stream in forward, autograd's in
             # backward): the allocator must not reuse the block while THIS stream reads it
-            hold.record_stream(torch.cuda.current_stream(self.device))
+            hold.record_stream(self._stream_obj(cur_h))
         if hold is not None:  # one allocation (on this stream) behind all of the module's full
             for m, full in out:  # tensors, whose views already have the full shapes
                 m.full_data = full
@@ -533,6 +572,7 @@ class _GatherRuntime:
     def end_iteration(self):
         for fn in self.iteration_callbacks:
             fn()
+        self._inputs_dirty = True  # step() has updated the shards
         if self.sequence:
             self.recording = False
         self.pending.clear()
@@ -1187,7 +1227,10 @@ class _GradReducer:
             recv, count, dt, sp, raw, ordered = tab
             for j, (_, t) in enumerate(sends):
                 sp[j] = t.data_ptr()
-            ordered(cur_h, self._ready_sync(k, cur_h).h, self._cs_h, self._done_h[k])
+            # only the last bucket's done is waited on (step(), the shard grads): the side stream
+            # runs the buckets in order, so the others need no record
+            ordered(cur_h, self._ready_sync(k, cur_h).h, self._cs_h,
+                    self._done_h[k] if k == self.K - 1 else 0)
             for i, send in sends:
                 send.record_stream(cs)
                 opt.params[i].grad = None
