@@ -1593,15 +1593,17 @@ def main(argv=None):
 
     def default_step(o):
         """The drop-in's default hand-off: opt.zero_grad() sets every grad to None, then the
-        step gets fresh gradient tensors (two sets, alternating, so every step sees new
-        addresses, as backward's allocations may be)."""
-        if len(grad_sets) == 1:
+        step gets fresh gradient tensors (at N = 1 two sets, alternating, so every step sees new
+        addresses, as backward's allocations may be: Adam reads them in place; at N > 1 one set —
+        step() copies it into the arena whatever its address, and ranks sharing one GPU in a
+        rehearsal have no room for a second)."""
+        if len(grad_sets) == 1 and not multi:
             grad_sets.append([g.clone() for g in grads])
         k = [0]
 
         def st():
             o.zero_grad()
-            for p, g in zip(params, grad_sets[k[0] & 1]):
+            for p, g in zip(params, grad_sets[k[0] % len(grad_sets)]):
                 p.grad = g
             k[0] += 1
             o.step()
