@@ -878,8 +878,8 @@ def zero3_gather_check(opt, model, shapes, full_copies, dev, world, rank, red_de
     ms = [opt.param_managers[getattr(layer, f"p{k}")] for k in range(layer.n)]
     rt.launch(("exchange-check",), ms)
     out, ev, _hold, _, _ = rt.pending.pop(("exchange-check",))
-    if ev is not None:  # (single-stream mode: already in order on this stream)
-        torch.cuda.current_stream(dev).wait_event(ev)
+    if ev is not None:  # a comm.Sync (raw stream handles); single-stream mode: already in order
+        ev.wait(torch.cuda.current_stream(dev).cuda_stream)
     torch.cuda.synchronize()
     bits = lambda t: t.reshape(-1).view(torch.int16 if t.element_size() == 2 else torch.int32)  # noqa: E731
     bad = [i for (m, full), i in zip(out, idx) if not torch.equal(bits(full[:m.numel]),

@@ -335,31 +335,39 @@ struct zs_sync {
 };
 
 namespace {
-// Flag words come from per-device slabs (one hipMalloc per 4096 flags, 64 B apart: one cache line
-// each): engines create a few hundred syncs, not a few hundred tiny device allocations.
+// Flag words come from slabs of pinned, host-coherent memory (one hipHostMalloc per 4096 flags, 64 B
+// apart: one cache line each; engines create a few hundred syncs, not a few hundred tiny
+// allocations).  The GPU writes and polls them like device memory, and the host can read them: a
+// wait whose epoch has already been written is skipped on the host, as the HIP runtime skips a wait
+// on a completed event — the enqueue of a stream wait costs ~3-5 us of the caller
+// (profiles/r05_sync_cost.json), and a prefetched gather has usually finished when its consumer
+// asks for it whenever the host, not the GPU, is the bottleneck.  Zero-filled by the host before
+// any word is handed out (no device work a record could race with).
 constexpr int kFlagsPerSlab = 4096;
 constexpr size_t kFlagStride = 64;
 std::mutex g_flag_mu;
-std::map<int, std::vector<uint32_t*>> g_flag_free;
+std::vector<uint32_t*> g_flag_free;
 
-hipError_t flag_take(int device, uint32_t** out) {
+hipError_t flag_take(uint32_t** out) {
   std::lock_guard<std::mutex> lk(g_flag_mu);
-  auto& fl = g_flag_free[device];
-  if (fl.empty()) {
-    unsigned char* slab = nullptr;
-    hipError_t e = hipMalloc(reinterpret_cast<void**>(&slab), kFlagsPerSlab * kFlagStride);
+  if (g_flag_free.empty()) {
+    void* slab = nullptr;
+    hipError_t e = hipHostMalloc(&slab, kFlagsPerSlab * kFlagStride,
+                                 hipHostMallocCoherent | hipHostMallocPortable | hipHostMallocMapped);
     if (e != hipSuccess) return e;
-    // zeroed and COMPLETE before any word is handed out: a record on another stream must never
-    // be overtaken by the zero fill
-    e = hipMemsetAsync(slab, 0, kFlagsPerSlab * kFlagStride, nullptr);
-    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
-    if (e != hipSuccess) return e;
+    std::memset(slab, 0, kFlagsPerSlab * kFlagStride);
     for (int i = kFlagsPerSlab - 1; i >= 0; --i)
-      fl.push_back(reinterpret_cast<uint32_t*>(slab + size_t(i) * kFlagStride));
+      g_flag_free.push_back(
+          reinterpret_cast<uint32_t*>(static_cast<unsigned char*>(slab) + size_t(i) * kFlagStride));
   }
-  *out = fl.back();
-  fl.pop_back();
+  *out = g_flag_free.back();
+  g_flag_free.pop_back();
   return hipSuccess;
+}
+
+// the word has reached epoch `e` (epochs grow by one per record; compared modulo 2^32)
+bool flag_reached(const uint32_t* w, uint32_t e) {
+  return int32_t(__atomic_load_n(w, __ATOMIC_ACQUIRE) - e) >= 0;
 }
 }  // namespace
 
@@ -375,7 +383,7 @@ int zs_sync_create(int kind, zs_sync** out) {
     if (kind == ZS_SYNC_EVENT) {
       e = hipEventCreateWithFlags(&s->event, hipEventDisableTiming);
     } else {
-      e = flag_take(s->device, &s->flag);  // (zeroed with its slab: epoch 0)
+      e = flag_take(&s->flag);  // (zeroed with its slab: epoch 0)
     }
   }
   if (e != hipSuccess) {
@@ -413,12 +421,17 @@ int zs_sync_wait(zs_sync* s, uintptr_t stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (s->kind == ZS_SYNC_EVENT) {
     ZS_HIP(hipStreamWaitEvent(st, s->event, 0));
-  } else if (s->epoch > 0) {  // never recorded: nothing to wait for (as an unrecorded event)
+  } else if (s->epoch > 0 && !flag_reached(s->flag, s->epoch)) {
+    // (never recorded, or the latest record already executed: nothing to wait for)
     ZS_HIP(hipStreamWaitValue32(st, s->flag, s->epoch, hipStreamWaitValueGte, 0xFFFFFFFFu));
   }
   return ZS_OK;
 }
 
+// `stream` after everything enqueued so far on `after_stream`.  (Not skipped when after_stream is
+// idle: tried with a hipStreamQuery per call, ~0.2 us for the caller, the process CPU of the
+// simulated C5 iteration rose from 7.2 to 11.1 ms against 11.7 ms with events — other threads'
+// time, as a pending event wait costs — profiles/r05_z3_host_ab_query.json.)
 static int synced_prologue(uintptr_t after_stream, zs_sync* ready, uintptr_t stream) {
   if (ready) {
     int rc = zs_sync_record(ready, after_stream);

@@ -241,9 +241,10 @@ class RcclComm:
 
 class Sync:
     """A cross-stream ordering point (``zs_sync``, include/zero_amd.h): a HIP event
-    (``kind=_lib.ZS_SYNC_EVENT``) or a stream memory operation on a device flag word
+    (``kind=_lib.ZS_SYNC_EVENT``) or a stream memory operation on a flag word in pinned host memory
     (``_lib.ZS_SYNC_FLAG``: hipStreamWriteValue32 of an epoch on the producer stream,
-    hipStreamWaitValue32 >= it on the consumer).  A wait on a pending HIP event keeps one HIP
+    hipStreamWaitValue32 >= it on the consumer; a wait whose record has already executed is
+    skipped on the host).  A wait on a pending HIP event keeps one HIP
     runtime thread polling for as long as it is pending; a flag wait is resolved by the GPU and
     costs the host nothing (profiles/r05_event_poll_probe.jsonl).  ``record(stream_h)`` /
     ``wait(stream_h)`` take raw stream handles; ``h`` is the raw handle the synced group calls

@@ -386,14 +386,15 @@ int zs_reduce_scatter_group_ordered(zs_comm* comm, int64_t n, const uint64_t* se
 /* hipStreamWaitEvent(stream, event): the consumer side of the ordered groups. */
 int zs_stream_wait_event(uintptr_t stream, uint64_t event);
 /* Sync objects (ABI v12): a cross-stream ordering point that is either a HIP event
- * (ZS_SYNC_EVENT) or a stream memory operation on a device flag word (ZS_SYNC_FLAG:
- * hipStreamWriteValue32 of an epoch on the producer, hipStreamWaitValue32 >= it on the consumer).
- * zs_sync_record enqueues the producer side on `stream`; zs_sync_wait makes `stream` wait for the
- * latest record (hipStreamWaitEvent's semantics; a never-recorded sync waits for nothing).  A flag
- * sync must be recorded from one stream at a time.  The ZeRO-3 gathers and gradient buckets
- * (zero3.py:36-41, 131-147; their torch.cuda.synchronize() after each collective becomes this
- * ordering) use the synced group forms: record `ready` on after_stream, wait for it on `stream`,
- * the RCCL group, record `done` on `stream` (either sync may be NULL). */
+ * (ZS_SYNC_EVENT) or a stream memory operation on a flag word in pinned host-coherent memory
+ * (ZS_SYNC_FLAG: hipStreamWriteValue32 of an epoch on the producer, hipStreamWaitValue32 >= it on
+ * the consumer).  zs_sync_record enqueues the producer side on `stream`; zs_sync_wait makes
+ * `stream` wait for the latest record (hipStreamWaitEvent's semantics; a never-recorded sync, or
+ * one whose latest record has already executed — the host reads the flag word — enqueues
+ * nothing).  A flag sync must be recorded from one stream at a time.  The ZeRO-3 gathers and
+ * gradient buckets (zero3.py:36-41, 131-147; their torch.cuda.synchronize() after each collective
+ * becomes this ordering) use the synced group forms: record `ready` on after_stream and wait for
+ * it on `stream`, the RCCL group, record `done` on `stream` (either sync may be NULL). */
 typedef struct zs_sync zs_sync;
 enum zs_sync_kind { ZS_SYNC_EVENT = 0, ZS_SYNC_FLAG = 1 };
 int zs_sync_create(int kind, zs_sync** out);

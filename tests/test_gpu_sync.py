@@ -1,8 +1,9 @@
 """Sync objects (include/zero_amd.h zs_sync, ABI v12): the engines' cross-stream ordering as a HIP
 event or as a stream memory operation on a device flag word.  Both kinds must order
 a consumer stream after a producer stream exactly like hipStreamWaitEvent, including when the
-producer is far behind the host, and a flag created while the legacy null stream is busy must not
-be zeroed behind a record (its slab is zero-filled to completion before any word is handed out)."""
+producer is far behind the host (the flag wait is then enqueued) and when it has finished (the
+host sees the word and enqueues nothing), and a flag created while the legacy null stream is busy
+must order as any other (its slab is zeroed by the host before any word is handed out)."""
 import pytest
 import torch
 
@@ -61,3 +62,60 @@ def test_unrecorded_sync_waits_for_nothing(gpu):
     for kind in ("flag", "event"):
         StreamEvent(kind).wait(s)
     s.synchronize()
+
+
+@pytest.mark.parametrize("kind", ["flag", "event"])
+def test_wait_after_producer_finished(gpu, kind):
+    """The producer's record has executed before the wait is asked for: the flag wait is then
+    skipped on the host (the word already holds the epoch) and the consumer still sees the data."""
+    from zero_amd.comm import StreamEvent
+
+    prod, cons = torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)
+    src = torch.zeros(1 << 16, device=gpu)
+    dst = torch.full((1 << 16,), -1.0, device=gpu)
+    ev = StreamEvent(kind)
+    for it in range(1, 4):
+        with torch.cuda.stream(prod):
+            src.fill_(float(it))
+        ev.record(prod)
+        prod.synchronize()
+        ev.wait(cons)
+        with torch.cuda.stream(cons):
+            dst.copy_(src)
+        cons.synchronize()
+        assert bool((dst == float(it)).all()), (kind, it)
+
+
+@pytest.mark.parametrize("busy", [True, False])
+def test_synced_prologue_orders_after_stream(gpu, busy):
+    """zs_all_gather_group_synced with no collective (n = 0): `stream` runs after everything
+    enqueued on after_stream, busy or already idle, and `done` orders a third stream after
+    `stream`."""
+    from zero_amd import _lib
+    from zero_amd.comm import Sync
+
+    after, side, cons = (torch.cuda.Stream(gpu) for _ in range(3))
+    ready, done = Sync(_lib.ZS_SYNC_FLAG), Sync(_lib.ZS_SYNC_FLAG)
+    src = torch.zeros(1 << 16, device=gpu)
+    mid = torch.full((1 << 16,), -1.0, device=gpu)
+    dst = torch.full((1 << 16,), -1.0, device=gpu)
+    for it in range(1, 4):
+        with torch.cuda.stream(after):
+            if busy:
+                torch.cuda._sleep(SLEEP_CYCLES // 4)
+            src.fill_(float(it))
+        if not busy:
+            after.synchronize()
+        rc = _lib.lib.zs_all_gather_group_synced(None, 0, None, None, None, _lib.ZS_F32,
+                                                  after.cuda_stream, ready.h, side.cuda_stream,
+                                                  done.h)
+        assert rc == 0
+        with torch.cuda.stream(side):
+            mid.copy_(src)
+        done.record(side.cuda_stream)
+        done.wait(cons.cuda_stream)
+        with torch.cuda.stream(cons):
+            dst.copy_(mid)
+        cons.synchronize()
+        assert bool((dst == float(it)).all()), (busy, it)
+    torch.cuda.synchronize()

@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=None, help="reduce-scatter bucket MB")
     ap.add_argument("--stream-sync", default=None, choices=["flag", "event"],
                     help="cross-stream ordering of the side stream (default: the library's)")
+    ap.add_argument("--single", action="store_true",
+                    help="collectives on the compute stream (side_stream=False)")
     ap.add_argument("--no-events", action="store_true",
                     help="DIAGNOSTIC: the ordered library calls and the consumer's stream wait "
                          "become no-ops (no HIP event record / wait at all): how much of the "
@@ -84,6 +86,8 @@ def main():
         kw["gather_wave"] = args.wave
     if args.bucket_mb is not None:
         kw["bucket_mb"] = args.bucket_mb
+    if args.single:
+        kw["side_stream"] = False
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
                                  sync=False, comm=comm, **kw)
     zero3.register_zero3_hooks(model, opt.param_managers)
@@ -134,7 +138,7 @@ def main():
         print(json.dumps(rows[-1]), flush=True)
     med = lambda k: sorted(r[k] for r in rows)[len(rows) // 2]  # noqa: E731
     summ = {"config": args.config, "simulated_ws": ws, "iters_per_block": args.iters,
-            "no_events": args.no_events, "gather_wave": opt.runtime.wave,
+            "no_events": args.no_events, "side_stream": not args.single, "gather_wave": opt.runtime.wave,
             "stream_sync": "flag" if opt.runtime.sync_kind == 1 else "event",
             "bucket_mb": args.bucket_mb,
             "autograd_thread_is_main": bool(bwd_tid and bwd_tid <= {main_tid}),
