@@ -1721,6 +1721,7 @@ def main(argv=None):
     eng.timing_events = None
     comm_events, eng.comm_events = eng.comm_events, None
     copy_events, eng.copy_events = eng.copy_events, None
+    headline_inplace = int(getattr(eng, "inplace_reads", 0))  # (before the other leg's steps)
     el_t = torch.tensor([el], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
@@ -1883,7 +1884,7 @@ def main(argv=None):
             out["fp32_master"] = fp32_master
         out["grad_handoff"] = {"handoff": handoff_used, "what": HANDOFF_WHAT[handoff_used]}
         if handoff_used == "default":
-            out["grad_handoff"]["grads_read_in_place"] = int(getattr(eng, "inplace_reads", 0))
+            out["grad_handoff"]["grads_read_in_place"] = headline_inplace
             out["default_zero_grad_ms_per_step"] = ms
         if other_leg is not None:
             out[f"{other_leg['handoff']}_handoff_ms_per_step"] = other_leg["ms_per_step"]

@@ -50,6 +50,12 @@ def test_bench_fp32_master_line_beside_split_headline(gpu):
     # 28 vs 26 B per element over the same elements
     ratio = fm["alg_bytes_per_launch"] / out["roofline"]["alg_bytes_per_launch"]
     assert abs(ratio - 28 / 26) < 1e-3, ratio
+    # N=1 times the default hand-off (zero_grad() -> None, fresh grads): Adam read every one of
+    # C2's 12 gradient tensors in place; the views hand-off is timed beside it
+    gh = out["grad_handoff"]
+    assert gh["handoff"] == "default" and gh["grads_read_in_place"] == 12, gh
+    assert out["default_zero_grad_ms_per_step"] == out["ms_per_step"]
+    assert out["views_handoff_ms_per_step"] > 0
 
 
 def test_bench_harness_two_ranks_gloo_staged(gpu):

@@ -26,17 +26,17 @@ import sys
 from pathlib import Path
 
 # lane width of each kernel's global reads / writes (bytes per lane per access)
-READ_WIDTH = {"convert_kernel<true>": 16, "convert_kernel<false>": 8,
+READ_WIDTH = {"convert_kernel<true,": 16, "convert_kernel<false,": 8,
               "fp8_quantize_rows_wave_kernel<unsigned short,": 16,
               "fp8_quantize_rowset_kernel<unsigned short,": 16,
               "fp8_dequantize_gathered_kernel<unsigned short,": 8,
-              "scale_kernel<unsigned short>": 16, "scale_kernel<float>": 16,
+              "scale_kernel<unsigned short,": 16, "scale_kernel<float,": 16,
               "copy_segments_kernel<": 16}
-WRITE_WIDTH = {"convert_kernel<true>": 8, "convert_kernel<false>": 16,
+WRITE_WIDTH = {"convert_kernel<true,": 8, "convert_kernel<false,": 16,
                "fp8_quantize_rows_wave_kernel<unsigned short,": 8,
                "fp8_quantize_rowset_kernel<unsigned short,": 8,
                "fp8_dequantize_gathered_kernel<unsigned short,": 16,
-               "scale_kernel<unsigned short>": 16, "scale_kernel<float>": 16,
+               "scale_kernel<unsigned short,": 16, "scale_kernel<float,": 16,
                "copy_segments_kernel<": 16}
 
 

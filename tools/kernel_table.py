@@ -75,9 +75,9 @@ def main():
     dst, _ = probed_zeros(n, torch.bfloat16, dev)
     src.normal_()
     timed("convert_kernel<true> (fp32->bf16)", lambda: convert(src, dst, st), 6 * n,
-          f"C3 gradient, {n:,} elements (grad_comm='bf16')", "convert_kernel<true>")
+          f"C3 gradient, {n:,} elements (grad_comm='bf16')", "convert_kernel<true,")
     timed("convert_kernel<false> (bf16->fp32)", lambda: convert(dst, src, st), 6 * n,
-          f"C3 gradient, {n:,} elements", "convert_kernel<false>")
+          f"C3 gradient, {n:,} elements", "convert_kernel<false,")
     del src, dst
     torch.cuda.empty_cache()
 
@@ -149,7 +149,7 @@ def main():
                   lambda b=b, code=code: _lib.call("zs_scale", b.data_ptr(), b.numel(), code, 3.0,
                                                    stream_handle(st)),
                   2 * es * m, f"DDP bucket, {mib} MiB {dt}" + (" (MALL-resident)" if mib <= 256 else ""),
-                  f"scale_kernel<{'unsigned short' if es == 2 else 'float'}>")
+                  f"scale_kernel<{'unsigned short' if es == 2 else 'float'},")  # (either cache policy)
             del b
             torch.cuda.empty_cache()
 

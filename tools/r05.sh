@@ -39,6 +39,19 @@ case "$step" in
     done
     python3 tools/pmc_summary.py "$O/pmc_${tag}_FETCH_SIZE" "$O/pmc_${tag}_WRITE_SIZE" "adam_segments_kernel<unsigned short, false, false, true>" \
       "$O/${tag}_pmc.json" "$alg" "$cfg" "python3 bench.py $*" | tail -8; echo "[pmc $tag] done";;
+  ktable)  # the kernel roofline table: timed run, rocprof stats of it, FETCH / WRITE passes, summary
+    timeout -k 10 300 python3 tools/kernel_table.py --out "$O/kernels_table.json" > "$O/ktable.log" 2>&1; rc=$?
+    tail -3 "$O/ktable.log"; fatal $rc; [ $rc -eq 0 ] || exit 1
+    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_ktable" -o run -- \
+      python3 "$R/tools/kernel_table.py" --out "$O/kernels_table_rocprof.json" > "$O/ktable_rocprof.log" 2>&1); rc=$?
+    fatal $rc; [ $rc -eq 0 ] || { tail -5 "$O/ktable_rocprof.log"; exit 1; }
+    for c in FETCH_SIZE WRITE_SIZE; do
+      (cd /tmp && timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_ktable_$c" -o run -- \
+        python3 "$R/tools/kernel_table.py" --iters 2 --out "$O/kernels_table_$c.json" > "$O/pmc_ktable_$c.log" 2>&1); rc=$?
+      fatal $rc; [ $rc -eq 0 ] || { echo "[ktable $c] rc=$rc"; tail -5 "$O/pmc_ktable_$c.log"; exit 1; }
+    done
+    python3 tools/kernel_pmc.py "$O/kernels_table_FETCH_SIZE.json" "$O/pmc_ktable_FETCH_SIZE" \
+      "$O/pmc_ktable_WRITE_SIZE" "$O/kernels_pmc.json" "$O/kernels_table.json" | tail -12; echo "[ktable] done";;
   rehearsal8)  # the driver's default N = 8 line (C4 ZeRO-2, arena auto) on the ONE GPU through real
     # RCCL (--share-gpu: 8 ranks on one card, sockets between them), as plain `python bench.py --gpus 8`
     GPU_MAX_HW_QUEUES=2 timeout -k 10 840 python3 bench.py --share-gpu --no-cpu-baseline --watchdog-s 800 \
