@@ -37,6 +37,7 @@ on the same side stream, so one communicator sees one totally ordered sequence o
 from __future__ import annotations
 
 import contextlib
+import os
 import time
 import weakref
 
@@ -54,6 +55,13 @@ from .comm import STREAM_SYNC, RcclComm, Sync, comm_stream, sync_kind, zs_dtype
 from .engine import ALIGN_ELEMS, probed_zeros
 from .kernels import AdamSet, adam_hparams, stream_handle
 from .training_utils.utils import get
+
+try:  # the hooks' per-module install / release in C++ (csrc/zs_host_ext.cpp, built with the library)
+    from . import _hostext
+except ImportError:  # (an image whose torch ABI differs: the same steps per parameter in Python)
+    _hostext = None
+if os.environ.get("ZERO_AMD_HOSTEXT", "1") == "0":  # A/B switch (tools/z3_host_ab.py)
+    _hostext = None
 
 
 def _chunk_geom(d0: int, ws: int, rank: int):
@@ -120,6 +128,37 @@ def _add_post_accumulate_hook(param, fn):
     return _PostAccHandle(param, fn)
 
 
+class _Gathered:
+    """A module's gathered allocation (``hold``) with its managers: iterating gives the
+    (manager, full tensor) pairs the per-parameter paths hold, built only when asked;
+    ``_GatherRuntime.materialize`` installs them through the module's ViewPlan in one call."""
+
+    __slots__ = ("ms", "hold", "views", "vplan")
+
+    def __init__(self, ms, hold, views, vplan):
+        self.ms, self.hold, self.views, self.vplan = ms, hold, views, vplan
+
+    def __iter__(self):
+        if self.vplan is not None:
+            return iter(list(zip(self.ms, self.vplan.views(self.hold))))
+        return iter([(m, self.hold.as_strided(shape, stride, off))
+                     for m, (shape, stride, off) in zip(self.ms, self.views)])
+
+
+def _release_group(ms):
+    """Every manager of ``ms`` back to its shard (zero3.py:43-52): one ViewPlan call when the
+    module has one (update mode's chunk-arena managers), else per parameter."""
+    rt = ms[0].runtime if ms else None
+    ent = rt._vplans.get(id(ms)) if rt is not None else None
+    if ent is not None and ent[0] is ms and ent[1] is not None:
+        ent[1].release()
+        for m in ms:
+            m.full_data = None
+        return
+    for m in ms:
+        m.release()
+
+
 class _GatherRuntime:
     """Side-stream collectives of one ShardedOptimizer: module all-gathers prefetched one wave
     ahead (and, in update mode, the gradient reduce-scatters, on the same stream).
@@ -180,6 +219,10 @@ class _GatherRuntime:
         self.iteration_callbacks = []  # called by end_iteration (hook bookkeeping resets)
         self._inputs_dirty = True  # the shards may have changed since the last gather (step)
         self._streams = {}  # raw handle -> torch stream object (record_stream)
+        # id(managers list) -> (that list, its _hostext.ViewPlan): the module's parameters
+        # installed from its gathered allocation and released to their shards in one C++ call
+        self._vplans = {}
+        self.use_hostext = True  # (False: per-parameter install / release, for A/B)
 
     def _ready_sync(self, key, cur_h) -> Sync:
         """The sync the consumer stream ``cur_h`` records before ``key``'s gather (one per stream:
@@ -251,8 +294,8 @@ class _GatherRuntime:
             hold = torch.empty(total, dtype=managers[0].shard.dtype, device=self.device)
             np.add(offs, np.uint64(hold.data_ptr()), out=recv)
             ordered(cur_h, 0, cur_h, 0)
-            self.pending[key] = ([(m, hold.as_strided(shape, stride, off)) for m, (shape, stride, off)
-                                  in zip(managers, views)], None, hold, cur_h, None)
+            self.pending[key] = (_Gathered(managers, hold, views, self._vplan(managers, views)),
+                                 None, hold, cur_h, None)
             self.n_gathers += 1
             return
         side = self.side()
@@ -265,8 +308,8 @@ class _GatherRuntime:
             hold = self._side_empty(total, managers[0].shard.dtype)
             np.add(offs, np.uint64(hold.data_ptr()), out=recv)
             ordered(cur_h, self._take_ready(ready_h), self._side_h, ev_h)
-            self.pending[key] = ([(m, hold.as_strided(shape, stride, off)) for m, (shape, stride, off)
-                                  in zip(managers, views)], done, hold, self._side_h, ev_h)
+            self.pending[key] = (_Gathered(managers, hold, views, self._vplan(managers, views)),
+                                 done, hold, self._side_h, ev_h)
             self.n_gathers += 1
             return
         side_h = self._side_h if self.stream is not None else cur_h
@@ -299,9 +342,8 @@ class _GatherRuntime:
                 raw(side)
             else:
                 self.comm.all_gather_group(send, recv, count, dt, side)
-            # each manager's full tensor: one strided view of the allocation (no slice + view)
-            out = [(m, hold.as_strided(shape, stride, off)) for m, (shape, stride, off)
-                   in zip(managers, views)]
+            # each manager's full tensor: one strided view of the allocation, built on install
+            out = _Gathered(managers, hold, views, self._vplan(managers, views))
         else:
             with torch.cuda.stream(side):
                 # kernels (fp8 quantisation) before the RCCL group, dequantisation after: an RCCL
@@ -360,6 +402,24 @@ class _GatherRuntime:
                     views, recv, raw, ordered)
         self._tables[key] = plan
         return plan
+
+    def _vplan(self, managers, views):
+        """The module's ViewPlan (shared by its forward and backward keys: the same managers
+        list), or None — no extension, reference mode (release shrinks gradients: per parameter),
+        or parameters the extension cannot rewrite in place."""
+        ent = self._vplans.get(id(managers))
+        if ent is not None and ent[0] is managers:
+            return ent[1]
+        vp = None
+        if self.use_hostext and _hostext is not None and all(m.keep_full_grad for m in managers):
+            try:
+                vp = _hostext.ViewPlan([m.param for m in managers], [m.shard for m in managers],
+                                       [list(v[0]) for v in views], [list(v[1]) for v in views],
+                                       [int(v[2]) for v in views])
+            except RuntimeError:
+                vp = None
+        self._vplans[id(managers)] = (managers, vp)
+        return vp
 
     def _take_ready(self, ready_h: int) -> int:
         """The ready sync a fast-path gather records on the consumer stream and waits for on the
@@ -498,8 +558,8 @@ class _GatherRuntime:
                 hold = self._side_empty(total, ms[0].shard.dtype)
             np.add(offs, np.uint64(hold.data_ptr()), out=recv)
             ordered(cur_h, ready_h if j == 0 else 0, side_h, done_h if j == last else 0)
-            self.pending[k] = ([(m, hold.as_strided(shape, stride, off)) for m, (shape, stride, off)
-                                in zip(ms, views)], done_ev, hold, side_h, done_h or None)
+            self.pending[k] = (_Gathered(ms, hold, views, self._vplan(ms, views)), done_ev, hold,
+                               side_h, done_h or None)
             self.n_gathers += 1
 
     def _ensure_wave(self, w, cur_h=None):
@@ -560,7 +620,12 @@ class _GatherRuntime:
             # backward): the allocator must not reuse the block while THIS stream reads it
             hold.record_stream(self._stream_obj(cur_h))
         if hold is not None:  # one allocation (on this stream) behind all of the module's full
-            for m, full in out:  # tensors, whose views already have the full shapes
+            if type(out) is _Gathered and out.vplan is not None:  # tensors: one C++ call
+                out.vplan.install(hold)
+                for m in out.ms:
+                    m.full_data = hold
+                return
+            for m, full in out:  # (per parameter: a strided view each)
                 m.full_data = full
                 m.param.data = full
             return
@@ -808,6 +873,7 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
     for rt in runtimes:
         rt.key_managers = {}
         rt._tables = {}  # a key's managers may differ from an earlier registration
+        rt._vplans = {}
         rt._fp8_tables = {}
         rt.iteration_callbacks = []  # (an earlier registration's bookkeeping is replaced)
         for mod in model.modules():
@@ -837,8 +903,9 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
         def post_hook(module, *args):
             if phase == "fwd" and not reshard_after_forward:
                 return None  # kept for backward
-            for m in mod_managers.get(id(module)) or []:
-                m.release()
+            ms = mod_managers.get(id(module))
+            if ms:
+                _release_group(ms)
             return None
         return post_hook
 
@@ -900,8 +967,7 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
     def end_backward():
         queued[0] = False
         for ms in open_.values():
-            for mg in ms:
-                mg.release()
+            _release_group(ms)
         open_.clear()
         pending.clear()
 
@@ -952,8 +1018,7 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
             if mid in open_:
                 pending[mid] -= 1
                 if pending[mid] == 0:
-                    for mg in open_.pop(mid):
-                        mg.release()
+                    _release_group(open_.pop(mid))
 
     state.grad_ready = grad_ready
     forward_pre.state = state  # (the strong reference: module hook -> forward_pre -> state)

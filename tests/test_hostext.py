@@ -1,0 +1,111 @@
+"""The ZeRO-3 hooks' host helper (csrc/zs_host_ext.cpp, zero_amd/_hostext*.so): a module's
+parameters installed from its gathered allocation and put back to their shards in one call.  CPU
+tensors: the helper only rewrites tensor metadata, so its semantics are checked here against the
+per-parameter Python it replaces (``param.data = hold.as_strided(...)`` / ``param.data = shard``,
+zero3.py:36-52)."""
+import pytest
+import torch
+
+
+def _ext():
+    from zero_amd import zero3
+
+    assert zero3._hostext is not None, "zero_amd/_hostext*.so missing: run __graft_entry__.build()"
+    return zero3._hostext
+
+
+def _plan(ext, dtype=torch.float32):
+    shapes = [(64, 64), (128,), (32, 8)]
+    params = [torch.nn.Parameter(torch.randn(s[0] // 4, *s[1:]).to(dtype)) if len(s) > 1
+              else torch.nn.Parameter(torch.randn(s[0] // 4).to(dtype)) for s in shapes]
+    shards = [p.data for p in params]
+    views, off = [], 0
+    for s in shapes:
+        stride, acc = [], 1
+        for d in reversed(s):
+            stride.append(acc)
+            acc *= d
+        views.append((s, tuple(reversed(stride)), off))
+        off += -(-acc // 64) * 64
+    vp = ext.ViewPlan(params, shards, [list(v[0]) for v in views], [list(v[1]) for v in views],
+                      [v[2] for v in views])
+    return vp, params, shards, views, off
+
+
+def test_install_release_match_per_parameter_python():
+    ext = _ext()
+    vp, params, shards, views, total = _plan(ext)
+    assert vp.size == 3 and vp.extent <= total
+    hold = torch.randn(total)
+    vp.install(hold)
+    for p, (shape, stride, off) in zip(params, views):
+        want = hold.as_strided(shape, stride, off)
+        assert p.shape == want.shape and p.stride() == want.stride()
+        assert p.data_ptr() == want.data_ptr() and torch.equal(p.detach(), want)
+        assert p.requires_grad and p.is_leaf
+    v0 = [p._version for p in params]
+    # autograd through the installed parameters: full-shape gradients
+    x = torch.randn(5, 64)
+    ((x @ params[0]).sum() + params[1].sum() + params[2].sum()).backward()
+    assert params[0].grad.shape == (64, 64) and params[1].grad.shape == (128,)
+    vp.release()
+    for p, sh in zip(params, shards):
+        assert p.shape == sh.shape and p.data_ptr() == sh.data_ptr() and torch.equal(p.detach(), sh)
+    assert [p._version for p in params] == v0  # as `param.data = x`: no version bump
+    assert params[0].grad.shape == (64, 64)  # release leaves the gradient alone (update mode)
+    # the views alone, parameters untouched
+    vs = vp.views(hold)
+    assert all(torch.equal(v, hold.as_strided(*spec)) for v, spec in zip(vs, views))
+    assert params[0].shape == shards[0].shape
+
+
+def test_install_refuses_a_short_or_foreign_allocation():
+    ext = _ext()
+    vp, params, shards, _, total = _plan(ext)
+    with pytest.raises(RuntimeError, match="views reach"):
+        vp.install(torch.zeros(vp.extent - 1))
+    with pytest.raises(RuntimeError, match="dtype"):
+        vp.install(torch.zeros(total, dtype=torch.float64))
+    with pytest.raises(RuntimeError, match="1-D"):
+        vp.install(torch.zeros(2, total))
+    assert all(p.data_ptr() == s.data_ptr() for p, s in zip(params, shards))  # nothing touched
+    with pytest.raises(RuntimeError, match="differ in length"):
+        ext.ViewPlan(params, shards[:2], [[1]] * 3, [[1]] * 3, [0] * 3)
+
+
+def test_release_group_uses_the_module_plan_or_falls_back():
+    from zero_amd import zero3
+
+    class M:  # the manager surface _release_group touches
+        def __init__(self, p, rt):
+            self.param, self.shard, self.runtime, self.full_data = p, p.data, rt, None
+            self.released = 0
+
+        def release(self):
+            self.released += 1
+            self.param.data = self.shard
+            self.full_data = None
+
+    class RT:
+        pass
+
+    ext = _ext()
+    vp, params, shards, _, total = _plan(ext)
+    rt = RT()
+    ms = [M(p, rt) for p in params]
+    for m, s in zip(ms, shards):
+        m.shard = s
+    rt._vplans = {id(ms): (ms, vp)}
+    hold = torch.zeros(total)
+    vp.install(hold)
+    for m in ms:
+        m.full_data = hold
+    zero3._release_group(ms)
+    assert all(m.full_data is None and m.released == 0 for m in ms)
+    assert all(p.data_ptr() == s.data_ptr() for p, s in zip(params, shards))
+    other = list(ms)  # another list object: no plan of its own -> per parameter
+    zero3._release_group(other)
+    assert all(m.released == 1 for m in ms)
+    rt._vplans[id(other)] = (other, None)  # a module the extension could not take: per parameter
+    zero3._release_group(other)
+    assert all(m.released == 2 for m in ms)

@@ -59,6 +59,8 @@ def main():
                     help="also time the current runtime with stream_sync='event'")
     ap.add_argument("--single", action="store_true",
                     help="also time the current runtime with side_stream=False")
+    ap.add_argument("--no-hostext", action="store_true",
+                    help="also time the current runtime without the C++ install / release")
     args = ap.parse_args()
     path = baseline_file(args.baseline)
     if args.extract_only:
@@ -99,8 +101,11 @@ def main():
         real_get = mod.get
         mod.get = lambda what, dm=None: {"ws": ws, "rank": 0}.get(what) if what in ("ws", "rank") \
             else real_get(what, dm)
+        use_hostext = okw.pop("use_hostext", True)
         opt = mod.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
                                    sync=False, comm=bench._NoComm(ws), **okw)
+        if hasattr(opt, "runtime") and opt.runtime is not None:
+            opt.runtime.use_hostext = use_hostext
         mod.register_zero3_hooks(model, opt.param_managers)
         x = torch.zeros(1, device=dev, requires_grad=True)
 
@@ -115,6 +120,11 @@ def main():
         variants["current_events"] = build(z3_new, 0, stream_sync="event")
     if args.single:  # the current runtime with its collectives on the compute stream
         variants["current_single_stream"] = build(z3_new, 0, side_stream=False)
+    if args.no_hostext:  # the current runtime installing / releasing per parameter in Python
+        variants["current_no_hostext"] = build(z3_new, 0, use_hostext=False)
+        if args.single:
+            variants["current_single_stream_no_hostext"] = build(z3_new, 0, side_stream=False,
+                                                                 use_hostext=False)
     for st in variants.values():
         for _ in range(args.warmup):
             st()
