@@ -8,6 +8,7 @@ autograd's device thread) per block — the box's host speed drifts by 30 % over
 the interleaved comparison means anything.
 
 Usage: python tools/z3_host_ab.py [--config C5] [--ws 8] [--iters 20] [--blocks 6] [--baseline r02|r03]
+       [--events] [--single] [--no-hostext]   (extra variants of the current runtime)
 The baseline module is ``git show <rev>:distributed-training-sandbox_amd/zero_amd/zero3.py`` (r02:
 1653aab, r03: 3d19026 — the runtimes profiles/r03_z3_host_ab*.json and r04_z3_host_ab.json compare),
 written to tools/.baselines/ (git-ignored, so it travels to the GPU box, which has no git history):
