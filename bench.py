@@ -1903,6 +1903,14 @@ def main(argv=None):
         if lib_auto is not None:
             out["arena_calibration_library_auto"] = lib_auto
         out["host_enqueue_ms_per_step"] = host_ms  # rank 0's Python + launch time per step
+        if handoff_used == "default" and not multi:
+            out["host_enqueue_note"] = (
+                "default hand-off: the host enqueues ~200 steps ahead at ~0.4 ms each, then each "
+                "step waits for the GPU (a HIP runtime resource bounds the queued depth — "
+                "presumably the kernel-argument pool: each step's gradient-pointer patch carries "
+                "a 1.8 KB table in its arguments; the views leg never waits), so over a long run "
+                "this average tends to the GPU's step time; it is not host work "
+                "(profiles/r05_handoff_host.json)")
         if collectives is not None:
             out["collectives"] = collectives
         if copy_kernels is not None:

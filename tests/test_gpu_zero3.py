@@ -176,6 +176,12 @@ def _update_hooks(rank, ws, name, dev, comm=None, backward_hooks=None, side_stre
     assert ws == 1 or opt.runtime.n_prefetch_hits > 0  # (ws=1: no hooks, nothing to gather)
     if ws > 1:
         assert opt.communication_time >= 0.0
+    if ws > 1 and hasattr(opt.runtime.comm, "all_gather_group"):
+        # the table path (RCCL): every Linear installed and released through its module's C++
+        # ViewPlan (csrc/zs_host_ext.cpp), none left to the per-parameter fallback
+        plans = [vp for _, vp in opt.runtime._vplans.values()]
+        assert zero3._hostext is not None and plans and all(vp is not None for vp in plans)
+        assert sum(vp.size for vp in plans) == len(params)
 
 
 def _update_hooks_module(rank, ws, name, dev, comm=None):
