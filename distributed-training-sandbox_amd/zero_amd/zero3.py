@@ -623,7 +623,7 @@ class _GatherRuntime:
             if type(out) is _Gathered and out.vplan is not None:  # tensors: one C++ call
                 out.vplan.install(hold)
                 for m in out.ms:
-                    m.full_data = hold
+                    m._full = True  # (full_data: the parameter's data)
                 return
             for m, full in out:  # (per parameter: a strided view each)
                 m.full_data = full
@@ -691,6 +691,18 @@ class Zero3ParamManager:
         # vector kernels' 8-B fp8 accesses); vectors (biases, norms) and other matrices gather as
         # they are
         self.fp8 = gather_dtype == "fp8" and len(self.full_shape) >= 2 and self.row % 8 == 0
+
+    @property
+    def full_data(self):
+        """zero3.py:40: the gathered full tensor while the parameter is materialised, else None
+        (a module installed through its ViewPlan marks its managers ``True``: the full tensor is
+        then the parameter's data itself)."""
+        f = self._full
+        return self.param.data if f is True else f
+
+    @full_data.setter
+    def full_data(self, value):
+        self._full = value
 
     def gather_bytes(self) -> int:
         """Bytes this rank contributes to one all-gather of the parameter."""

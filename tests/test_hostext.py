@@ -109,3 +109,19 @@ def test_release_group_uses_the_module_plan_or_falls_back():
     rt._vplans[id(other)] = (other, None)  # a module the extension could not take: per parameter
     zero3._release_group(other)
     assert all(m.released == 2 for m in ms)
+
+
+def test_manager_full_data_is_the_parameters_full_tensor():
+    """zero3.py:40 exposes the gathered tensor as ``full_data``; a module installed through its
+    ViewPlan marks its managers, and full_data is then the parameter's (full) data."""
+    from zero_amd import zero3
+
+    p = torch.nn.Parameter(torch.randn(4, 8))
+    m = zero3.Zero3ParamManager(p, 0, 2)
+    assert m.full_data is None and m.full_shape == (8, 8)
+    full = torch.randn(8, 8)
+    p.data = full
+    m._full = True  # as _GatherRuntime.materialize after ViewPlan.install
+    assert m.full_data.shape == (8, 8) and m.full_data.data_ptr() == full.data_ptr()
+    m.full_data = None
+    assert m.full_data is None
