@@ -42,6 +42,11 @@ static int to_nccl(int dtype, ncclDataType_t* t) {
   }
 }
 
+int& zs::sync_host_flags() {  // (zs_tune "sync_host_flags"; zs_common.h)
+  static int mode = 1;
+  return mode;
+}
+
 extern "C" {
 
 int zs_comm_unique_id(void* out128) {
@@ -331,6 +336,7 @@ struct zs_sync {
   int device = 0;
   hipEvent_t event = nullptr;
   uint32_t* flag = nullptr;
+  bool host_word = false;  // the flag word is host-readable (pinned): satisfied waits are skipped
   uint32_t epoch = 0;
 };
 
@@ -343,25 +349,54 @@ namespace {
 // (profiles/r05_sync_cost.json), and a prefetched gather has usually finished when its consumer
 // asks for it whenever the host, not the GPU, is the bottleneck.  Zero-filled by the host before
 // any word is handed out (no device work a record could race with).
+// (Should pinned memory be refused, the words come from device slabs instead — zeroed to
+// completion on the device before any word is handed out, so no record can be overtaken by the
+// fill — and every wait is enqueued.)
 constexpr int kFlagsPerSlab = 4096;
 constexpr size_t kFlagStride = 64;
 std::mutex g_flag_mu;
-std::vector<uint32_t*> g_flag_free;
+std::vector<uint32_t*> g_flag_free;                      // host-coherent words
+std::map<int, std::vector<uint32_t*>> g_flag_dev_free;  // device words, per device (fallback)
+bool g_host_flags = true;
 
-hipError_t flag_take(uint32_t** out) {
+void carve(unsigned char* slab, std::vector<uint32_t*>& fl) {
+  for (int i = kFlagsPerSlab - 1; i >= 0; --i)
+    fl.push_back(reinterpret_cast<uint32_t*>(slab + size_t(i) * kFlagStride));
+}
+
+hipError_t flag_take(int device, uint32_t** out, bool* host_word) {
   std::lock_guard<std::mutex> lk(g_flag_mu);
-  if (g_flag_free.empty()) {
+  const bool host = g_host_flags && zs::sync_host_flags();
+  if (host && g_flag_free.empty()) {
     void* slab = nullptr;
-    hipError_t e = hipHostMalloc(&slab, kFlagsPerSlab * kFlagStride,
-                                 hipHostMallocCoherent | hipHostMallocPortable | hipHostMallocMapped);
-    if (e != hipSuccess) return e;
-    std::memset(slab, 0, kFlagsPerSlab * kFlagStride);
-    for (int i = kFlagsPerSlab - 1; i >= 0; --i)
-      g_flag_free.push_back(
-          reinterpret_cast<uint32_t*>(static_cast<unsigned char*>(slab) + size_t(i) * kFlagStride));
+    if (hipHostMalloc(&slab, kFlagsPerSlab * kFlagStride,
+                      hipHostMallocCoherent | hipHostMallocPortable | hipHostMallocMapped) ==
+        hipSuccess) {
+      std::memset(slab, 0, kFlagsPerSlab * kFlagStride);
+      carve(static_cast<unsigned char*>(slab), g_flag_free);
+    } else {
+      (void)hipGetLastError();
+      g_host_flags = false;
+    }
   }
-  *out = g_flag_free.back();
-  g_flag_free.pop_back();
+  if (host && g_host_flags) {
+    *out = g_flag_free.back();
+    g_flag_free.pop_back();
+    *host_word = true;
+    return hipSuccess;
+  }
+  auto& fl = g_flag_dev_free[device];
+  if (fl.empty()) {
+    unsigned char* slab = nullptr;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&slab), kFlagsPerSlab * kFlagStride);
+    if (e == hipSuccess) e = hipMemsetAsync(slab, 0, kFlagsPerSlab * kFlagStride, nullptr);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    if (e != hipSuccess) return e;
+    carve(slab, fl);
+  }
+  *out = fl.back();
+  fl.pop_back();
+  *host_word = false;
   return hipSuccess;
 }
 
@@ -383,7 +418,7 @@ int zs_sync_create(int kind, zs_sync** out) {
     if (kind == ZS_SYNC_EVENT) {
       e = hipEventCreateWithFlags(&s->event, hipEventDisableTiming);
     } else {
-      e = flag_take(&s->flag);  // (zeroed with its slab: epoch 0)
+      e = flag_take(s->device, &s->flag, &s->host_word);  // (zeroed with its slab: epoch 0)
     }
   }
   if (e != hipSuccess) {
@@ -421,7 +456,7 @@ int zs_sync_wait(zs_sync* s, uintptr_t stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (s->kind == ZS_SYNC_EVENT) {
     ZS_HIP(hipStreamWaitEvent(st, s->event, 0));
-  } else if (s->epoch > 0 && !flag_reached(s->flag, s->epoch)) {
+  } else if (s->epoch > 0 && !(s->host_word && flag_reached(s->flag, s->epoch))) {
     // (never recorded, or the latest record already executed: nothing to wait for)
     ZS_HIP(hipStreamWaitValue32(st, s->flag, s->epoch, hipStreamWaitValueGte, 0xFFFFFFFFu));
   }

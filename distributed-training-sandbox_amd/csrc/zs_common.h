@@ -11,6 +11,10 @@ namespace zs {
 
 void set_error(const char* fmt, ...);
 
+// zs_tune("sync_host_flags"): 1 (default) = new flag syncs take pinned host words, 0 = device words
+// (the fallback when pinned memory is refused; zs_comm.cpp)
+int& sync_host_flags();
+
 inline int fail(int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;

@@ -1770,6 +1770,9 @@ int zs_tune(const char* key, int64_t value, int64_t* previous) {
   } else if (std::strcmp(key, "adam_wg_per_cu") == 0) {
     slot = &adam_wg_per_cu();
     ok = value >= 0 && value <= 1024;
+  } else if (std::strcmp(key, "sync_host_flags") == 0) {
+    slot = &zs::sync_host_flags();
+    ok = value == 0 || value == 1;
   } else {
     return zs::fail(ZS_ERR_INVALID, "zs_tune: unknown key '%s'", key);
   }

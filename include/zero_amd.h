@@ -321,7 +321,9 @@ int zs_device_free(void* p);
  * non-temporal above 256 MiB; 0 default policy; 1 non-temporal), "convert_nt" (zs_convert's, the
  * same by source + destination bytes), "copy_nt" (zs_copyset_run's, by 2 x the set's bytes),
  * "adam_wg_per_cu" (0 = 128 workgroups per CU, the default grid of the fused Adam; k = at most k
- * per CU).  *previous (may be NULL) gets the
+ * per CU), "sync_host_flags" (1: flag syncs created from now on take words in pinned host
+ * memory, whose satisfied waits the host skips; 0: device words, every wait enqueued — the
+ * fallback the library takes by itself when pinned memory is refused).  *previous (may be NULL) gets the
  * old value;
  * ZS_ERR_INVALID for an unknown key or value. */
 int zs_tune(const char* key, int64_t value, int64_t* previous);

@@ -119,3 +119,34 @@ def test_synced_prologue_orders_after_stream(gpu, busy):
         cons.synchronize()
         assert bool((dst == float(it)).all()), (busy, it)
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("kind", ["flag", "event"])
+def test_device_flag_words_order_streams(gpu, kind):
+    """The fallback flag words in device memory (zs_tune("sync_host_flags", 0): every wait
+    enqueued, none skipped on the host) order streams as the pinned host words do."""
+    from zero_amd import _lib
+    from zero_amd.comm import StreamEvent
+
+    _lib.call("zs_tune", b"sync_host_flags", 0, None)
+    try:
+        evs = [StreamEvent(kind) for _ in range(3)]
+    finally:
+        _lib.call("zs_tune", b"sync_host_flags", 1, None)
+    prod, cons = torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)
+    src = torch.zeros(1 << 16, device=gpu)
+    dst = torch.full((1 << 16,), -1.0, device=gpu)
+    for it, ev in enumerate(evs, 1):
+        for behind in (True, False):
+            with torch.cuda.stream(prod):
+                if behind:
+                    torch.cuda._sleep(SLEEP_CYCLES // 4)
+                src.fill_(float(it))
+            ev.record(prod)
+            if not behind:
+                prod.synchronize()
+            ev.wait(cons)
+            with torch.cuda.stream(cons):
+                dst.copy_(src)
+            cons.synchronize()
+            assert bool((dst == float(it)).all()), (kind, it, behind)
