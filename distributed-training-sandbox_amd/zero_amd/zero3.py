@@ -691,6 +691,9 @@ class Zero3ParamManager:
         # vector kernels' 8-B fp8 accesses); vectors (biases, norms) and other matrices gather as
         # they are
         self.fp8 = gather_dtype == "fp8" and len(self.full_shape) >= 2 and self.row % 8 == 0
+        # this manager as a one-member module (materialize()): one list object for its lifetime,
+        # so the runtime's per-module caches (gather table, ViewPlan) key on it once
+        self._as_group = [self]
 
     @property
     def full_data(self):
@@ -780,7 +783,7 @@ class Zero3ParamManager:
         """zero3.py:36-41 for this one parameter."""
         rt = self._runtime()
         key = ("param", id(self))
-        rt.launch(key, [self])
+        rt.launch(key, self._as_group)
         out, done, hold, _, _ = rt.pending.pop(key)
         cur = torch.cuda.current_stream(self.shard.device)
         if done is not None:

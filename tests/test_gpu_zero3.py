@@ -121,12 +121,14 @@ def _update_injected(rank, ws, name, dev, comm=None, dtype=torch.float32):
             for i, p in enumerate(params):
                 want = _chunk(z[f"r{rank}_t{t}_p{i}"], ws, rank)
                 assert rel(p.detach().cpu().numpy(), want) <= 1e-6, (t, i)
-    for i, p in enumerate(params):
-        m = opt.param_managers[p]
-        m.materialize()
-        torch.cuda.synchronize()
-        assert rel(p.detach().cpu().numpy(), z[f"r{rank}_t9_p{i}"]) <= 1e-6
-        m.release()
+    for rep in range(2):  # (twice: the runtime's per-module caches must not grow per call)
+        for i, p in enumerate(params):
+            m = opt.param_managers[p]
+            m.materialize()
+            torch.cuda.synchronize()
+            assert rel(p.detach().cpu().numpy(), z[f"r{rank}_t9_p{i}"]) <= 1e-6
+            m.release()
+        assert len(opt.runtime._vplans) <= len(params) and len(opt.runtime._tables) <= len(params)
     # every rank's optimizer state is its chunk of the reference's (DP-Adam) state
     for i, p in enumerate(params):
         key = f"r{rank}_state_{i}_exp_avg"
