@@ -125,3 +125,20 @@ def test_manager_full_data_is_the_parameters_full_tensor():
     assert m.full_data.shape == (8, 8) and m.full_data.data_ptr() == full.data_ptr()
     m.full_data = None
     assert m.full_data is None
+
+
+def test_gathered_pairs_with_and_without_a_plan():
+    """_Gathered (a module's pending gather) yields the same (manager, full tensor) pairs through
+    its ViewPlan's views as through per-parameter strided views."""
+    from zero_amd import zero3
+
+    ext = _ext()
+    vp, params, shards, views, total = _plan(ext)
+    hold = torch.randn(total)
+    ms = [object() for _ in params]
+    a = list(zero3._Gathered(ms, hold, views, vp))
+    b = list(zero3._Gathered(ms, hold, views, None))
+    assert [m for m, _ in a] == ms == [m for m, _ in b]
+    for (_, x), (_, y), (shape, stride, off) in zip(a, b, views):
+        assert x.shape == y.shape == shape and x.stride() == y.stride() == stride
+        assert x.data_ptr() == y.data_ptr() == hold.data_ptr() + off * hold.element_size()
