@@ -17,12 +17,15 @@ Prints ONE JSON line on rank 0 (plus diagnostics on stderr).
 """
 from __future__ import annotations
 
-import argparse
-import json
-import os
-import sys
 import time
-from pathlib import Path
+
+_T0 = time.monotonic()  # process start: the watchdog's default budget counts from here
+
+import argparse  # noqa: E402
+import json  # noqa: E402
+import os  # noqa: E402
+import sys  # noqa: E402
+from pathlib import Path  # noqa: E402
 
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "distributed-training-sandbox_amd"))
@@ -310,22 +313,108 @@ def _phase(name: str) -> None:
     log(f"[bench] phase: {name}")
 
 
+# The driver kills a bench run after 600 s of its own clock (BENCH_r05.json run.timeout_s), and a
+# run killed from outside leaves nothing.  So the watchdog's default fires inside that limit,
+# counted from process start (a fresh box's first `import torch` can take a minute or two), and a
+# run that dies says where it was and what it had measured: every thread's Python stack on stderr
+# and, on rank 0, one JSON line with "value": null, the phase and the partial results.
+WATCHDOG_BUDGET_S = 540.0
+_PARTIAL = {}     # what this run has measured so far (dicts are shared: later updates show)
+_OUT_FD = [None]  # a duplicate of the original stdout (fd 1 may be pointed at stderr for a block)
+_EMITTED = [False]
+
+
+def watchdog_seconds(requested, now=None) -> float:
+    """The watchdog delay: ``requested`` (seconds; <= 0 disables it), or by default what is left
+    of ``WATCHDOG_BUDGET_S`` since process start (at least 30 s)."""
+    if requested is not None:
+        return float(requested)
+    elapsed = (time.monotonic() if now is None else now) - _T0
+    return max(30.0, WATCHDOG_BUDGET_S - elapsed)
+
+
+def partial_line(failure: str, error=None) -> dict:
+    """Rank 0's line for a run that did not finish: ``value`` null, the phase it died in, why, and
+    whatever it had already measured (communicator self-check, exchange checks, arena calibration
+    with its bus bandwidth, a timed headline if it got that far)."""
+    out = {"metric": METRIC, "value": None, "unit": "params/s",
+           "n_gpus": int(os.environ.get("WORLD_SIZE", "1")), "higher_is_better": True,
+           "failed_phase": _PHASE[0], "failure": failure}
+    if error is not None:
+        out["error"] = str(error)[-2000:]
+    out.update({k: v for k, v in _PARTIAL.items() if k not in out})
+    return out
+
+
+def _emit_partial(failure: str, error=None) -> None:
+    """Print ``partial_line`` once, on rank 0 (on the original stdout)."""
+    if _EMITTED[0] or int(os.environ.get("RANK", "0")) != 0:
+        return
+    _EMITTED[0] = True
+    try:
+        line = json.dumps(partial_line(failure, error), default=str) + "\n"
+    except Exception as e:  # noqa: BLE001 — never lose the line to one odd value
+        line = json.dumps({"metric": METRIC, "value": None, "failed_phase": _PHASE[0],
+                           "failure": failure, "error": f"partial results unserialisable: {e}"}) + "\n"
+    fd = _OUT_FD[0] if _OUT_FD[0] is not None else 1
+    try:
+        sys.stdout.flush()
+    except Exception:  # noqa: BLE001
+        pass
+    os.write(fd, line.encode())
+
+
+def _dump_stacks(why: str) -> None:
+    import faulthandler
+
+    log(f"[bench] {why}: phase '{_PHASE[0]}'; every thread's stack follows")
+    try:
+        faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+    except Exception as e:  # noqa: BLE001
+        log(f"[bench] (stack dump failed: {e})")
+
+
 def _start_watchdog(seconds: float) -> None:
-    """A daemon timer: if the run is still going after ``seconds``, say which phase it was in and
-    end the process (os._exit, no exec) so a collective that never completes fails loudly instead of
-    holding the job until an outer limit."""
+    """A daemon timer: if the run is still going after ``seconds``, dump every thread's stack and
+    the phase, print the partial line (rank 0) and end the process (os._exit(3), no exec), so a
+    collective that never completes fails loudly — with evidence — before an outer limit kills the
+    job silently."""
     import threading
 
     if seconds <= 0:
         return
 
     def fire():
-        log(f"[bench] WATCHDOG: still in phase '{_PHASE[0]}' after {seconds:.0f} s; exiting")
+        _dump_stacks(f"WATCHDOG after {seconds:.0f} s (rank {os.environ.get('RANK', '0')})")
+        _emit_partial(f"watchdog: still in phase '{_PHASE[0]}' after {seconds:.0f} s")
+        sys.stderr.flush()
         os._exit(3)
 
     t = threading.Timer(seconds, fire)
     t.daemon = True
     t.start()
+
+
+def _install_term_handler() -> None:
+    """Under a launcher, SIGTERM is how torch.distributed.run ends the other ranks once one has
+    failed.  The main thread may be blocked in a collective and would never run a Python signal
+    handler, so SIGTERM is blocked in every thread and taken by a thread of its own that dumps the
+    stacks, prints rank 0's partial line and exits 143."""
+    import signal
+    import threading
+
+    if not hasattr(signal, "pthread_sigmask"):
+        return
+    signal.pthread_sigmask(signal.SIG_BLOCK, {signal.SIGTERM})  # (threads started later inherit it)
+
+    def waiter():
+        signal.sigwait({signal.SIGTERM})
+        _dump_stacks("SIGTERM (the launcher ends this rank: another rank failed or a limit hit)")
+        _emit_partial("terminated by SIGTERM (another rank failed, or an outer limit)")
+        sys.stderr.flush()
+        os._exit(143)
+
+    threading.Thread(target=waiter, name="bench-sigterm", daemon=True).start()
 
 
 def _teardown(opt):
@@ -380,6 +469,7 @@ def _fail_comm(rank: int, detail) -> None:
     log(f"[bench] COMMUNICATOR FAILED on rank {rank}: {detail}")
     if _IN_PROCESS[0]:
         raise CommFailed(f"rank {rank}: {detail}")
+    _emit_partial(f"communicator failed on rank {rank}", detail)
     sys.stdout.flush()
     sys.stderr.flush()
     os._exit(5)
@@ -708,6 +798,7 @@ def _zero3_comm(args, world, rank, dev):
         kw["comm"] = C10dComm() if args.comm == "c10d" else _product_comm(rank)
         _phase("communicator self-check")
         chk = _checked_comm(kw, world, rank, dev)
+        _PARTIAL["rccl_selfcheck"] = chk
         return kw["comm"], chk
     return None, None
 
@@ -724,7 +815,8 @@ NORTH_STAR_BUS_FRAC = 0.60   # ... and reduce-scatter / all-gather >= 60 % of xG
 
 
 def expected_scaling(shapes, zero: int, arena: str, world: int, elem_bytes: int = 2,
-                     adam_bytes_per_elem: int = 26, bucket_mb: float | None = None) -> dict:
+                     adam_bytes_per_elem: int = 26, bucket_mb: float | None = None,
+                     layout: str = "reference") -> dict:
     """The step the planner predicts on ``world`` GPUs, before it is measured, for
     the slowest rank — no overlap credit, like ``step_roofline``:
 
@@ -737,6 +829,12 @@ def expected_scaling(shapes, zero: int, arena: str, world: int, elem_bytes: int 
     * ZeRO-3 (Layout Z, zero3.py:105-110) hooked iteration: HBM = the max-rank chunks x Adam bytes;
       bus = forward gather + backward gather + gradient reduce-scatter of every padded chunk,
       3 x sum_i S_i x N x es x (N-1)/N.
+
+    ``layout`` (ZeRO-1/2; VERDICT r5 #6, what the reference's ownership costs): "reference"
+    (Layout R, whole parameters by index — the drop-in's, bit-exact against the reference), "flat"
+    (Layout F, balanced contiguous 1/N slices of the concatenation: in the flat arena, the N > 1
+    line's ``layout_ablation`` leg) or "chunk" (Layout Z, zero3.py:107-108's dim-0 chunks: bucket
+    arena only, so + pack / unpack).
 
     ``ideal_ms`` = HBM / 8 TB/s + bus / the peer links (min(N-1, 7) x 153 GB/s);
     ``at_north_star_ms`` = HBM / (70 % of 8 TB/s) + bus / (60 % of the peer links): the step the
@@ -758,10 +856,12 @@ def expected_scaling(shapes, zero: int, arena: str, world: int, elem_bytes: int 
         hbm = bpe * own
         model = "ZeRO-3: forward + backward gathers and the reduce-scatter of every padded chunk"
     else:
+        if layout == "chunk" and arena != "buckets":
+            raise ValueError("Layout Z (chunk) runs in the bucket arena")
         win = 0
         if arena == "buckets" and ws > 1:
             win = max(64, int((bucket_mb or 256.0) * (1 << 20)) // (ws * es))
-        plan = Plan(numels, ws, 0, "reference", dim0=dim0, align_elems=64, window_elems=win)
+        plan = Plan(numels, ws, 0, layout, dim0=dim0, align_elems=64, window_elems=win)
         own = max(int(plan.pieces(r).length.sum()) for r in range(ws))
         hbm = bpe * own
         if ws == 1:
@@ -774,7 +874,7 @@ def expected_scaling(shapes, zero: int, arena: str, world: int, elem_bytes: int 
             for k in range(plan.num_buckets):
                 b = plan.bucket(k)
                 bus += 2 * (b.elems * es * (ws - 1) / ws if b.even else int(b.win_len.sum()) * es)
-        model = f"ZeRO-{zero} {arena} arena"
+        model = f"ZeRO-{zero} {arena} arena" + ("" if layout == "reference" else f", layout {layout}")
     links = peer_link_peak_gbs(ws) * 1e9
     hbm_ms = hbm / (HBM_PEAK_GBS * 1e9) * 1e3
     bus_ms = bus / links * 1e3
@@ -793,11 +893,29 @@ def _expected_block(shapes, zero, arena, world, es, bpe, bucket_mb, measured_ms)
     e = expected_scaling(shapes, zero, arena, world, es, bpe, bucket_mb)
     e["measured_ms"] = measured_ms
     e["measured_over_ideal"] = measured_ms / e["ideal_ms"] if e["ideal_ms"] else None
+    keys = ("ideal_ms", "ideal_overlapped_ms", "at_north_star_ms", "hbm_gb_per_rank",
+            "bus_gb_per_rank", "max_rank_adam_gb")
     e["curve"] = {str(n): {k: round(v, 3) for k, v in expected_scaling(
-        shapes, zero, arena, n, es, bpe, bucket_mb).items()
-        if k in ("ideal_ms", "ideal_overlapped_ms", "at_north_star_ms", "hbm_gb_per_rank",
-                 "bus_gb_per_rank")} for n in (1, 2, 4, 8)}
+        shapes, zero, arena, n, es, bpe, bucket_mb).items() if k in keys} for n in (1, 2, 4, 8)}
+    if zero in (1, 2):
+        e["layouts"] = layout_costs(shapes, zero, world, es, bpe, bucket_mb)
     return e
+
+
+def layout_costs(shapes, zero, world, es=2, bpe=26, bucket_mb=None) -> dict:
+    """What the reference's whole-parameter ownership (Layout R) costs at ``world`` GPUs against
+    the balanced layouts, predicted by the planner: the slowest rank's Adam bytes and the step's
+    ideal time for Layout R / flat arena (the drop-in), Layout F / flat arena (the N > 1 line's
+    ``layout_ablation`` leg) and Layout Z / bucket arena (zero3.py's chunks; + pack / unpack)."""
+    rows = {"reference_flat_arena": ("flat", "reference"), "balanced_F_flat_arena": ("flat", "flat"),
+            "chunk_Z_bucket_arena": ("buckets", "chunk")}
+    out = {}
+    for name, (arena, layout) in rows.items():
+        e = expected_scaling(shapes, zero, arena, world, es, bpe,
+                             bucket_mb if arena == "flat" else None, layout=layout)
+        out[name] = {k: round(e[k], 3) for k in ("max_rank_adam_gb", "hbm_gb_per_rank",
+                                                  "bus_gb_per_rank", "ideal_ms")}
+    return out
 
 
 def match_traffic(want: dict, alg_bytes_per_launch: float, traffic_json=None):
@@ -830,6 +948,7 @@ def _fail_check(what: str, rank: int, detail) -> None:
     log(f"[bench] EXCHANGE CHECK FAILED on rank {rank}: {what}: {detail}")
     if _IN_PROCESS[0]:
         raise ExchangeCheckFailed(f"rank {rank}: {what}: {detail}")
+    _emit_partial(f"exchange check failed on rank {rank}: {what}", detail)
     sys.stdout.flush()
     sys.stderr.flush()
     os._exit(4)
@@ -977,27 +1096,29 @@ def zero12_exchange_check(opt, step, params, shapes, dev, world, rank, red_dev, 
 
     eng = opt.engine
     pc = eng.pieces
-    own = [int(i) for i, n in zip(pc.param, pc.length) if n > 0]
-    so_of = {int(i): int(so) for i, so, n in zip(pc.param, pc.stream_off, pc.length) if n > 0}
+    # this rank's pieces (param, element range, stream offset): whole parameters under the
+    # reference's layout, slices of them under the balanced Layout F of the layout ablation
+    own = [(int(i), int(po), int(so), int(n)) for i, po, so, n
+           in zip(pc.param, pc.param_off, pc.stream_off, pc.length) if n > 0]
     cap = torch.zeros(max(eng.L, 1), dtype=eng.dtype, device=dev)
-    before = {i: params[i].detach().clone() for i in own}
+    before = {(i, po): params[i].detach().reshape(-1)[po:po + n].clone() for i, po, _, n in own}
     eng.capture_reduced = cap
     step()
     torch.cuda.synchronize()
     eng.capture_reduced = None
-    exact, absum = _regen_grads(shapes, world, dev, {i: slice(None) for i in own}, eng.dtype)
+    exact, absum = _regen_grads(shapes, world, dev, {i: slice(None) for i, *_ in own}, eng.dtype)
     bf16 = eng.dtype == torch.bfloat16
     tol = _bf16_sum_tolerance(world) if bf16 else world * 2.0 ** -22
     worst_sum, worst_ulp, bad = 0.0, 0, []
-    for i in own:
-        n = params[i].numel()
-        got = cap[so_of[i]:so_of[i] + n]
-        ratio = float(((got.float() - exact[i]).abs() / (tol * absum[i] + 1e-30)).max())
+    for i, po, so, n in own:
+        got = cap[so:so + n]
+        ex, ab = exact[i][po:po + n], absum[i][po:po + n]
+        ratio = float(((got.float() - ex).abs() / (tol * ab + 1e-30)).max())
         worst_sum = max(worst_sum, ratio)
         if ratio > 1.0:
             bad.append(("reduced grad", i, ratio))
-        want = _adam_step1_restated(before[i].reshape(-1), got, world)
-        p = params[i].detach().reshape(-1)
+        want = _adam_step1_restated(before[(i, po)], got, world)
+        p = params[i].detach().reshape(-1)[po:po + n]
         if bf16:
             d = (_bits(p).int() - _bits(want.to(torch.bfloat16)).int()).abs().max()
             worst_ulp = max(worst_ulp, int(d))
@@ -1018,7 +1139,8 @@ def zero12_exchange_check(opt, step, params, shapes, dev, world, rank, red_dev, 
     diverged = sorted(set(int(k) // 2 for k in np.nonzero((lo != hi).cpu().numpy())[0]))
     ok = torch.tensor([0.0 if (bad or diverged) else 1.0], device=red_dev)
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-    res = {"arena": getattr(eng, "arena_kind", "buckets"), "owned_tensors": len(own),
+    res = {"arena": getattr(eng, "arena_kind", "buckets"), "owned_tensors": len({i for i, *_ in own}),
+           "owned_pieces": len(own),
            "reduce_max_err_over_bound": worst_sum,
            "reduce_bound": (f"|sum - exact fp32 sum| <= {world} * 2^-8 * sum_r |g_r| (bf16 ring: one "
                             "rounding per hop)") if bf16 else f"{world} * 2^-22 * sum_r |g_r|",
@@ -1445,6 +1567,9 @@ def main(argv=None):
                          "(two alternating sets), as backward leaves them after the drop-in's "
                          "default zero_grad() (zero2.py:138-139); auto: default at N=1, views "
                          "at N>1 (where the hooks land backward's grads into the views)")
+    ap.add_argument("--no-layout-ablation", action="store_true",
+                    help="N>1 ZeRO-2: skip timing the balanced Layout F beside the reference "
+                         "layout's headline (after everything else)")
     ap.add_argument("--no-default-leg", action="store_true",
                     help="skip timing the other hand-off beside the headline's")
     ap.add_argument("--simulate-ws", type=int, default=0,
@@ -1462,9 +1587,12 @@ def main(argv=None):
     ap.add_argument("--traffic-json", default=None,
                     help="PMC HBM-bytes summary for the roofline 'traffic' field (default: the "
                          "profiles/*_pmc.json whose config matches this run)")
-    ap.add_argument("--watchdog-s", type=float, default=1200.0,
-                    help="end the process (exit 3) with a diagnostic if the run has not finished "
-                         "after this many seconds (a collective that never completes)")
+    ap.add_argument("--watchdog-s", type=float, default=None,
+                    help="end the process (exit 3) with every thread's stack and rank 0's partial "
+                         "JSON line if the run has not finished after this many seconds (a "
+                         "collective that never completes); default: what is left of "
+                         f"{WATCHDOG_BUDGET_S:.0f} s since process start, inside the driver's 600 s; "
+                         "0 disables it")
     args = ap.parse_args(argv)
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
@@ -1487,7 +1615,35 @@ def main(argv=None):
         args.warmup = 2 if args.train else 5
     if args.dtype is None:
         args.dtype = "fp32" if (args.zero == 3 and args.config in ("C2", "C3")) else "bf16"
-    _start_watchdog(args.watchdog_s)
+    if not _IN_PROCESS[0]:
+        _OUT_FD[0] = os.dup(1)
+        if env_world is not None and int(env_world) > 1:
+            _install_term_handler()
+        _start_watchdog(watchdog_seconds(args.watchdog_s))
+    _PARTIAL.clear()
+    _EMITTED[0] = False
+    _PARTIAL["config"] = {"workload": args.config, "zero": args.zero, "arena_requested": args.arena,
+                          "parallelism": f"dp{int(env_world or 1)}",
+                          "train": args.train, "dtype": args.dtype}
+    try:
+        return _main(args)
+    except SystemExit:
+        raise
+    except BaseException as e:  # noqa: BLE001 — reported (partial line) and fatal
+        import traceback
+
+        log(f"[bench] FAILED in phase '{_PHASE[0]}': {type(e).__name__}: {e}")
+        traceback.print_exc(file=sys.stderr)
+        if _IN_PROCESS[0]:
+            raise
+        _emit_partial(f"{type(e).__name__} in phase '{_PHASE[0]}'", f"{type(e).__name__}: {e}")
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(7)
+
+
+def _main(args):
+    """main() after the arguments: the run itself (rank 0's JSON object, None on other ranks)."""
 
     import numpy as np
     import torch
@@ -1576,6 +1732,7 @@ def main(argv=None):
         _phase("communicator self-check")
         selfcheck = _checked_comm(kw, world, rank, dev)
         comm_used = selfcheck.pop("comm_used", comm_used)
+        _PARTIAL["rccl_selfcheck"] = selfcheck
     red_dev = dev if use_nccl else "cpu"
     multi = world > 1 or args.simulate_ws > 1
     arenas = ["flat", "buckets"] if (args.arena == "auto" and multi) else \
@@ -1651,6 +1808,8 @@ def main(argv=None):
         return float(t.item()) / n * 1e3
 
     exchange_check, arena_ab, arena_cal = {}, {}, {}
+    _PARTIAL.update(exchange_check_all_arenas=exchange_check, arena_calibration=arena_cal,
+                    arena_calibration_ms_per_step=arena_ab)
     opt = step = None
     for arena in arenas:
         if opt is not None:
@@ -1698,6 +1857,7 @@ def main(argv=None):
         _phase("library arena=auto calibration")
         lib_auto = calibrate_arena(opt)
         lib_auto["agrees_with_full_step"] = lib_auto["chosen"] == arena_used
+        _PARTIAL["arena_calibration_library_auto"] = lib_auto
 
     _phase("warmup")
     for _ in range(args.warmup):
@@ -1727,6 +1887,8 @@ def main(argv=None):
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     el = float(el_t.item())
     ms = el / args.steps * 1e3
+    _PARTIAL["timed_before_failure"] = {"ms_per_step": ms, "value": total / (ms / 1e3),
+                                        "steps": args.steps, "arena": getattr(eng, "arena_kind", None)}
 
     # Adam roofline: algorithmic bytes / kernel time, per launch, from HIP events on the launch stream
     adam_ms = sum(a.elapsed_time(b) for a, b, _ in eng_events)
@@ -1738,6 +1900,10 @@ def main(argv=None):
     if world > 1:  # report the slowest rank's Adam
         dist.all_reduce(stats, op=dist.ReduceOp.MIN)
     achieved = float(stats[0])
+    hb = torch.tensor([adam_bytes / args.steps], dtype=torch.float64, device=red_dev)
+    if world > 1:
+        dist.all_reduce(hb, op=dist.ReduceOp.MAX)
+    headline_adam_gb = float(hb.item()) / 1e9  # the slowest rank's Adam bytes per step
     want = {"workload": args.config, "zero": args.zero, "param_dtype": args.dtype,
             "layout": args.layout, "n_gpus": world}
     if args.dtype == "bf16":
@@ -1819,6 +1985,52 @@ def main(argv=None):
             _phase("bucket-size sweep")
             sweep_buf = eng.arena if getattr(eng, "arena", None) is not None else eng.R
             collectives["sweep"] = comm_sweep(opt._comm, sweep_buf, world, red_dev)
+
+    layout_ablation = None
+    if (world > 1 and args.zero == 2 and args.layout == "reference" and args.simulate_ws <= 1
+            and not args.no_layout_ablation):
+        # what the reference's whole-parameter ownership costs: the same step with
+        # the balanced Layout F in the flat arena — its own exchange check, then timed — after
+        # everything of the headline's (its memory is freed first)
+        _phase("layout ablation (balanced Layout F, flat arena)")
+        eng = None
+        _teardown_engine(opt)
+        opt = None
+        o_f = mod.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), layout="flat",
+                                   bucket_mb=args.bucket_mb, sync=False, master=args.master,
+                                   arena="flat", **kw)
+        st_f = views_step(o_f)
+        chk_f = zero12_exchange_check(o_f, st_f, params, shapes, dev, world, rank, red_dev,
+                                      fatal=False)
+        layout_ablation = {"layout": "flat (Layout F: balanced contiguous 1/N slices)",
+                           "arena": "flat", "exchange_check": chk_f}
+        if chk_f["all_ranks_ok"]:
+            for _ in range(args.warmup):
+                st_f()
+            o_f.engine.timing_events = []
+            n_f = min(args.steps, 50)
+            ms_f = timed(st_f, n_f)
+            ev_f, o_f.engine.timing_events = o_f.engine.timing_events, None
+            a_ms = sum(a.elapsed_time(b) for a, b, _ in ev_f)
+            a_b = sum(nb for *_, nb in ev_f)
+            t = torch.tensor([a_b / n_f, a_b / (a_ms / 1e3) / 1e9 if a_ms > 0 else 0.0],
+                             dtype=torch.float64, device=red_dev)
+            mx, mn = t.clone(), t.clone()
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            dist.all_reduce(mn, op=dist.ReduceOp.MIN)
+            layout_ablation.update(
+                ms_per_step=ms_f, steps=n_f, vs_headline=ms_f / ms,
+                max_rank_adam_gb_per_step=float(mx[0]) / 1e9,
+                headline_max_rank_adam_gb_per_step=headline_adam_gb,
+                min_rank_adam_achieved_gbs=float(mn[1]),
+                rounds=o_f.engine.K)
+        layout_ablation["expected"] = layout_costs(shapes, args.zero, world,
+                                                   es=2 if args.dtype == "bf16" else 4,
+                                                   bpe=26 if (args.dtype == "bf16"
+                                                              and args.master == "split") else 28,
+                                                   bucket_mb=bucket_mb)
+        _PARTIAL["layout_ablation"] = layout_ablation
+        opt = o_f  # (torn down at the end like the headline's)
 
     if rank == 0 and args.simulate_ws > 1:
         print(json.dumps({"diagnostic": f"simulate-ws {args.simulate_ws}: rank-0 compute of the "
@@ -1902,6 +2114,8 @@ def main(argv=None):
             out["arena_calibration"] = arena_cal
         if lib_auto is not None:
             out["arena_calibration_library_auto"] = lib_auto
+        if layout_ablation is not None:
+            out["layout_ablation"] = layout_ablation
         out["host_enqueue_ms_per_step"] = host_ms  # rank 0's Python + launch time per step
         if handoff_used == "default" and not multi:
             out["host_enqueue_note"] = (

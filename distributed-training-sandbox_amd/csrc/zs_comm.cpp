@@ -325,19 +325,24 @@ int zs_stream_wait_event(uintptr_t stream, uint64_t event) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Sync objects (ABI v12): the cross-stream ordering of the ZeRO-3 gathers as either a HIP event or
-// a stream memory operation on a flag word (hipStreamWriteValue32 after the producer's work,
-// hipStreamWaitValue32 >= the recorded epoch before the consumer's).  A record bumps the object's
-// epoch on the host and enqueues its write; a wait enqueues a wait for the epoch of the latest
-// record, the semantics of hipStreamWaitEvent.  A flag object must be recorded from one stream at a
-// time (its epochs then reach the word in order).
+// Sync objects (ABI v12; 64-bit words since v13): the cross-stream ordering of the engines as either
+// a HIP event or a stream memory operation on a flag word (hipStreamWriteValue64 after the
+// producer's work, hipStreamWaitValue64 >= the recorded epoch before the consumer's).  A record
+// bumps the object's epoch on the host and enqueues its write; a wait enqueues a wait for the epoch
+// of the latest record, the semantics of hipStreamWaitEvent.  Epochs are 64-bit and only grow: at
+// one record per microsecond a word wraps after 584,000 years, so the unsigned >= of the GPU wait
+// and the host's skip test agree for the life of any process (v12's 32-bit epoch wrapped after
+// 2^32 records, where the GPU's unsigned compare and the host's modulo compare disagree).
+// A record from a different stream than the previous one first makes its stream wait for the
+// previous epoch, so the words reach the flag in epoch order whichever streams record.
 struct zs_sync {
   int kind = ZS_SYNC_EVENT;
   int device = 0;
   hipEvent_t event = nullptr;
-  uint32_t* flag = nullptr;
+  uint64_t* flag = nullptr;
   bool host_word = false;  // the flag word is host-readable (pinned): satisfied waits are skipped
-  uint32_t epoch = 0;
+  uint64_t epoch = 0;
+  hipStream_t last_stream = nullptr;  // the stream of the latest record (flag kind)
 };
 
 namespace {
@@ -355,16 +360,16 @@ namespace {
 constexpr int kFlagsPerSlab = 4096;
 constexpr size_t kFlagStride = 64;
 std::mutex g_flag_mu;
-std::vector<uint32_t*> g_flag_free;                      // host-coherent words
-std::map<int, std::vector<uint32_t*>> g_flag_dev_free;  // device words, per device (fallback)
+std::vector<uint64_t*> g_flag_free;                      // host-coherent words
+std::map<int, std::vector<uint64_t*>> g_flag_dev_free;  // device words, per device (fallback)
 bool g_host_flags = true;
 
-void carve(unsigned char* slab, std::vector<uint32_t*>& fl) {
+void carve(unsigned char* slab, std::vector<uint64_t*>& fl) {
   for (int i = kFlagsPerSlab - 1; i >= 0; --i)
-    fl.push_back(reinterpret_cast<uint32_t*>(slab + size_t(i) * kFlagStride));
+    fl.push_back(reinterpret_cast<uint64_t*>(slab + size_t(i) * kFlagStride));
 }
 
-hipError_t flag_take(int device, uint32_t** out, bool* host_word) {
+hipError_t flag_take(int device, uint64_t** out, bool* host_word) {
   std::lock_guard<std::mutex> lk(g_flag_mu);
   const bool host = g_host_flags && zs::sync_host_flags();
   if (host && g_flag_free.empty()) {
@@ -400,9 +405,13 @@ hipError_t flag_take(int device, uint32_t** out, bool* host_word) {
   return hipSuccess;
 }
 
-// the word has reached epoch `e` (epochs grow by one per record; compared modulo 2^32)
-bool flag_reached(const uint32_t* w, uint32_t e) {
-  return int32_t(__atomic_load_n(w, __ATOMIC_ACQUIRE) - e) >= 0;
+// the word has reached epoch `e` (epochs only grow; 64-bit, so they never wrap)
+bool flag_reached(const uint64_t* w, uint64_t e) { return __atomic_load_n(w, __ATOMIC_ACQUIRE) >= e; }
+
+// `st` waits for the word to reach `e` unless the host already sees it there
+hipError_t flag_wait(const zs_sync* s, hipStream_t st, uint64_t e) {
+  if (e == 0 || (s->host_word && flag_reached(s->flag, e))) return hipSuccess;
+  return hipStreamWaitValue64(st, s->flag, e, hipStreamWaitValueGte, ~uint64_t(0));
 }
 }  // namespace
 
@@ -445,8 +454,12 @@ int zs_sync_record(zs_sync* s, uintptr_t stream) {
   if (s->kind == ZS_SYNC_EVENT) {
     ZS_HIP(hipEventRecord(s->event, st));
   } else {
-    ZS_HIP(hipStreamWriteValue32(st, s->flag, s->epoch + 1, 0));
+    // another stream than the last record's: order this write after that one's, or the word
+    // could go back from epoch + 1 to epoch when the two streams run in the other order
+    if (s->epoch > 0 && st != s->last_stream) ZS_HIP(flag_wait(s, st, s->epoch));
+    ZS_HIP(hipStreamWriteValue64(st, s->flag, s->epoch + 1, 0));
     ++s->epoch;
+    s->last_stream = st;
   }
   return ZS_OK;
 }
@@ -456,9 +469,41 @@ int zs_sync_wait(zs_sync* s, uintptr_t stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (s->kind == ZS_SYNC_EVENT) {
     ZS_HIP(hipStreamWaitEvent(st, s->event, 0));
-  } else if (s->epoch > 0 && !(s->host_word && flag_reached(s->flag, s->epoch))) {
-    // (never recorded, or the latest record already executed: nothing to wait for)
-    ZS_HIP(hipStreamWaitValue32(st, s->flag, s->epoch, hipStreamWaitValueGte, 0xFFFFFFFFu));
+  } else {
+    // (epoch 0: never recorded, nothing to wait for; a record that already executed: skipped)
+    ZS_HIP(flag_wait(s, st, s->epoch));
+  }
+  return ZS_OK;
+}
+
+int zs_sync_set_epoch(zs_sync* s, uint64_t epoch) {
+  ZS_REQUIRE(s != nullptr, "zs_sync_set_epoch: NULL sync");
+  ZS_REQUIRE(s->kind == ZS_SYNC_FLAG, "zs_sync_set_epoch: not a flag sync");
+  ZS_REQUIRE(epoch >= s->epoch, "zs_sync_set_epoch: epochs only grow (%llu < %llu)",
+             (unsigned long long)epoch, (unsigned long long)s->epoch);
+  // every record enqueued so far has executed (the caller's contract); then the word and the
+  // host epoch move together
+  if (s->host_word) {
+    ZS_REQUIRE(flag_reached(s->flag, s->epoch), "zs_sync_set_epoch: a record is still pending");
+    __atomic_store_n(s->flag, epoch, __ATOMIC_RELEASE);
+  } else {
+    ZS_HIP(hipMemcpy(s->flag, &epoch, sizeof(epoch), hipMemcpyHostToDevice));
+  }
+  s->epoch = epoch;
+  return ZS_OK;
+}
+
+int zs_sync_query(zs_sync* s, uint64_t* epoch, uint64_t* word) {
+  ZS_REQUIRE(s != nullptr, "zs_sync_query: NULL sync");
+  if (epoch) *epoch = s->kind == ZS_SYNC_FLAG ? s->epoch : 0;
+  if (word) {
+    *word = 0;
+    if (s->kind == ZS_SYNC_FLAG) {
+      if (s->host_word)
+        *word = __atomic_load_n(s->flag, __ATOMIC_ACQUIRE);
+      else
+        ZS_HIP(hipMemcpy(word, s->flag, sizeof(*word), hipMemcpyDeviceToHost));
+    }
   }
   return ZS_OK;
 }

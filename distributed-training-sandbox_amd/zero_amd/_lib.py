@@ -21,7 +21,7 @@ ZS_F32, ZS_BF16, ZS_U8, ZS_BF16_SPLIT = 0, 1, 2, 3
 ZS_LAYOUT_R, ZS_LAYOUT_Z, ZS_LAYOUT_F = 0, 1, 2
 ZS_BUCKETS_RAGGED, ZS_BUCKETS_PADDED = 0, 1
 ZS_SYNC_EVENT, ZS_SYNC_FLAG = 0, 1
-ABI_VERSION = 12
+ABI_VERSION = 13
 ZS_UNIQUE_ID_BYTES = 128
 
 # Every symbol include/zero_amd.h declares (tests check the library exports all of them).
@@ -39,7 +39,7 @@ EXPORTED = (
     "zs_comm_unique_id", "zs_comm_init", "zs_comm_destroy", "zs_reduce_scatter", "zs_all_gather",
     "zs_all_reduce", "zs_reduce", "zs_broadcast", "zs_reduce_group", "zs_broadcast_group", "zs_all_gather_group", "zs_reduce_scatter_group",
     "zs_all_gather_group_ordered", "zs_reduce_scatter_group_ordered", "zs_stream_wait_event",
-    "zs_sync_create", "zs_sync_destroy", "zs_sync_record", "zs_sync_wait",
+    "zs_sync_create", "zs_sync_destroy", "zs_sync_record", "zs_sync_wait", "zs_sync_set_epoch", "zs_sync_query",
     "zs_all_gather_group_synced", "zs_reduce_scatter_group_synced",
     "zs_group_start", "zs_group_end", "zs_rccl_version",
     "zs_device_alloc", "zs_device_free", "zs_tune",
@@ -147,6 +147,8 @@ _SIGS = {
     "zs_sync_destroy": ([_P], ctypes.c_int),
     "zs_sync_record": ([_P, _U], ctypes.c_int),
     "zs_sync_wait": ([_P, _U], ctypes.c_int),
+    "zs_sync_set_epoch": ([_P, ctypes.c_uint64], ctypes.c_int),
+    "zs_sync_query": ([_P, _PU64, _PU64], ctypes.c_int),
     "zs_all_gather_group_synced": ([_P, _I64, _PU64, _PU64, _PI64, ctypes.c_int, _U, _P, _U, _P],
                                    ctypes.c_int),
     "zs_reduce_scatter_group_synced": ([_P, _I64, _PU64, _PU64, _PI64, ctypes.c_int, _U, _P, _U, _P],

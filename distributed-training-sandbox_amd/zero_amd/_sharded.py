@@ -121,7 +121,10 @@ class ShardedOptimizerBase:
             self._overlap_hooks = self.engine.register_marks()
 
     def _flat(self) -> bool:
-        return self._arena == "flat" and self._layout == "reference"
+        """The flat parameter arena: the reference layout (the drop-in), or the balanced Layout F
+        ablation for ZeRO-2 (the ZeRO-1 carry is per whole parameter: bucket arena there)."""
+        return self._arena == "flat" and (self._layout == "reference" or
+                                          (self._layout == "flat" and not self._carry))
 
     def _shard_optimizer_params(self):
         """zero1.py:71-74: drop non-owned params from the inner optimizer's groups."""
@@ -143,7 +146,8 @@ class ShardedOptimizerBase:
 
             self.engine = FlatEngine(self.params, self._group_of, self.world_size, self.rank,
                                      carry=carry, comm=comm, bucket_bytes=self._bucket_bytes,
-                                     master=self._master, grad_comm=self._grad_comm)
+                                     master=self._master, grad_comm=self._grad_comm,
+                                     layout=self._layout)
         else:
             self.engine = ShardEngine(self.params, self._group_of, self.world_size, self.rank,
                                       layout=self._layout, carry=carry, comm=comm,
@@ -201,9 +205,11 @@ class ShardedOptimizerBase:
             # step releases is not kept alive by the check)
             if g is None or (seen[i] is not None and seen[i]() is g):
                 continue
-            if g.dtype != p.dtype or g.shape != p.shape or not g.is_contiguous():
-                raise ValueError("zero_amd: grads must be contiguous and match their param's "
-                                 "dtype and shape")
+            # (the flat arena copies a strided / expanded gradient into its slot through torch,
+            # as torch's Adam would read it; the bucket arena packs raw runs: dense only)
+            if g.dtype != p.dtype or g.shape != p.shape or not (g.is_contiguous() or self._flat()):
+                raise ValueError("zero_amd: grads must match their param's dtype and shape (and "
+                                 "be contiguous outside the flat arena)")
             seen[i] = weakref.ref(g)
         with torch.no_grad():
             self.engine.step(grads, self._hparams_of)

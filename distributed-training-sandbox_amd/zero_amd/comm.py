@@ -242,13 +242,14 @@ class RcclComm:
 class Sync:
     """A cross-stream ordering point (``zs_sync``, include/zero_amd.h): a HIP event
     (``kind=_lib.ZS_SYNC_EVENT``) or a stream memory operation on a flag word in pinned host memory
-    (``_lib.ZS_SYNC_FLAG``: hipStreamWriteValue32 of an epoch on the producer stream,
-    hipStreamWaitValue32 >= it on the consumer; a wait whose record has already executed is
-    skipped on the host).  A wait on a pending HIP event keeps one HIP
+    (``_lib.ZS_SYNC_FLAG``: hipStreamWriteValue64 of a 64-bit epoch on the producer stream,
+    hipStreamWaitValue64 >= it on the consumer; a wait whose record has already executed is
+    skipped on the host; epochs never wrap).  A wait on a pending HIP event keeps one HIP
     runtime thread polling for as long as it is pending; a flag wait is resolved by the GPU and
     costs the host nothing (profiles/r05_event_poll_probe.jsonl).  ``record(stream_h)`` /
     ``wait(stream_h)`` take raw stream handles; ``h`` is the raw handle the synced group calls
-    take.  A flag sync is recorded from one stream at a time (its epochs reach the word in order)."""
+    take.  A flag record from another stream than the previous record's is ordered after it (ABI
+    v13), so the word's epochs only grow whichever streams record."""
 
     __slots__ = ("h", "kind")
 
@@ -266,6 +267,16 @@ class Sync:
         rc = _lib.lib.zs_sync_wait(self.h, stream_h)
         if rc:
             _lib.check(rc, "zs_sync_wait")
+
+    def set_epoch(self, epoch: int) -> None:
+        """Test hook: move a flag sync's epoch and word forward (every record must have executed)."""
+        _lib.call("zs_sync_set_epoch", self.h, int(epoch))
+
+    def query(self) -> tuple[int, int]:
+        """(latest recorded epoch, current word) of a flag sync; (0, 0) for an event."""
+        e, w = ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.call("zs_sync_query", self.h, ctypes.byref(e), ctypes.byref(w))
+        return int(e.value), int(w.value)
 
     def __del__(self):
         h = getattr(self, "h", 0)
@@ -295,7 +306,7 @@ class StreamEvent:
     """The ordering surface of a non-timing ``torch.cuda.Event`` — ``record(stream=None)``,
     ``wait(stream=None)``, so ``torch.cuda.Stream.wait_event(ev)`` takes it — over a ``Sync`` of
     the process default kind (``STREAM_SYNC``): the engines' cross-stream ordering without a HIP
-    runtime thread polling.  Recorded from one stream at a time (see ``Sync``)."""
+    runtime thread polling.  Any stream may record (see ``Sync``)."""
 
     __slots__ = ("sync",)
 

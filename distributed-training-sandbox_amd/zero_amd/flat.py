@@ -66,28 +66,47 @@ class _Round:
 
 
 class FlatEngine(ShardEngine):
+    """``layout``: "reference" (Layout R, the reference's whole-parameter ownership, zero1.py:55-62
+    — the drop-in's) or "flat" (Layout F, the ablation: balanced contiguous 1/ws slices of the
+    aligned concatenation, so a parameter may straddle two owners; ZeRO-2 only, no overlap).
+    Either way rank r's stream is one contiguous region of P (Layout F: P is the aligned
+    concatenation itself, rank r's slice at r·S), so the rounds, the Adam rows and the grouped
+    reduce / broadcast are the same code."""
+
     def __init__(self, params, group_of, ws: int, rank: int, *, carry=False, comm=None,
                  bucket_bytes: int = 256 << 20, master: str = "split", placement_tries: int = 8,
-                 grad_comm: str | None = None):
-        # the base class gives the reference layout's streams, the optimizer state and the Adam
-        # launch machinery; its bucket plan (one bucket) is unused
-        super().__init__(params, group_of, ws, rank, layout="reference", carry=carry, comm=comm,
+                 grad_comm: str | None = None, layout: str = "reference"):
+        if layout not in ("reference", "flat"):
+            raise ValueError(f"the flat arena takes layout 'reference' or 'flat' (got {layout!r})")
+        if layout == "flat" and carry:
+            raise ValueError("layout='flat' in the flat arena is ZeRO-2 only (the ZeRO-1 carry is "
+                             "per whole parameter)")
+        # the base class gives the layout's streams, the optimizer state and the Adam launch
+        # machinery; its bucket plan (one bucket) is unused
+        super().__init__(params, group_of, ws, rank, layout=layout, carry=carry, comm=comm,
                          bucket_bytes=1 << 62, buckets="ragged", placement_tries=placement_tries,
                          master=master)
         self.arena_kind = "flat"
+        self.layout = layout
         plan, es, dev, dt = self.plan, self.es, self.device, self.dtype
         n = len(self.params)
         self.Ls = np.array([plan.stream_len(r) for r in range(ws)], np.int64)
         self.base = np.concatenate([[0], np.cumsum(self.Ls)[:-1]]).astype(np.int64)
         self.slot = np.zeros(n, np.int64)
         self.numel = np.array([p.numel() for p in self.params], np.int64)
-        owner = np.zeros(n, np.int64)
+        owner = np.zeros(n, np.int64)  # (Layout F: the rank holding the parameter's first element)
         for r in range(ws):
             pc = plan.pieces(r)
-            self.slot[pc.param] = self.base[r] + pc.stream_off
-            owner[pc.param] = r
+            first = pc.param_off == 0  # Layout R: every piece is a whole parameter
+            self.slot[pc.param[first]] = self.base[r] + pc.stream_off[first]
+            owner[pc.param[first]] = r
+        if layout == "flat":  # every parameter one contiguous run of P (its pieces abut)
+            for r in range(ws):
+                pc = plan.pieces(r)
+                assert np.array_equal(self.base[r] + pc.stream_off, self.slot[pc.param] + pc.param_off)
         self.owner = owner
-        self.owned = owner == rank
+        self.owned = np.zeros(n, bool)  # this rank updates (part of) the parameter
+        self.owned[self.pieces.param[self.pieces.length > 0]] = True
         total = int(max(self.Ls.sum(), ALIGN_ELEMS))
         self.P, self.arena_placement = _zeros_placed(total, dt, dev, placement_tries)
         with torch.no_grad():
@@ -226,7 +245,7 @@ class FlatEngine(ShardEngine):
         if g is self._views[i]:
             return True
         return (g.data_ptr() == self.G.data_ptr() + int(self.slot[i]) * self.es
-                and g.shape == self.params[i].shape)
+                and g.shape == self.params[i].shape and g.is_contiguous())
 
     def install_views(self):
         for i, p in enumerate(self.params):
@@ -430,6 +449,8 @@ class FlatEngine(ShardEngine):
         and broadcasts in rounds as without overlap: no unpack, the parameters are the arena."""
         from .overlap import plan_grad_buckets
 
+        if self.layout != "reference":
+            raise ValueError("backward overlap needs the reference (owner-by-index) layout")
         groups, keys, *_ = plan_grad_buckets(self.numel.tolist(), self.owner.tolist(),
                                              int(bucket_bytes), self.ces, align=ALIGN_ELEMS)
         n = len(self.params)
@@ -703,14 +724,16 @@ class FlatEngine(ShardEngine):
     def _bind_inplace(self, grads, has, view, stream) -> np.ndarray:
         """ws == 1: the gradient address Adam reads per parameter (0 = none): an arena view's slot,
         a fresh tensor itself (zero2.py:120 reads p.grad where backward left it) — or, for a
-        gradient the vector kernel cannot read in place (misaligned), its G slot after a copy,
-        p.grad then becoming the slot's view."""
+        gradient the vector kernel cannot read in place (misaligned, or not one dense run of the
+        parameter's dtype: a transposed or expanded tensor a caller assigned), its G slot after a
+        copy, p.grad then becoming the slot's view."""
         n = len(self.params)
         gptr = np.zeros(n, np.uint64)
         align = 8 if self.dtype == torch.bfloat16 else 16
         fresh = np.nonzero(has & ~view)[0]
         ptrs = np.fromiter((_ptr(grads[i]) for i in fresh), np.uint64, len(fresh))
-        ok = (ptrs % np.uint64(align)) == 0
+        dense = np.fromiter((_dense(grads[i], self.params[i]) for i in fresh), bool, len(fresh))
+        ok = ((ptrs % np.uint64(align)) == 0) & dense
         gptr[fresh[ok]] = ptrs[ok]
         odd = fresh[~ok]
         if len(odd):
@@ -749,6 +772,12 @@ class FlatEngine(ShardEngine):
         if self.ws == 1:
             return 0.0
         return max(0.0, self.ev_c0.elapsed_time(self.ev_c1) / 1e3)
+
+
+def _dense(g: torch.Tensor, p: torch.Tensor) -> bool:
+    """``g`` is one contiguous run of ``p.numel()`` elements of ``p``'s dtype (Adam reads it as
+    such); a stride-0 expand or a transpose is not."""
+    return g.dtype == p.dtype and g.numel() == p.numel() and g.is_contiguous()
 
 
 class _nullgroup:

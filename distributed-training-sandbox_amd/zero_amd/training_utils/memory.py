@@ -8,9 +8,13 @@ physical: the distinct storages behind those tensors.  The two differ for the dr
 are views of one flat chunk arena, so the physical column shows what is really resident.
 "Total allocated" / "Max allocated" are torch's allocator figures, as the reference prints them.
 The placed buffers of 1 GiB or more (optimizer state, parameter / gradient arenas:
-``engine.probed_zeros``) are device allocations of their own outside torch's cache; they get a
-line of their own — held now and the device's high-water mark, the placement probe's candidates
-included — rather than being added to torch's peak (the two peaks need not coincide in time).
+``engine.probed_zeros``) are device allocations of their own outside torch's cache, so torch's two
+figures alone under-report the drop-in's residency against the reference's (whose whole state
+lives in torch's allocator).  When anything is placed, two more lines follow: the placed bytes
+(held now, and the device's high-water mark with the placement probe's candidates), and the
+combined figures comparable to the reference's — "Total incl. placed" (torch's allocated + placed,
+both now) and "Max incl. placed", an upper bound: the sum of the two peaks, which need not
+coincide in time.
 """
 from __future__ import annotations
 
@@ -65,7 +69,20 @@ class MemoryReport:
         if self.placed_peak_mb:
             out.append(f"  Placed outside torch's allocator: {self.placed_mb:.2f} MB "
                        f"(peak {self.placed_peak_mb:.2f} MB incl. placement-probe candidates)")
+            out.append(f"  Total incl. placed: {self.total_mb:.2f} MB "
+                       f"(max <= {self.max_total_mb:.2f} MB, the sum of the two peaks)")
         return out + ["-" * 40]
+
+    @property
+    def total_mb(self) -> float:
+        """torch's allocated + the placed buffers: the residency the reference's "Total
+        allocated" counts (its state is all in torch's allocator)."""
+        return self.allocated_mb + self.placed_mb
+
+    @property
+    def max_total_mb(self) -> float:
+        """An upper bound of the combined peak (the two peaks need not coincide)."""
+        return self.max_allocated_mb + self.placed_peak_mb
 
 
 def memory_report(model, optimizer, device) -> MemoryReport:

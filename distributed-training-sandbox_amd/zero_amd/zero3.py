@@ -226,7 +226,7 @@ class _GatherRuntime:
 
     def _ready_sync(self, key, cur_h) -> Sync:
         """The sync the consumer stream ``cur_h`` records before ``key``'s gather (one per stream:
-        a flag is recorded from one stream at a time)."""
+        a flag record from another stream would first wait for the previous stream's record)."""
         k = ("ready", key, cur_h)
         sy = self._syncs.get(k)
         if sy is None:
@@ -634,6 +634,14 @@ class _GatherRuntime:
             full.record_stream(cur)
             m._install_full(full)
 
+    def mark_inputs_changed(self):
+        """The shards changed outside step()'s Adam (a checkpoint load, a caller's
+        ``p.data.copy_``): the next gather waits for the compute stream again (see _take_ready),
+        and gathers prefetched before the change — they read the old shards — are dropped, so
+        their modules gather again on demand."""
+        self._inputs_dirty = True
+        self.pending.clear()
+
     def end_iteration(self):
         for fn in self.iteration_callbacks:
             fn()
@@ -886,6 +894,7 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
               if p in param_managers and id(p) not in covered]
         mod_managers[id(mod)] = ms
     for rt in runtimes:
+        rt.mark_inputs_changed()  # (a new registration: nothing gathered before it is reused)
         rt.key_managers = {}
         rt._tables = {}  # a key's managers may differ from an earlier registration
         rt._vplans = {}
@@ -1703,6 +1712,14 @@ class ShardedOptimizer:
     def zero_grad(self, set_to_none: bool = True):
         self.optimizer.zero_grad(set_to_none=set_to_none)
 
+    def mark_params_changed(self):
+        """Tell the gathers that this rank's shards (``p.data`` between gathers) were written
+        outside ``step()``: the side-stream all-gathers read the shards and are ordered after the
+        compute stream only at the first gather after a step, so an in-place edit between two
+        steps (e.g. step → eval forward → ``p.data.copy_(...)`` → train forward) must be followed
+        by this call before the next forward.  ``load_state_dict`` calls it."""
+        self.runtime.mark_inputs_changed()
+
     # checkpointing (zero_amd/checkpoint.py) -------------------------------------------------------
     def _ckpt_header(self):
         return ckpt.header(3, self.world_size, self.rank, self.local_param_indices, update=self.update)
@@ -1728,8 +1745,12 @@ class ShardedOptimizer:
     def load_state_dict(self, state_dict):
         """Restore this rank's ``state_dict()``: hyper-parameters through torch's loader, the
         chunk state copied into the flat buffers.  The parameters themselves (this rank's chunks)
-        are restored by the caller, e.g. ``p.data.copy_(saved_chunk)``."""
+        are restored by the caller, e.g. ``p.data.copy_(saved_chunk)``, on the compute stream
+        before the next forward.  Loading marks the shards changed (``mark_params_changed``), so
+        the next gather is ordered after that copy; a caller that edits the shards at any other
+        time between two steps (after an eval forward, say) calls ``mark_params_changed()``."""
         ckpt.check_header(state_dict, self._ckpt_header())
+        self.mark_params_changed()
         torch.cuda.synchronize(self._arena.device)
         ckpt.load_param_groups(self.optimizer, state_dict)
         self.original_param_groups = self.optimizer.param_groups

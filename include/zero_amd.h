@@ -29,7 +29,7 @@ extern "C" {
  * the *_ex entry points), so a caller built against an older header links and then passes the
  * wrong arguments.  The Python binding (zero_amd/_lib.py) and tests/c/abi_host.c refuse a
  * mismatch. */
-#define ZS_ABI_VERSION 12
+#define ZS_ABI_VERSION 13
 
 enum zs_status {
   ZS_OK = 0,
@@ -387,13 +387,14 @@ int zs_reduce_scatter_group_ordered(zs_comm* comm, int64_t n, const uint64_t* se
                                     uint64_t done_event);
 /* hipStreamWaitEvent(stream, event): the consumer side of the ordered groups. */
 int zs_stream_wait_event(uintptr_t stream, uint64_t event);
-/* Sync objects (ABI v12): a cross-stream ordering point that is either a HIP event
- * (ZS_SYNC_EVENT) or a stream memory operation on a flag word in pinned host-coherent memory
- * (ZS_SYNC_FLAG: hipStreamWriteValue32 of an epoch on the producer, hipStreamWaitValue32 >= it on
- * the consumer).  zs_sync_record enqueues the producer side on `stream`; zs_sync_wait makes
- * `stream` wait for the latest record (hipStreamWaitEvent's semantics; a never-recorded sync, or
- * one whose latest record has already executed — the host reads the flag word — enqueues
- * nothing).  A flag sync must be recorded from one stream at a time.  The ZeRO-3 gathers and
+/* Sync objects (ABI v12; v13: 64-bit epochs): a cross-stream ordering point that is either a HIP
+ * event (ZS_SYNC_EVENT) or a stream memory operation on a flag word in pinned host-coherent memory
+ * (ZS_SYNC_FLAG: hipStreamWriteValue64 of an epoch on the producer, hipStreamWaitValue64 >= it on
+ * the consumer; epochs only grow and never wrap).  zs_sync_record enqueues the producer side on
+ * `stream`; zs_sync_wait makes `stream` wait for the latest record (hipStreamWaitEvent's
+ * semantics; a never-recorded sync, or one whose latest record has already executed — the host
+ * reads the flag word — enqueues nothing).  A flag record from another stream than the previous
+ * record's first waits for that record (v13), so any stream may record.  The ZeRO-3 gathers and
  * gradient buckets (zero3.py:36-41, 131-147; their torch.cuda.synchronize() after each collective
  * becomes this ordering) use the synced group forms: record `ready` on after_stream and wait for
  * it on `stream`, the RCCL group, record `done` on `stream` (either sync may be NULL). */
@@ -403,6 +404,13 @@ int zs_sync_create(int kind, zs_sync** out);
 int zs_sync_destroy(zs_sync* sync);
 int zs_sync_record(zs_sync* sync, uintptr_t stream);
 int zs_sync_wait(zs_sync* sync, uintptr_t stream);
+/* Test hook (v13): move a flag sync's epoch (and its word) forward to `epoch` — every record made
+ * so far must have executed.  Lets a test cross an epoch boundary (2^32) without 2^32 records.
+ * ZS_ERR_INVALID for an event sync, a smaller epoch or a pending record. */
+int zs_sync_set_epoch(zs_sync* sync, uint64_t epoch);
+/* Diagnostic (v13): a flag sync's latest recorded epoch and the current value of its word (the
+ * word read through hipMemcpy when it lives in device memory); 0 / 0 for an event sync. */
+int zs_sync_query(zs_sync* sync, uint64_t* epoch, uint64_t* word);
 int zs_all_gather_group_synced(zs_comm* comm, int64_t n, const uint64_t* send,
                                const uint64_t* recv, const int64_t* send_count, int dtype,
                                uintptr_t after_stream, zs_sync* ready, uintptr_t stream,

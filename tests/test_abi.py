@@ -37,7 +37,7 @@ def test_library_is_gfx950_code_object():
 def test_abi_version_and_error_text():
     from zero_amd import _lib
 
-    assert _lib.lib.zs_abi_version() == _lib.ABI_VERSION == 12
+    assert _lib.lib.zs_abi_version() == _lib.ABI_VERSION == 13
     h = ctypes.c_void_p()
     rc = _lib.lib.zs_plan_create_ex(0, None, None, 0, 0, 0, 64, 0, 0, ctypes.byref(h))
     assert rc == _lib.ZS_ERR_INVALID

@@ -186,3 +186,142 @@ def test_expected_scaling_matches_the_planner_at_c4_n8():
     c5 = CONFIGS["C5"][1]()
     z = bench.expected_scaling(c5, 3, "chunk", 8)
     assert 3 * 8.03 * 2 * 7 / 8 <= z["bus_gb_per_rank"] < 3 * 8.1 * 2 * 7 / 8
+
+
+# --- a run that dies leaves evidence -----------------------------------------
+def test_default_watchdog_fires_inside_the_drivers_limit():
+    """The driver kills a bench run at 600 s; the default watchdog fires before, counted from
+    process start (the first import torch on a fresh box is part of the driver's clock)."""
+    assert bench.WATCHDOG_BUDGET_S <= 540.0
+    assert bench.watchdog_seconds(None, now=bench._T0) == bench.WATCHDOG_BUDGET_S < 600.0
+    assert bench.watchdog_seconds(None, now=bench._T0 + 120.0) == bench.WATCHDOG_BUDGET_S - 120.0
+    assert bench.watchdog_seconds(None, now=bench._T0 + 1e4) == 30.0  # (late start: still fires)
+    assert bench.watchdog_seconds(250.0) == 250.0 and bench.watchdog_seconds(0) == 0.0
+
+
+_STUCK = r"""
+import sys, time
+sys.path.insert(0, {repo!r})
+import bench
+bench._PARTIAL["rccl_selfcheck"] = {{"ok": True, "all_ranks_ok": True}}
+bench._PARTIAL["arena_calibration"] = {{"flat": {{"busbw_gbs": 123.5, "ms_per_step": 40.0}}}}
+bench._PARTIAL["exchange_check_all_arenas"] = {{"flat": {{"all_ranks_ok": True}}}}
+{setup}
+bench._phase("exchange check (buckets arena)")
+print("ready", file=sys.stderr, flush=True)
+def stuck_in_a_collective():
+    time.sleep(120)
+stuck_in_a_collective()
+"""
+
+
+def _run_stuck(setup, env=None, signal_after=None):
+    import os
+    import signal
+    import subprocess
+    import sys
+    import time
+
+    code = _STUCK.format(repo=str(bench.REPO), setup=setup)
+    p = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True, env=dict(os.environ, **(env or {})))
+    if signal_after is not None:
+        line = ""
+        while "ready" not in line:
+            line = p.stderr.readline()
+            assert line, "the child ended before it was ready"
+        time.sleep(signal_after)
+        p.send_signal(signal.SIGTERM)
+    out, err = p.communicate(timeout=60)
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    return p.returncode, lines, err
+
+
+def _check_partial(lines, err, phase="exchange check (buckets arena)"):
+    import json
+
+    assert len(lines) == 1, lines
+    d = json.loads(lines[0])
+    assert d["value"] is None and d["metric"] == bench.METRIC and d["failed_phase"] == phase
+    assert d["rccl_selfcheck"]["all_ranks_ok"] and d["arena_calibration"]["flat"]["busbw_gbs"] == 123.5
+    assert d["exchange_check_all_arenas"]["flat"]["all_ranks_ok"]
+    # every thread's Python stack, down to the frame that was stuck
+    assert "stuck_in_a_collective" in err and "Thread 0x" in err, err[-2000:]
+    return d
+
+
+def test_watchdog_dumps_stacks_and_prints_the_partial_line():
+    """An injected stuck phase: exit 3, every thread's stack on stderr, rank 0's JSON line with
+    value null, the phase and what was measured before it."""
+    rc, lines, err = _run_stuck("bench._start_watchdog(3.0)")
+    assert rc == 3, (rc, err[-2000:])
+    d = _check_partial(lines, err)
+    assert d["failure"].startswith("watchdog")
+
+
+def test_watchdog_on_a_nonzero_rank_prints_no_line():
+    rc, lines, err = _run_stuck("bench._start_watchdog(2.0)", env={"RANK": "3"})
+    assert rc == 3 and lines == [] and "stuck_in_a_collective" in err
+
+
+def test_sigterm_from_the_launcher_leaves_the_partial_line():
+    """torch.distributed.run ends the surviving ranks with SIGTERM once one rank has failed: the
+    rank blocked in a collective still dumps its stacks and prints the partial line (exit 143)."""
+    rc, lines, err = _run_stuck("bench._install_term_handler()", signal_after=1.0)
+    assert rc == 143, (rc, err[-2000:])
+    d = _check_partial(lines, err)
+    assert "SIGTERM" in d["failure"]
+
+
+def test_a_run_that_raises_prints_the_partial_line(tmp_path):
+    """main() on a machine without a GPU raises in its first device call: the run ends with exit
+    7 and ONE JSON line (value null, the phase, the error), not a bare traceback."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    if torch.cuda.is_available():
+        import pytest
+
+        pytest.skip("needs a machine without a GPU (the raise is the device call)")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(bench.REPO / "bench.py"), "--steps", "1", "--warmup", "0",
+                        "--no-cpu-baseline", "--watchdog-s", "0"], capture_output=True, text=True,
+                       timeout=300, env=env, cwd=tmp_path)
+    assert r.returncode == 7, (r.returncode, r.stderr[-3000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["value"] is None and d["error"] and d["config"]["workload"] == "C4"
+
+
+def test_layout_costs_of_reference_ownership_at_c4_n8():
+    """what the reference's whole-parameter ownership (Layout R) costs at N = 8 on
+    C4, from the planner: the slowest rank's Adam traffic is 15.23 GB against the balanced 1/8 of
+    79.95 GB = 9.99 GB for Layout Z (zero3.py's chunks) and Layout F (the flat arena's balanced
+    slices, the N > 1 line's layout_ablation leg); the exchange is the same, so the balanced flat
+    arena's ideal step is ~0.65 ms shorter, while Layout Z's bucket arena adds pack / unpack."""
+    import sys
+
+    sys.path.insert(0, str(bench.REPO / "distributed-training-sandbox_amd"))
+    from zero_amd.plan import Plan
+    from zero_amd.shapes import CONFIGS
+
+    c4 = CONFIGS["C4"][1]()
+    lc = bench.layout_costs(c4, 2, 8)
+    r, f, z = lc["reference_flat_arena"], lc["balanced_F_flat_arena"], lc["chunk_Z_bucket_arena"]
+    assert abs(r["max_rank_adam_gb"] - 15.23) < 0.01
+    assert abs(f["max_rank_adam_gb"] - 79.9526 / 8) < 0.01 and abs(z["max_rank_adam_gb"] - 9.99) < 0.01
+    # ... against the planner itself: 26 B per element of the longest Layout Z / F stream
+    numels = [int(np.prod(s)) for s in c4]
+    dim0 = [int(s[0]) for s in c4]
+    for layout, row in (("chunk", z), ("flat", f)):
+        pl = Plan(numels, 8, 0, layout, dim0=dim0, align_elems=64)
+        own = max(int(pl.pieces(k).length.sum()) for k in range(8))
+        assert abs(26 * own / 1e9 - row["max_rank_adam_gb"]) < 1e-3, layout
+    assert f["bus_gb_per_rank"] == r["bus_gb_per_rank"]
+    assert 0.5 < r["ideal_ms"] - f["ideal_ms"] < 0.8
+    assert z["hbm_gb_per_rank"] > r["hbm_gb_per_rank"]  # pack + unpack outweigh the balance
+    e = bench._expected_block(c4, 2, "flat", 8, 2, 26, 1024.0, measured_ms=20.0)
+    assert e["layouts"] == lc and e["curve"]["8"]["max_rank_adam_gb"] == r["max_rank_adam_gb"]

@@ -133,6 +133,45 @@ def test_zero2_ws1_mixed_handoffs_bit_exact(gpu):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_zero2_ws1_strided_assigned_grads_are_landed(gpu, dtype):
+    """a gradient the caller assigns that is not one dense run — a transpose
+    (``p.grad = x.t()``) or a stride-0 ``expand`` — has the parameter's shape and dtype, so torch
+    accepts it, but Adam would read ``numel`` contiguous elements from its pointer.  It must be
+    copied into its slot through torch (``_land``'s non-dense path) and read from there; the step
+    stays bit-exact against the oracle on the gradient's logical values."""
+    from oracle import c_oracle
+    from zero_amd import zero2
+
+    init_pg(0, 1, free_port())
+    try:
+        torch.manual_seed(2)
+        w = torch.nn.Parameter(torch.randn(64, 96, device=gpu).to(dtype))  # transposed grad
+        r = torch.nn.Parameter(torch.randn(48, 80, device=gpu).to(dtype))  # expanded row grad
+        c = torch.nn.Parameter(torch.randn(40, 64, device=gpu).to(dtype))  # expanded column grad
+        d = torch.nn.Parameter(torch.randn(256, device=gpu).to(dtype))     # dense, read in place
+        params = [w, r, c, d]
+        opt = zero2.ShardedOptimizer(torch.optim.Adam(params, lr=1e-3))
+        eng = opt.engine
+        st = _oracle_state(params, dtype)
+        for t in range(1, 5):
+            opt.zero_grad()
+            w.grad = (torch.randn(96, 64, device=gpu) * 1e-2).to(dtype).t()
+            r.grad = (torch.randn(1, 80, device=gpu) * 1e-2).to(dtype).expand(48, 80)
+            c.grad = (torch.randn(40, 1, device=gpu) * 1e-2).to(dtype).expand(40, 64)
+            d.grad = (torch.randn(256, device=gpu) * 1e-2).to(dtype)
+            assert not any(p.grad.is_contiguous() for p in params[:3])
+            grads = [p.grad.detach().contiguous().clone() for p in params]
+            dptr = d.grad.data_ptr()
+            opt.step()
+            _oracle_step(st, grads, c_oracle.hparams(step=t), dtype)
+            _assert_params(params, st, dtype, t)
+            assert all(eng.is_view(i, params[i].grad) for i in range(3))  # landed and adopted
+            assert d.grad.data_ptr() == dptr and eng.inplace_reads == 1
+    finally:
+        dist.destroy_process_group()
+
+
 def test_adamset_set_grads_rebinds_in_stream_order(gpu):
     """zs_adamset_set_grads: the same set run over two gradient buffers in turn (segments with
     vector parts and scalar tails) equals the oracle bit for bit; a misaligned pointer for a

@@ -77,6 +77,8 @@ def _zero12_cases(ws):
                   (_bf16comm_worker, ("zero2",)),
                   (ov_worker, (2, "traj_z2_ws4_d16_distinct.npz", True, "flat")),
                   (layout_worker, ("chunk", "traj_z2_ws4_d64_distinct.npz", "ragged", 64))]
+    if ws in (2, 8):  # the layout ablation's balanced Layout F in the flat arena (bench.py N > 1)
+        cases += [(layout_worker, ("flat", f"traj_z2_ws{ws}_d16_distinct.npz", "ragged", 64, "flat"))]
     if ws == 8:
         cases += [(_bf16comm_worker, ("zero2",))]
     return cases
@@ -102,7 +104,8 @@ def _zero3_cases(ws):
                  ("_update_hooks_single", "traj_z2_ws2_d16_distinct.npz"),
                  ("_update_hooks_wave3", "traj_z2_ws2_d16_distinct.npz"),
                  ("_update_hooks_events", "traj_z2_ws2_d16_distinct.npz"),
-                 ("_ref_mode_single", "traj_z3_ws2_d16_distinct.npz")],
+                 ("_ref_mode_single", "traj_z3_ws2_d16_distinct.npz"),
+                 ("_shards_changed", "traj_z2_ws2_d16_distinct.npz")],
              3: [("_update_injected", "traj_z2_ws3_d16_distinct.npz"),
                  ("_update_hooks_single", "traj_z2_ws3_d16_distinct.npz")],
              4: [("_ref_mode", "traj_z3_ws4_d16_distinct.npz"), ("_ref_injected", "traj_z3_ws4_d16_ref.npz"),
@@ -263,7 +266,7 @@ def _bench_rank(rank, ws, port, argv):
 def test_bench_share_gpu_n8_both_arenas(gpu):
     """The driver's default N=8 run (C4 ZeRO-2, ``--arena auto``) rehearsed through real RCCL on a
     4-layer copy of the SmolLM3-3B set (the full set at N = 8 takes minutes over sockets:
-    tools/r05.sh rehearsal8, profiles/r04_rccl_net/c4_n8_full.json): communicator
+    tools/r06.sh rehearsal8, profiles/r04_rccl_net/c4_n8_full.json): communicator
     self-check, then BOTH arenas the calibration can pick — the flat arena's grouped reduce /
     broadcast rounds and the bucket arena's pack / RS / AG / unpack — each exchange-checked (reduced
     grads within the ring bound, Adam within 1 bf16 ulp of the restatement, ranks bit-identical),

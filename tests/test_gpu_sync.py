@@ -150,3 +150,83 @@ def test_device_flag_words_order_streams(gpu, kind):
                 dst.copy_(src)
             cons.synchronize()
             assert bool((dst == float(it)).all()), (kind, it, behind)
+
+
+def _flag_syncs(host_words: bool, n: int):
+    from zero_amd import _lib
+    from zero_amd.comm import Sync
+
+    _lib.call("zs_tune", b"sync_host_flags", int(host_words), None)
+    try:
+        return [Sync(_lib.ZS_SYNC_FLAG) for _ in range(n)]
+    finally:
+        _lib.call("zs_tune", b"sync_host_flags", 1, None)
+
+
+@pytest.mark.parametrize("host_words", [True, False], ids=["host_word", "device_word"])
+def test_flag_epochs_cross_2_pow_32(gpu, host_words):
+    """a flag sync seeded at epoch 2^32 - 3 orders a slow producer before its
+    consumer on every record across 2^32 (ABI v13: 64-bit words; v12's 32-bit epoch wrapped there,
+    the GPU's unsigned >= was then satisfied by the stale pre-wrap word and the host skipped the
+    first wait).  Both word locations: pinned host (satisfied waits skipped on the host) and device
+    memory (every wait enqueued)."""
+    (sy,) = _flag_syncs(host_words, 1)
+    start = (1 << 32) - 3
+    sy.set_epoch(start)
+    assert sy.query() == (start, start)
+    prod, cons = torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)
+    src = torch.zeros(1 << 20, device=gpu)
+    dst = torch.full((1 << 20,), -1.0, device=gpu)
+    for it in range(1, 8):  # epochs 2^32 - 2 ... 2^32 + 4
+        with torch.cuda.stream(prod):
+            torch.cuda._sleep(SLEEP_CYCLES // 2)  # the host runs far ahead of the producer
+            src.fill_(float(it))
+        sy.record(prod.cuda_stream)
+        sy.wait(cons.cuda_stream)
+        with torch.cuda.stream(cons):
+            dst.copy_(src)
+        cons.synchronize()
+        assert bool((dst == float(it)).all()), (host_words, it)
+    torch.cuda.synchronize()
+    assert sy.query() == (start + 7, start + 7)
+    assert sy.query()[0] > (1 << 32)
+
+
+@pytest.mark.parametrize("host_words", [True, False], ids=["host_word", "device_word"])
+def test_flag_record_from_two_streams_keeps_epochs_in_order(gpu, host_words):
+    """a record from a second stream while the first stream's record is still pending.
+    The second write waits for the first, so the word ends at the latest epoch (v12 let the slow
+    first write land last and move the word back, so a later wait for the latest epoch could never
+    be satisfied), and a consumer of the second record sees the first producer's work too."""
+    (sy,) = _flag_syncs(host_words, 1)
+    a, b, cons = (torch.cuda.Stream(gpu) for _ in range(3))
+    src = torch.zeros(1 << 20, device=gpu)
+    dst = torch.full((1 << 20,), -1.0, device=gpu)
+    for it in range(1, 4):
+        with torch.cuda.stream(a):
+            torch.cuda._sleep(SLEEP_CYCLES)  # a's record executes long after b's
+            src.fill_(float(it))
+        sy.record(a.cuda_stream)
+        sy.record(b.cuda_stream)
+        sy.wait(cons.cuda_stream)
+        with torch.cuda.stream(cons):
+            dst.copy_(src)
+        cons.synchronize()
+        assert bool((dst == float(it)).all()), (host_words, it)
+        torch.cuda.synchronize()
+        epoch, word = sy.query()
+        assert epoch == 2 * it and word == epoch, (epoch, word)
+
+
+def test_set_epoch_refusals(gpu):
+    from zero_amd import _lib
+    from zero_amd.comm import Sync
+
+    (sy,) = _flag_syncs(True, 1)
+    sy.set_epoch(10)
+    with pytest.raises(_lib.ZeroAmdError):
+        sy.set_epoch(9)  # epochs only grow
+    ev = Sync(_lib.ZS_SYNC_EVENT)
+    with pytest.raises(_lib.ZeroAmdError):
+        ev.set_epoch(5)
+    assert ev.query() == (0, 0)

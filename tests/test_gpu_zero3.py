@@ -186,6 +186,56 @@ def _update_hooks(rank, ws, name, dev, comm=None, backward_hooks=None, side_stre
         assert sum(vp.size for vp in plans) == len(params)
 
 
+def _shards_changed(rank, ws, name, dev, comm=None):
+    """this rank's shards rewritten between two steps — after an eval forward
+    has consumed the step's ready sync and prefetched ahead — by ``p.data.copy_`` on the compute
+    stream (held back behind a spinning kernel, so an unordered side-stream gather would run
+    first).  After ``mark_params_changed()`` (or ``load_state_dict``, which marks) the next forward
+    must gather exactly the new shards, and the prefetched gathers of the old ones are dropped."""
+    from zero_amd import zero3
+
+    z = np.load(GOLDEN / name)
+    model = _model(z, dev)
+    kw = {} if comm is None else {"comm": comm}
+    opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
+                                 bucket_mb=2e-3, **kw)
+    zero3.register_zero3_hooks(model, opt.param_managers)
+    params = list(model.parameters())
+    lins = [m for m in model if isinstance(m, torch.nn.Linear)]
+    seen = []
+    for lin in lins:  # (after zero3's pre-hooks: sees the gathered full parameters)
+        lin.register_forward_pre_hook(lambda mod, a: seen.append(
+            [q.detach().clone() for q in mod.parameters(recurse=False)]))
+    x, y = _xy(z, rank, dev)
+    for _ in range(2):  # the runtime learns its order, then prefetches
+        opt.zero_grad()
+        torch.nn.functional.mse_loss(model(x), y).backward()
+        opt.step()
+    full_shapes = [tuple(z[f"init_{i}"].shape) for i in range(len(params))]
+    for k, how in enumerate(("mark", "load", "mark")):
+        with torch.no_grad():
+            model(x)  # eval forward
+        sd = opt.state_dict() if how == "load" else None
+        new = [torch.arange(int(np.prod(s)), dtype=torch.float32, device=dev).reshape(s) * 1e-3
+               + 10 * k + i for i, s in enumerate(full_shapes)]
+        if how == "load":
+            opt.load_state_dict(sd)
+        torch.cuda._sleep(50_000_000)  # the compute stream is far behind the host
+        with torch.no_grad():
+            for p, full in zip(params, new):
+                p.data.copy_(_chunk(full, ws, rank))
+        if how == "mark":
+            opt.mark_params_changed()
+        seen.clear()
+        opt.zero_grad()
+        torch.nn.functional.mse_loss(model(x), y).backward()
+        assert len(seen) == len(lins)
+        for j, got in enumerate(seen):
+            for q, want in zip(got, new[2 * j:2 * j + 2]):
+                assert torch.equal(q, want), (how, k, j)
+        opt.step()
+
+
 def _update_hooks_module(rank, ws, name, dev, comm=None):
     _update_hooks(rank, ws, name, dev, comm=comm, backward_hooks="module")
 

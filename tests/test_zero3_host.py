@@ -81,6 +81,9 @@ class _FakeRuntime:
         for fn in self.iteration_callbacks:
             fn()
 
+    def mark_inputs_changed(self):  # (register_zero3_hooks: nothing gathered before is reused)
+        self.log.append(("inputs changed",))
+
 
 class _FakeManager:
     """What register_zero3_hooks reads of a Zero3ParamManager (update mode: keep_full_grad)."""
