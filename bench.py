@@ -918,6 +918,22 @@ def layout_costs(shapes, zero, world, es=2, bpe=26, bucket_mb=None) -> dict:
     return out
 
 
+def _placement_dependence(placement: dict) -> dict:
+    """``roofline.placement_dependence``: the Adam rate is conditional on the physical memory its
+    streams landed on (DESIGN §5 allocation study) — per placed buffer the candidate kept, its
+    in-place stream rate, the route and what a plain single allocation gave (``unprobed_gbs``)."""
+    out = {"note": "frac is conditional on placement: Adam streams at the rate of the memory its "
+                   "buffers landed on (5.0-6.3 TB/s per allocation on MI355X, stable per "
+                   "allocation); the probe keeps the first candidate >= accept_gbs, else the "
+                   "fastest (plain hipMalloc candidates, then 1-GiB chunked ranges)"}
+    for name, pl in placement.items():
+        if isinstance(pl, dict) and pl.get("gbs"):
+            k = int(pl.get("chosen", 0))
+            out[name] = {"chosen": k, "of": len(pl["gbs"]), "chosen_gbs": pl["gbs"][k],
+                         "unprobed_gbs": pl.get("unprobed_gbs"), "route": pl.get("route", "hipMalloc")}
+    return out
+
+
 def match_traffic(want: dict, alg_bytes_per_launch: float, traffic_json=None):
     """roofline.traffic: HBM bytes per Adam launch from a PMC summary of THIS configuration —
     ``--traffic-json`` if given, else the profiles/*_pmc.json whose ``config`` equals ``want`` — used
@@ -2082,6 +2098,7 @@ def _main(args):
                 "avg_launch_ms": float(stats[1]), "alg_bytes_per_launch": float(stats[2]),
                 "launches_per_step": launches / args.steps,
                 "traffic_source": traffic_src, "traffic_note": traffic_note,
+                "placement_dependence": _placement_dependence(placement),
             },
         }
         out["step_roofline"] = step_roofline
@@ -2120,11 +2137,14 @@ def _main(args):
         if handoff_used == "default" and not multi:
             out["host_enqueue_note"] = (
                 "default hand-off: the host enqueues ~200 steps ahead at ~0.4 ms each, then each "
-                "step waits for the GPU (a HIP runtime resource bounds the queued depth — "
-                "presumably the kernel-argument pool: each step's gradient-pointer patch carries "
-                "a 1.8 KB table in its arguments; the views leg never waits), so over a long run "
-                "this average tends to the GPU's step time; it is not host work "
-                "(profiles/r05_handoff_host.json)")
+                "step waits for the GPU, so over a long run this average tends to the GPU's step "
+                "time; it is not host work.  The queued depth is bounded by the kernel-argument "
+                "bytes pending: each step's two gradient-pointer patch launches carry 1,808-B "
+                "arguments; the same step without them (unchanged pointers) or with two "
+                "small-argument launches instead never waits within 400 steps, the views step plus "
+                "two 1,808-B launches waits from step 174 (profiles/r06_handoff_host.json); "
+                "standalone, launches queue until ~3.7-4 MB of arguments are pending "
+                "(profiles/r06_queue_depth_probe.jsonl)")
         if collectives is not None:
             out["collectives"] = collectives
         if copy_kernels is not None:

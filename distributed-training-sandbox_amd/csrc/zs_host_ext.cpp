@@ -9,13 +9,28 @@
 // in C++ and rewrites each parameter's storage / sizes / strides / offset in place — the metadata
 // half of Tensor::set_data (`param.data = x`), no view tensors built.
 //
+// Round 6: GradCounter — the per-parameter post-accumulate-grad bookkeeping of the ZeRO-3 backward
+// (zero3.py:56-77's hooks fire per parameter; the gradient reduce-scatter buckets and the
+// per-module release count parameters) as C++ hooks on the parameters' AccumulateGrad: a
+// parameter's completed gradient decrements its bucket's / module's count without entering
+// Python, and Python is called once per completed bucket (or run of buckets) and once per
+// released module instead of once per parameter and counter.
+//
 // Built against the torch headers of this image (no HIP code): zero_amd/_hostext*.so.
+#include <Python.h>
+#include <torch/csrc/autograd/function_hook.h>
+#include <torch/csrc/autograd/variable.h>
 #include <torch/extension.h>
 
 #include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <tuple>
 #include <vector>
 
 namespace {
+namespace py = pybind11;
 
 class ViewPlan {
  public:
@@ -113,10 +128,167 @@ class ViewPlan {
   at::Device device_ = at::kCPU;
 };
 
+// Counts completed parameter gradients into slots.
+//   ordered (gradient buckets): slot k's count drops by one per parameter; whenever the run of
+//     completed slots from `next` grows, on_ready(new next) — the caller launches buckets
+//     [old next, new next) in order; a parameter counted twice before reset() is an error
+//     (the reference reduces each gradient once per step).
+//   unordered (modules): a slot counts only while open (open(slot, n) at the module's backward
+//     gather); when it reaches zero it closes and on_ready(slot) — the caller releases the module.
+// on_first() (may be None) runs at the first count after reset(): the caller queues its
+// end-of-backward callback from inside the backward.  Counting takes no GIL; the callbacks take it.
+class GradCounter {
+ public:
+  GradCounter(std::vector<int64_t> sizes, int64_t n_params, bool ordered, py::object on_first,
+              py::object on_ready, std::string twice_msg)
+      : sizes_(std::move(sizes)), ordered_(ordered), on_first_(std::move(on_first)),
+        on_ready_(std::move(on_ready)), twice_msg_(std::move(twice_msg)) {
+    TORCH_CHECK(n_params >= 0, "GradCounter: n_params < 0");
+    marked_.assign(static_cast<size_t>(n_params), 0);
+    reset();
+  }
+
+  ~GradCounter() {
+    if (Py_IsInitialized()) {
+      py::gil_scoped_acquire g;
+      on_first_ = py::object();
+      on_ready_ = py::object();
+    } else {  // interpreter gone: leak the two references rather than touch it
+      on_first_.release();
+      on_ready_.release();
+    }
+  }
+
+  void reset() {
+    std::lock_guard<std::mutex> lk(mu_);
+    pending_ = ordered_ ? sizes_ : std::vector<int64_t>(sizes_.size(), 0);
+    open_.assign(sizes_.size(), 0);
+    std::fill(marked_.begin(), marked_.end(), 0);
+    next_ = 0;
+    first_ = true;
+    counted_ = 0;
+  }
+
+  void open(int64_t slot, int64_t n) {
+    std::lock_guard<std::mutex> lk(mu_);
+    check_slot(slot);
+    pending_[slot] = n;
+    open_[slot] = n > 0;
+  }
+
+  void close_all() {
+    std::lock_guard<std::mutex> lk(mu_);
+    std::fill(open_.begin(), open_.end(), 0);
+  }
+
+  // one parameter's gradient is complete (param: its index for the twice check, or -1)
+  void count(int64_t param, int64_t slot) {
+    bool first = false;
+    int64_t ready = -1;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      check_slot(slot);
+      if (param >= 0 && static_cast<size_t>(param) < marked_.size()) {
+        TORCH_CHECK(!marked_[param], twice_msg_, " (parameter ", param, ")");
+        marked_[param] = 1;
+      }
+      ++counted_;
+      first = first_;
+      first_ = false;
+      if (ordered_) {
+        --pending_[slot];
+        const int64_t old = next_;
+        while (next_ < static_cast<int64_t>(pending_.size()) && pending_[next_] <= 0) ++next_;
+        if (next_ != old) ready = next_;
+      } else if (open_[slot] && --pending_[slot] == 0) {
+        open_[slot] = 0;
+        ready = slot;
+      }
+    }
+    if (!first && ready < 0) return;
+    py::gil_scoped_acquire g;
+    if (first && !on_first_.is_none()) on_first_();
+    if (ready >= 0 && !on_ready_.is_none()) on_ready_(ready);
+  }
+
+  int64_t next() const { return next_; }
+  int64_t counted() const { return counted_; }
+  std::vector<int64_t> pending() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return pending_;
+  }
+
+ private:
+  void check_slot(int64_t slot) const {
+    TORCH_CHECK(slot >= 0 && static_cast<size_t>(slot) < sizes_.size(), "GradCounter: slot ", slot,
+                " out of range [0, ", sizes_.size(), ")");
+  }
+
+  std::mutex mu_;
+  std::vector<int64_t> sizes_, pending_;
+  std::vector<uint8_t> open_, marked_;
+  bool ordered_;
+  int64_t next_ = 0, counted_ = 0;
+  bool first_ = true;
+  py::object on_first_, on_ready_;
+  std::string twice_msg_;
+};
+
+// The parameter's post-accumulate-grad hook slot holds ONE object (torch keeps its Python hooks
+// dict in it, torch/csrc/autograd/variable.h): this one runs whatever it replaced (the Python
+// hooks) first, then counts into its targets — a counter's callback may launch the gradient's
+// reduce-scatter and drop p.grad, so every Python hook, registered before the counter or after,
+// still sees the gradient backward produced.  attach() first makes sure the Python dict exists,
+// so a later Python registration adds to it instead of replacing the slot.
+struct CountingHook : torch::autograd::PostAccumulateGradHook {
+  std::vector<std::tuple<std::shared_ptr<GradCounter>, int64_t, int64_t>> targets;
+  std::unique_ptr<torch::autograd::PostAccumulateGradHook> prev;
+
+  void operator()(const torch::autograd::Variable& t) override {
+    if (prev) (*prev)(t);
+    const auto tg = targets;  // (a callback may detach a target)
+    for (const auto& [c, param, slot] : tg) c->count(param, slot);
+  }
+};
+
+void attach(const at::Tensor& param, const std::shared_ptr<GradCounter>& counter, int64_t index,
+            int64_t slot) {
+  TORCH_CHECK(param.requires_grad() && param.is_leaf(),
+              "attach: the tensor must be a leaf that requires grad");
+  auto& hook = torch::autograd::impl::post_acc_grad_hooks(param);
+  auto* ch = dynamic_cast<CountingHook*>(hook.get());
+  if (ch == nullptr) {
+    auto h = std::make_unique<CountingHook>();
+    h->prev = std::move(hook);
+    ch = h.get();
+    torch::autograd::impl::set_post_acc_grad_hooks(param, std::move(h));
+  }
+  ch->targets.emplace_back(counter, index, slot);
+}
+
+// drop every target of `counter` from the parameter's hook (the hook object itself stays: it may
+// be running — a callback detaching from inside the backward — and passes through to `prev`)
+void detach(const at::Tensor& param, const std::shared_ptr<GradCounter>& counter) {
+  auto& hook = torch::autograd::impl::post_acc_grad_hooks(param);
+  auto* ch = dynamic_cast<CountingHook*>(hook.get());
+  if (ch == nullptr) return;
+  auto& tg = ch->targets;
+  tg.erase(std::remove_if(tg.begin(), tg.end(),
+                          [&](const auto& t) { return std::get<0>(t) == counter; }),
+           tg.end());
+}
+
+int64_t attached(const at::Tensor& param) {
+  auto& hook = torch::autograd::impl::post_acc_grad_hooks(param);
+  auto* ch = dynamic_cast<CountingHook*>(hook.get());
+  return ch == nullptr ? -1 : static_cast<int64_t>(ch->targets.size());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
-  m.doc() = "zero_amd host helper: per-module install / release of ZeRO-3 gathered parameters";
+  m.doc() = "zero_amd host helper: per-module install / release of ZeRO-3 gathered parameters, "
+            "and the per-parameter gradient counting of the ZeRO-3 backward";
   pybind11::class_<ViewPlan>(m, "ViewPlan")
       .def(pybind11::init<std::vector<at::Tensor>, std::vector<at::Tensor>,
                           std::vector<std::vector<int64_t>>, std::vector<std::vector<int64_t>>,
@@ -126,4 +298,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("release", &ViewPlan::release)
       .def_property_readonly("size", &ViewPlan::size)
       .def_property_readonly("extent", &ViewPlan::extent);
+  pybind11::class_<GradCounter, std::shared_ptr<GradCounter>>(m, "GradCounter")
+      .def(pybind11::init<std::vector<int64_t>, int64_t, bool, py::object, py::object, std::string>(),
+           py::arg("sizes"), py::arg("n_params"), py::arg("ordered"), py::arg("on_first"),
+           py::arg("on_ready"), py::arg("twice_msg") = "gradient accumulated twice before reset")
+      .def("reset", &GradCounter::reset)
+      .def("open", &GradCounter::open)
+      .def("close_all", &GradCounter::close_all)
+      .def("count", &GradCounter::count, py::call_guard<py::gil_scoped_release>())
+      .def("pending", &GradCounter::pending)
+      .def_property_readonly("next", &GradCounter::next)
+      .def_property_readonly("counted", &GradCounter::counted);
+  m.def("attach", &attach, "count `param`'s completed gradients into counter slot `slot`");
+  m.def("detach", &detach, "drop every target of `counter` from `param`'s hook");
+  m.def("attached", &attached, "targets on `param`'s counting hook (-1: none installed)");
 }

@@ -1798,8 +1798,103 @@ int zs_device_alloc(int64_t bytes, void** out) {
   return ZS_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// Chunked allocations (zs_device_alloc_chunked): the physical handles behind each reserved range.
+struct ChunkedAlloc {
+  size_t bytes = 0;
+  std::vector<hipMemGenericAllocationHandle_t> handles;
+};
+std::mutex g_chunked_mu;
+std::map<void*, ChunkedAlloc> g_chunked;
+
+void chunked_release(void* p, ChunkedAlloc& a) {  // (every chunk of a live range is mapped)
+  (void)hipMemUnmap(p, a.bytes);
+  for (auto h : a.handles) (void)hipMemRelease(h);
+  (void)hipMemAddressFree(p, a.bytes);
+}
+}  // namespace
+
+extern "C" {
+
+int zs_device_alloc_chunked(int64_t bytes, int64_t chunk_bytes, void** out) {
+  ZS_REQUIRE(out != nullptr, "zs_device_alloc_chunked: out is NULL");
+  ZS_REQUIRE(bytes > 0 && chunk_bytes > 0, "zs_device_alloc_chunked: bytes and chunk_bytes must be > 0");
+  *out = nullptr;
+  int dev = 0;
+  ZS_HIP(hipGetDevice(&dev));
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = dev;
+  size_t gran = 0;
+  ZS_HIP(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum));
+  ZS_REQUIRE(gran > 0 && size_t(chunk_bytes) % gran == 0,
+             "zs_device_alloc_chunked: chunk_bytes %lld is not a multiple of the granularity %zu",
+             (long long)chunk_bytes, gran);
+  const size_t chunk = size_t(chunk_bytes);
+  const size_t total = (size_t(bytes) + chunk - 1) / chunk * chunk;
+  ChunkedAlloc a;
+  a.bytes = total;
+  void* p = nullptr;
+  hipError_t e = hipMemAddressReserve(&p, total, 0, nullptr, 0);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return zs::fail(ZS_ERR_HIP, "zs_device_alloc_chunked: hipMemAddressReserve(%zu): %s", total,
+                    hipGetErrorString(e));
+  }
+  for (size_t off = 0; off < total && e == hipSuccess; off += chunk) {
+    hipMemGenericAllocationHandle_t h;
+    e = hipMemCreate(&h, chunk, &prop, 0);
+    if (e != hipSuccess) break;
+    e = hipMemMap(static_cast<char*>(p) + off, chunk, 0, h, 0);
+    if (e != hipSuccess) {
+      (void)hipMemRelease(h);
+      break;
+    }
+    a.handles.push_back(h);
+  }
+  if (e == hipSuccess) {
+    hipMemAccessDesc acc = {};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    e = hipMemSetAccess(p, total, &acc, 1);
+  }
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    const size_t n = a.handles.size();
+    if (n) (void)hipMemUnmap(p, n * chunk);
+    for (auto h : a.handles) (void)hipMemRelease(h);
+    (void)hipMemAddressFree(p, total);
+    (void)hipGetLastError();
+    return zs::fail(e == hipErrorOutOfMemory ? ZS_ERR_NOMEM : ZS_ERR_HIP,
+                    "zs_device_alloc_chunked: %lld bytes in %lld-byte chunks: %s", (long long)bytes,
+                    (long long)chunk_bytes, hipGetErrorString(e));
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_chunked_mu);
+    g_chunked[p] = std::move(a);
+  }
+  *out = p;
+  return ZS_OK;
+}
+
 int zs_device_free(void* p) {
   if (p == nullptr) return ZS_OK;
+  {
+    std::unique_lock<std::mutex> lk(g_chunked_mu);
+    auto it = g_chunked.find(p);
+    if (it != g_chunked.end()) {
+      ChunkedAlloc a = std::move(it->second);
+      g_chunked.erase(it);
+      lk.unlock();
+      // hipFree waits for the device; an unmap does not: no queued work may still use the range
+      ZS_HIP(hipDeviceSynchronize());
+      chunked_release(p, a);
+      return ZS_OK;
+    }
+  }
   ZS_HIP(hipFree(p));
   return ZS_OK;
 }

@@ -32,3 +32,21 @@ class WeakCall:
 
     def alive(self) -> bool:
         return self._ref() is not None
+
+
+class WeakArgCall:
+    """``owner.<name>(*args, *call_args)`` through a weak reference to ``owner`` — the callbacks of
+    the C++ gradient counters (zero_amd/_hostext ``GradCounter``), which pass a bucket or module
+    index.  A no-op once the owner is gone."""
+
+    __slots__ = ("_ref", "_name", "_args")
+
+    def __init__(self, owner, name: str, *args):
+        self._ref = weakref.ref(owner)
+        self._name = name
+        self._args = args
+
+    def __call__(self, *call_args):
+        owner = self._ref()
+        if owner is not None:
+            getattr(owner, self._name)(*self._args, *call_args)

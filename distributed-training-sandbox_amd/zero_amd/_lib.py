@@ -42,7 +42,7 @@ EXPORTED = (
     "zs_sync_create", "zs_sync_destroy", "zs_sync_record", "zs_sync_wait", "zs_sync_set_epoch", "zs_sync_query",
     "zs_all_gather_group_synced", "zs_reduce_scatter_group_synced",
     "zs_group_start", "zs_group_end", "zs_rccl_version",
-    "zs_device_alloc", "zs_device_free", "zs_tune",
+    "zs_device_alloc", "zs_device_alloc_chunked", "zs_device_free", "zs_tune",
 )
 
 
@@ -158,6 +158,7 @@ _SIGS = {
     "zs_rccl_version": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "zs_device_alloc": ([_I64, ctypes.POINTER(_P)], ctypes.c_int),
     "zs_device_free": ([_P], ctypes.c_int),
+    "zs_device_alloc_chunked": ([_I64, _I64, ctypes.POINTER(_P)], ctypes.c_int),
     "zs_tune": ([ctypes.c_char_p, _I64, _PI64], ctypes.c_int),
 }
 

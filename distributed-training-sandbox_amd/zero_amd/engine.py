@@ -94,6 +94,15 @@ PROBE_MIN_BYTES = 1 << 30
 # guide's float4 copy: 6.29); in the slow regions at ~5.2 (profiles/r02_alloc/).  A candidate at or
 # above this is kept at once, without allocating the remaining ones.
 PROBE_ACCEPT_GBS = 5950.0
+# The probe's second route (round 6): when none of the plain allocations reaches
+# the acceptance rate, up to this many candidates of 1-GiB physical chunks (hipMemCreate) mapped
+# side by side into one virtual range (zs_device_alloc_chunked).  Interleaved A/B at the exact
+# fp32-master state size, 36 GiB, six rounds on one box (profiles/r06_vmm_modes_36g.jsonl):
+# plain hipMalloc 5.45-6.19 TB/s, 3 of 6 at >= 6.0; 1-GiB chunks 5.46-6.13, 4 of 6 at >= 6.0
+# (round 2's 12- and 40-GiB runs: no consistent winner) — a different draw of physical memory,
+# not a cure, so it is a fallback after the plain candidates, held under the same 3-buffer bound.
+PROBE_CHUNKED_TRIES = 3
+PROBE_CHUNK_BYTES = 1 << 30
 
 
 # device memory held by placed buffers (outside torch's cache), per device index: bytes and buffers
@@ -134,13 +143,17 @@ class _DeviceBuffer:
     ``zs_device_free`` when the last tensor viewing it is released (torch keeps this object alive
     through ``__cuda_array_interface__``).  Nothing here touches torch's caching allocator."""
 
-    def __init__(self, nbytes: int, device):
+    def __init__(self, nbytes: int, device, chunk_bytes: int = 0):
         import ctypes
 
         self.nbytes, self.device = int(nbytes), torch.device(device)
         ptr = ctypes.c_void_p()
         with torch.cuda.device(self.device):
-            _lib.call("zs_device_alloc", self.nbytes, ctypes.byref(ptr))
+            if chunk_bytes:  # physical chunks side by side in one virtual range (whole chunks)
+                self.nbytes = -(-self.nbytes // int(chunk_bytes)) * int(chunk_bytes)
+                _lib.call("zs_device_alloc_chunked", int(nbytes), int(chunk_bytes), ctypes.byref(ptr))
+            else:
+                _lib.call("zs_device_alloc", self.nbytes, ctypes.byref(ptr))
         self.ptr = int(ptr.value)
         acc = _placed(self.device.index or 0)
         acc["bytes"] += self.nbytes
@@ -199,10 +212,12 @@ def probed_zeros(n: int, dtype, device, tries: int = 8, accept_gbs: float = PROB
     speed (alloc_tlb2.jsonl: not a clock effect), and the fast buffers do not translate better
     (they see MORE UTCL1 misses; identical DRAM request counts — pmc_pass*.json).  So for buffers
     of 1 GiB or more, candidates are allocated and streamed once in place by the gfx950 copy
-    kernel; the first at ``accept_gbs`` or above is kept at once, otherwise the fastest of
-    ``tries``.  At most THREE candidates are held at once (the best so far, the newest, and the
+    kernel; the first at ``accept_gbs`` or above is kept at once.  When none of ``tries`` plain
+    allocations reaches it, up to ``PROBE_CHUNKED_TRIES`` more candidates take the second route —
+    1-GiB physical chunks mapped side by side (``zs_device_alloc_chunked``) — and the fastest of
+    all is kept.  At most THREE candidates are held at once (the best so far, the newest, and the
     last rejected one, so the next allocation cannot be handed the memory just rejected): peak
-    transient memory is 3x the buffer.
+    transient memory is 3x the buffer (chunked candidates: rounded up to whole GiB).
 
     Candidates are device allocations of their own (``zs_device_alloc``, outside torch's caching
     allocator — round 4): a rejected one goes straight back to the device, and the caller's cached
@@ -234,10 +249,20 @@ def probed_zeros(n: int, dtype, device, tries: int = 8, accept_gbs: float = PROB
                     probe="off" if tries <= 1 else "skipped: free memory short")
         return buf, info
     best = newest_rejected = None
-    for k in range(tries):
-        cand = _DeviceBuffer(nbytes, device)
+    chunked = PROBE_CHUNKED_TRIES if room >= 3 + (PROBE_CHUNK_BYTES * 3) // nbytes else 0
+    routes = ["hipMalloc"] * tries + ["chunked"] * chunked
+    info["routes"] = []
+    for k, route in enumerate(routes):
+        try:
+            cand = _DeviceBuffer(nbytes, device, PROBE_CHUNK_BYTES if route == "chunked" else 0)
+        except _lib.ZeroAmdError:
+            if route == "chunked":  # the virtual-memory API refused: the plain candidates stand
+                info["chunked_error"] = _lib.lib.zs_last_error().decode(errors="replace")[:200]
+                break
+            raise
         g = _stream_gbs(cand.ptr, nbytes, stream)
         info["gbs"].append(round(g, 1))
+        info["routes"].append(route)
         if best is None or g > best[0]:
             rejected, best = best, (g, k, cand)
         else:
@@ -258,8 +283,11 @@ def probed_zeros(n: int, dtype, device, tries: int = 8, accept_gbs: float = PROB
     out = keep.tensor(n, dtype)
     out.zero_()
     del best, newest_rejected, keep
+    route = info["routes"][chosen]
     info.update(tries=len(info["gbs"]), chosen=chosen, accept_gbs=accept_gbs,
-                unprobed_gbs=info["gbs"][0], held_max=3, allocator="zs_device_alloc (hipMalloc)")
+                unprobed_gbs=info["gbs"][0], held_max=3, route=route,
+                allocator="zs_device_alloc (hipMalloc)" if route == "hipMalloc" else
+                "zs_device_alloc_chunked (1-GiB hipMemCreate chunks in one range)")
     return out, info
 
 

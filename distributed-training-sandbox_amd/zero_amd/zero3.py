@@ -40,6 +40,7 @@ import contextlib
 import os
 import time
 import weakref
+from collections import OrderedDict
 
 import numpy as np
 import torch
@@ -49,7 +50,7 @@ from torch.utils.weak import WeakIdKeyDictionary
 from . import _lib
 from ._lib import ZS_BF16, ZS_BF16_SPLIT, ZS_F32
 from . import checkpoint as ckpt
-from ._hooks import WeakCall
+from ._hooks import WeakArgCall, WeakCall
 from ._sharded import adam_group_hparams
 from .comm import STREAM_SYNC, RcclComm, Sync, comm_stream, sync_kind, zs_dtype
 from .engine import ALIGN_ELEMS, probed_zeros
@@ -62,6 +63,10 @@ except ImportError:  # (an image whose torch ABI differs: the same steps per par
     _hostext = None
 if os.environ.get("ZERO_AMD_HOSTEXT", "1") == "0":  # A/B switch (tools/z3_host_ab.py)
     _hostext = None
+# the backward's per-parameter gradient counting (reduce-scatter buckets, module releases) in C++
+# hooks when the extension has them; False: one Python post-accumulate hook per parameter and
+# counter (read when hooks are registered; tools/z3_host_ab.py --no-counting)
+HOSTEXT_COUNTING = True
 
 
 def _chunk_geom(d0: int, ws: int, rank: int):
@@ -126,6 +131,27 @@ def _add_post_accumulate_hook(param, fn):
         _post_acc[param] = (param.register_post_accumulate_grad_hook(dispatch), weakref.ref(fns))
     fns.append(fn)
     return _PostAccHandle(param, fn)
+
+
+class _CounterHandle:
+    """``remove()`` detaches a parameter from a C++ gradient counter (the counting hook stays on the
+    parameter, passing through to its Python hooks)."""
+
+    __slots__ = ("_param", "_counter")
+
+    def __init__(self, param, counter, index: int, slot: int):
+        if param._post_accumulate_grad_hooks is None:
+            # torch's Python hooks dict first: a later Python registration then adds to it instead
+            # of replacing the hook slot the counter shares (csrc/zs_host_ext.cpp CountingHook)
+            param._post_accumulate_grad_hooks = OrderedDict()
+        _hostext.attach(param, counter, int(index), int(slot))
+        self._param, self._counter = weakref.ref(param), counter
+
+    def remove(self):
+        p = self._param()
+        if p is not None and self._counter is not None:
+            _hostext.detach(p, self._counter)
+        self._counter = None
 
 
 class _Gathered:
@@ -814,9 +840,12 @@ class Zero3ParamManager:
 
 
 class _TensorHookState:
-    """Holder of the tensor-style backward bookkeeping's ``grad_ready`` (register_zero3_hooks)."""
+    """Holder of the tensor-style backward bookkeeping's ``grad_ready`` / ``module_done``
+    (register_zero3_hooks)."""
 
     grad_ready = None
+    module_done = None
+    counter = None
 
 
 def _grad_tensors(output):
@@ -953,6 +982,19 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
     post_fwd = make_post("fwd")
     hooked = [m for m in model.modules() if mod_managers[id(m)]]
     managed = [mg for m in hooked for mg in mod_managers[id(m)]]
+    hooked_ids = [id(m) for m in hooked]
+    slot_of = {mid: k for k, mid in enumerate(hooked_ids)}
+    mods_of = {}  # id(param) -> the hooked modules it counts into (whatever requires grad)
+    for m in hooked:
+        for mg in mod_managers[id(m)]:
+            mods_of.setdefault(id(mg.param), []).append(id(m))
+    state = _TensorHookState()
+    counter = None
+    if HOSTEXT_COUNTING and _hostext is not None and hasattr(_hostext, "GradCounter"):
+        # module slots count their parameters' gradients in C++; Python hears once per module
+        counter = _hostext.GradCounter([0] * len(hooked), 0, False, None,
+                                       WeakArgCall(state, "module_done"))
+        state.counter = counter
     # per backward: how many of a module's parameters will count in (trainable ones), and which
     # modules each trainable parameter counts in; re-derived at the first backward gather of a
     # backward whenever requires_grad changed since (gradual unfreezing, frozen layers)
@@ -975,21 +1017,28 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
             p = mg.param
             if p.requires_grad and id(p) not in hooked_params:
                 # newly trainable: its post-accumulate hook from now on (keyed by id, so the hook
-                # the parameter holds keeps no reference to it)
+                # the parameter holds keeps no reference to it) — a C++ count into its modules'
+                # slots, or a Python hook per parameter
                 hooked_params.add(id(p))
-                handles.append(_add_post_accumulate_hook(p, WeakCall(state, "grad_ready", id(p))))
+                if counter is not None:
+                    for mid in mods_of[id(p)]:
+                        handles.append(_CounterHandle(p, counter, -1, slot_of[mid]))
+                else:
+                    handles.append(_add_post_accumulate_hook(p, WeakCall(state, "grad_ready", id(p))))
 
     open_ = {}     # id(module) -> managers gathered for its backward, not released yet
     pending = {}   # id(module) -> parameter gradients still to come this backward
     queued = [False]
     warned = set()
-    # the parameters' post-accumulate hooks reach grad_ready through a weak reference to this
-    # holder (a strong closure would be a cycle through the parameter's C++-held hook dict,
-    # _hooks.py); the module hooks below keep it alive as long as the model has them
-    state = _TensorHookState()
+    # the parameters' post-accumulate hooks (and the C++ counter's callback) reach grad_ready /
+    # module_done through a weak reference to ``state`` (a strong closure would be a cycle
+    # through the parameter's C++-held hook, _hooks.py); the module hooks below keep it alive as
+    # long as the model has them
 
     def end_backward():
         queued[0] = False
+        if counter is not None:
+            counter.close_all()
         for ms in open_.values():
             _release_group(ms)
         open_.clear()
@@ -1011,6 +1060,8 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
         open_[mid] = mod_managers[mid]
         # nothing will count in: released at the end of backward
         pending[mid] = n_req.get(mid, 0) or -1
+        if counter is not None:
+            counter.open(slot_of[mid], pending[mid])
 
     def forward_pre(module, *args):
         reset_stale()
@@ -1044,7 +1095,13 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
                 if pending[mid] == 0:
                     _release_group(open_.pop(mid))
 
+    def module_done(slot):  # (C++ counting: the module's last trainable gradient is in)
+        ms = open_.pop(hooked_ids[slot], None)
+        if ms is not None:
+            _release_group(ms)
+
     state.grad_ready = grad_ready
+    state.module_done = module_done
     forward_pre.state = state  # (the strong reference: module hook -> forward_pre -> state)
     for m in hooked:
         handles.append(m.register_forward_pre_hook(forward_pre))
@@ -1158,6 +1215,8 @@ class _GradReducer:
             self._cs_h = cs.cuda_stream
         self.timing = None  # optional list of (start, end, bus_bytes) per launched bucket
         self._rs_tables = {}
+        self.use_hostext = HOSTEXT_COUNTING  # (False: per-parameter Python hooks, for A/B)
+        self._counter = None     # the C++ gradient counter (register_hooks)
         self.reset()
 
     def _ready_sync(self, k: int, cur_h: int) -> Sync:
@@ -1177,14 +1236,45 @@ class _GradReducer:
         self.next = 0
         self.callback_queued = False
         self.launched_in_backward = 0
+        if getattr(self, "_counter", None) is not None:
+            self._counter.reset()
 
     def register_hooks(self):
-        # weakly (_hooks.py): the reducer is owned by its optimizer
-        return [_add_post_accumulate_hook(p, WeakCall(self, "on_grad_ready", i))
-                for i, p in enumerate(self.opt.params) if p.requires_grad]
+        """The parameters' post-accumulate-grad counting.  With the host extension: C++ hooks
+        (``_hostext.GradCounter``, csrc/zs_host_ext.cpp) count each completed gradient into its
+        bucket without entering Python, which hears once per completed run of buckets
+        (``_launch_upto``) and once per backward (``_first_grad``) — 34 + 1 calls per C5 backward
+        instead of 291.  Without it: one Python hook per parameter (``on_grad_ready``).  Either
+        way the callbacks hold the reducer weakly (_hooks.py): it is owned by its optimizer."""
+        params = [(i, p) for i, p in enumerate(self.opt.params) if p.requires_grad]
+        if self.use_hostext and _hostext is not None and hasattr(_hostext, "GradCounter"):
+            self._counter = _hostext.GradCounter(
+                self._size_l, len(self.opt.params), True, WeakCall(self, "_first_grad"),
+                WeakArgCall(self, "_launch_upto"),
+                "zero_amd ZeRO-3: gradient accumulated twice before step(); update mode "
+                "reduce-scatters each gradient once per step")
+            return [_CounterHandle(p, self._counter, i, self._bucket_of_l[i]) for i, p in params]
+        return [_add_post_accumulate_hook(p, WeakCall(self, "on_grad_ready", i)) for i, p in params]
+
+    def _first_grad(self):
+        """The first gradient of a backward (C++ counting): the end-of-backward flush, queued from
+        inside the backward."""
+        if not self.callback_queued:
+            self.callback_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._end_backward)
+
+    def _launch_upto(self, upto: int):
+        """Buckets [next, upto) are complete (C++ counting): launch them, in order."""
+        while self.next < upto:
+            self._launch(self.next)
+            self.launched_in_backward += 1
+            self.next += 1
 
     def on_grad_ready(self, i: int, _param=None):
         """Parameter i's gradient is complete (its post-accumulate-grad hook, or by hand)."""
+        if self._counter is not None:
+            self._counter.count(i, self._bucket_of_l[i])
+            return
         if self.marked[i]:
             raise RuntimeError(
                 "zero_amd ZeRO-3: gradient of parameter %d accumulated twice before step(); "

@@ -311,8 +311,13 @@ int zs_adam_step_ex(float* p, uint16_t* p_bf16, const void* g, int g_dtype, floa
 /* hipMalloc of `bytes` (> 0) into *out; ZS_ERR_NOMEM when the device is full. */
 int zs_device_alloc(int64_t bytes, void** out);
 /* hipFree (NULL is a no-op).  Synchronises the device as hipFree does: only for buffers no queued
- * work still uses. */
+ * work still uses.  Also frees a zs_device_alloc_chunked range (unmap, release, address free). */
 int zs_device_free(void* p);
+/* (v13) `bytes` rounded up to whole `chunk_bytes` chunks: physical chunks of their own
+ * (hipMemCreate) mapped side by side into one reserved virtual range, read / write for this
+ * device.  The placement probe's second route (zero_amd/engine.py probed_zeros): tried when no
+ * plain allocation streams at the acceptance rate.  Freed with zs_device_free. */
+int zs_device_alloc_chunked(int64_t bytes, int64_t chunk_bytes, void** out);
 
 /* Diagnostic A/B knobs (process-wide; the defaults are the measured best, so a product caller
  * never needs this): "dq_unroll" (4 / 8 / 16 accesses in flight per lane of the fp8 dequantise),

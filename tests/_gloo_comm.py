@@ -191,21 +191,47 @@ def _add_table_methods(cls):
 _add_table_methods(GlooStagedComm)
 
 
+# RcclComm per (world size, rank) within ONE batch of cases (tests/_zero_run.py _run_seq opens
+# and closes the scope on every rank, so every rank of a batch creates — or reuses — its
+# communicator at the same case): an RCCL communicator over the socket transport costs ~1-2 s to
+# bootstrap at ws = 8, and a batch runs up to a dozen cases.  The communicator is independent of
+# the per-case torch.distributed group it was bootstrapped over.
+_RCCL_SCOPE = [None]
+
+
+def open_comm_scope():
+    _RCCL_SCOPE[0] = {}  # (what an earlier, failed batch left open is not touched)
+
+
+def close_comm_scope():
+    comms, _RCCL_SCOPE[0] = _RCCL_SCOPE[0], None
+    for c in (comms or {}).values():
+        c.close()
+
+
 def test_comm(group=None):
     """The multi-rank GPU workers' communicator.  Default: GlooStagedComm.  With
     ``ZS_TEST_COMM=rccl`` (tests/test_gpu_rccl.py): the PRODUCT communicator, RcclComm — every rank
     of the one-GPU box is made a separate node to RCCL by its own NCCL_HOSTID, so RCCL accepts the
     shared device and runs its real collectives (its kernels, ring order and bf16 rounding) between
     the ranks through the socket transport over loopback.  NCCL_HOSTID is read at communicator
-    init, so it is set here, per rank, just before."""
+    init, so it is set here, per rank, just before.  Inside a batch scope (open_comm_scope) the
+    world group's communicator is created once and reused by the batch's later cases."""
     if os.environ.get("ZS_TEST_COMM", "") != "rccl":
         return GlooStagedComm(group)
     from zero_amd.comm import RcclComm
 
+    scope = _RCCL_SCOPE[0]
+    key = (dist.get_world_size(), dist.get_rank()) if group is None else None
+    if scope is not None and key in scope:
+        return scope[key]
     os.environ["NCCL_HOSTID"] = f"zs-test-rank{dist.get_rank()}"
     os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     os.environ.setdefault("NCCL_IB_DISABLE", "1")
-    return RcclComm(group)
+    c = RcclComm(group)
+    if scope is not None and key is not None:
+        scope[key] = c
+    return c
 
 
 class SimRankComm:

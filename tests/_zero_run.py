@@ -229,8 +229,13 @@ def spawn_all_ranks(fn, ws: int, args=(), deadline_s: float = 150.0):
 
 
 def _run_seq(rank, calls):
+    from _gloo_comm import close_comm_scope, open_comm_scope
+
+    open_comm_scope()  # (every rank: the batch's cases share one RCCL communicator per rank)
     for fn, args in calls:
         fn(rank, *args)
+    # (closed only after success: a failed case may have left a collective a dead peer never joins)
+    close_comm_scope()
 
 
 def spawn_batch(ws: int, cases, all_spawned: bool = False, deadline_s: float = 150.0):

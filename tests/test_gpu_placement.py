@@ -86,3 +86,41 @@ def test_zero3_update_state_freed_with_optimizer(gpu, pg1):
     gc.collect()
     torch.cuda.synchronize()
     assert engine.placed_bytes() == before
+
+
+def test_probe_falls_back_to_chunked_route(gpu, monkeypatch):
+    """when no plain allocation reaches the acceptance rate, the probe tries 1-GiB
+    physical chunks mapped side by side (zs_device_alloc_chunked) and keeps the fastest of every
+    candidate; a chunked buffer works as any other (zero-filled, written and read back through
+    torch) and goes back to the device with its tensor."""
+    import gc
+
+    from zero_amd import engine
+
+    monkeypatch.setattr(engine, "PROBE_CHUNKED_TRIES", 2)
+    before = engine.placed_bytes()
+    n = (5 << 30) // 4 + 7  # 5 GiB + a bit of fp32: the chunked candidates round up to 6 GiB
+    buf, info = engine.probed_zeros(n, torch.float32, gpu, tries=2, accept_gbs=1e9)  # never accepted
+    assert info["routes"] == ["hipMalloc", "hipMalloc", "chunked", "chunked"], info
+    assert info["tries"] == 4 and len(info["gbs"]) == 4 and min(info["gbs"]) > 1000.0, info
+    assert info["route"] == info["routes"][info["chosen"]]
+    assert info["gbs"][info["chosen"]] == max(info["gbs"])
+    assert buf.numel() == n and int(torch.count_nonzero(buf)) == 0
+    buf[-3:] = torch.tensor([1.0, 2.0, 3.0], device=gpu)
+    buf[:5] = 4.0
+    assert buf[-3:].tolist() == [1.0, 2.0, 3.0] and float(buf[:5].sum()) == 20.0
+    assert engine.placed_bytes() - before in (6 << 30, n * 4)  # only the kept buffer is held
+    del buf
+    gc.collect()
+    torch.cuda.synchronize()
+    assert engine.placed_bytes() == before
+
+
+def test_chunked_allocation_refuses_a_bad_chunk_size(gpu):
+    import ctypes
+
+    from zero_amd import _lib
+
+    p = ctypes.c_void_p()
+    rc = _lib.lib.zs_device_alloc_chunked(1 << 20, 12345, ctypes.byref(p))
+    assert rc == _lib.ZS_ERR_INVALID and not p.value

@@ -142,3 +142,113 @@ def test_gathered_pairs_with_and_without_a_plan():
     for (_, x), (_, y), (shape, stride, off) in zip(a, b, views):
         assert x.shape == y.shape == shape and x.stride() == y.stride() == stride
         assert x.data_ptr() == y.data_ptr() == hold.data_ptr() + off * hold.element_size()
+
+
+# --- GradCounter: the ZeRO-3 backward's per-parameter gradient counting in C++ (round 6) ------
+def _chain(n=5, width=8):
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.randn(width, width) * 0.1) for _ in range(n)]
+
+    def loss():
+        h = torch.ones(2, width)
+        for p in ps:
+            h = torch.tanh(h @ p)
+        return h.sum()
+    return ps, loss
+
+
+def test_ordered_counter_calls_python_once_per_completed_run_of_buckets():
+    """Backward produces the chain's gradients last parameter first; buckets (in backward order)
+    [4, 3] [2] [1, 0]: Python hears 'next = 1' after parameter 3, 'next = 2' after 2 and 'next =
+    3' after 0 — three calls for five gradients — plus one on_first at the first gradient; the
+    Python post-accumulate hooks registered before and after the counter still run, in order, and
+    BEFORE the count (a bucket launch drops p.grad: every Python hook still sees the gradient)."""
+    ext = _ext()
+    ps, loss = _chain()
+    bucket_of = [2, 2, 1, 0, 0]
+    log = []
+    ps[2].register_post_accumulate_grad_hook(lambda p: log.append("py-before"))
+    c = ext.GradCounter([2, 1, 2], len(ps), True, lambda: log.append("first"),
+                        lambda nxt: log.append(("ready", nxt)), "twice")
+    for i, p in enumerate(ps):
+        ext.attach(p, c, i, bucket_of[i])
+    ps[2].register_post_accumulate_grad_hook(lambda p: log.append("py-after"))
+    loss().backward()
+    assert log == ["first", ("ready", 1), "py-before", "py-after", ("ready", 2), ("ready", 3)], log
+    assert c.next == 3 and c.counted == 5 and c.pending() == [0, 0, 0]
+    assert [ext.attached(p) for p in ps] == [1] * 5
+    # a second backward before reset(): every gradient would be reduced twice
+    with pytest.raises(RuntimeError, match="twice"):
+        loss().backward()
+    c.reset()
+    log.clear()
+    for p in ps:
+        p.grad = None
+    loss().backward()
+    assert log[0] == "first" and log[-1] == ("ready", 3)
+
+
+def test_unordered_counter_counts_open_slots_only_and_detaches():
+    """Module counting: a slot counts only while open (from its backward gather), fires once when
+    its last trainable parameter's gradient is in, and a detached counter hears nothing."""
+    ext = _ext()
+    ps, loss = _chain(4)
+    fired = []
+    c = ext.GradCounter([0, 0], 0, False, None, lambda slot: fired.append(slot))
+    slot_of = [0, 0, 1, 1]
+    for i, p in enumerate(ps):
+        ext.attach(p, c, -1, slot_of[i])
+    c.open(1, 2)  # module 1 (params 2, 3) open; module 0 never opened
+    loss().backward()
+    assert fired == [1]
+    c.reset()
+    c.open(0, 2)
+    c.open(1, -1)  # nothing will count in: never fires (released at the end of backward)
+    for p in ps:
+        p.grad = None
+    loss().backward()
+    assert fired == [1, 0]
+    for p in ps:
+        ext.detach(p, c)
+        p.grad = None
+    c.reset()
+    c.open(0, 2)
+    c.open(1, 2)
+    loss().backward()
+    assert fired == [1, 0] and [ext.attached(p) for p in ps] == [0] * 4
+    with pytest.raises(RuntimeError, match="out of range"):
+        c.open(2, 1)
+
+
+def test_counter_callbacks_hold_their_owner_weakly():
+    """The counter lives on the parameters' hooks; its callbacks must not keep the reducer alive
+    (zero_amd/_hooks.py): a WeakArgCall to a dropped owner is a no-op."""
+    import gc
+    import weakref
+
+    from zero_amd._hooks import WeakArgCall
+
+    ext = _ext()
+    ps, loss = _chain(2)
+
+    class Owner:
+        def __init__(self):
+            self.seen = []
+
+        def ready(self, k):
+            self.seen.append(k)
+
+    o = Owner()
+    c = ext.GradCounter([2], 2, True, None, WeakArgCall(o, "ready"))
+    for i, p in enumerate(ps):
+        ext.attach(p, c, i, 0)
+    loss().backward()
+    assert o.seen == [1]
+    ref = weakref.ref(o)
+    del o
+    gc.collect()
+    assert ref() is None
+    c.reset()
+    for p in ps:
+        p.grad = None
+    loss().backward()  # the owner is gone: nothing happens

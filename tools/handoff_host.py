@@ -4,6 +4,15 @@ them in place after a gradient-pointer patch launch) and through the views hand-
 synchronisation inside the loop: shows how far the host runs ahead of the GPU before a launch has
 to wait, i.e. whether bench.py's ``host_enqueue_ms_per_step`` measures host work or the GPU.
 
+Round 6 (is the bound the kernel-argument pool?): the same step with the
+patch launches' argument payload taken out or put back —
+  default_same_grads  one gradient set every step: the pointers never change, no patch launch;
+  views_plus_patch    the views step + two patch launches (1,808-B GradPatch arguments) per step
+                      on a one-segment dummy set (negligible GPU work);
+  views_plus_small    the views step + two launches with small arguments (zs_scale of 64 floats).
+If views_plus_patch blocks like default and views_plus_small like views, the depth follows the
+argument bytes (tools/queue_depth_probe.hip measures the pool itself).
+
 Usage: python tools/handoff_host.py [--config C4] [--steps 400] [--out …]
 """
 from __future__ import annotations
@@ -78,11 +87,46 @@ def main():
         opt.step()
 
     run("default", default_step)
+
+    def default_same():
+        opt.zero_grad()
+        for p, g in zip(params, sets[0]):
+            p.grad = g
+        opt.step()
+
+    run("default_same_grads", default_same)
     opt.zero_grad(set_to_none=False)
     with torch.no_grad():
         for p, g in zip(params, sets[0]):
             p.grad.copy_(g)
     run("views", lambda: opt.step())
+
+    from zero_amd import _lib
+    from zero_amd.kernels import AdamSet
+
+    dp = torch.zeros(256, device=dev)
+    dm, dv = torch.zeros_like(dp), torch.zeros_like(dp)
+    dg = [torch.zeros_like(dp), torch.zeros_like(dp)]
+    rows = np.array([[0, dp.data_ptr(), dp.data_ptr(), 0, dm.data_ptr(), dv.data_ptr(), 0, 0, 256]],
+                    np.uint64)
+    dummy = AdamSet(rows, _lib.ZS_F32)
+    ptrs = [np.array([g.data_ptr()], np.uint64) for g in dg]
+    st = torch.cuda.current_stream()
+
+    def views_plus_patch():
+        opt.step()
+        dummy.set_grads(ptrs[0], st)  # (alternating pointers: each call launches one patch)
+        dummy.set_grads(ptrs[1], st)
+
+    run("views_plus_patch", views_plus_patch)
+    small = torch.ones(64, device=dev)
+
+    def views_plus_small():
+        opt.step()
+        for _ in range(2):
+            _lib.call("zs_scale", small.data_ptr(), 64, _lib.ZS_F32, 1.0, st.cuda_stream)
+
+    run("views_plus_small", views_plus_small)
     if args.out:
         Path(args.out).write_text(json.dumps(res, indent=1) + "\n")
     dist.destroy_process_group()

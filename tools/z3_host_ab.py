@@ -7,8 +7,10 @@ host time).  Wall time per iteration and process CPU time (all threads: the back
 autograd's device thread) per block — the box's host speed drifts by 30 % over minutes, so only
 the interleaved comparison means anything.
 
-Usage: python tools/z3_host_ab.py [--config C5] [--ws 8] [--iters 20] [--blocks 6] [--baseline r02|r03]
-       [--events] [--single] [--no-hostext]   (extra variants of the current runtime)
+Usage: python tools/z3_host_ab.py [--config C5] [--ws 8] [--iters 20] [--blocks 6]
+       [--baseline none|r02|r03] [--events] [--single] [--no-hostext] [--no-counting]
+       (extra variants of the current runtime; --no-counting: the per-parameter Python
+       post-accumulate hooks instead of the C++ gradient counters, round 6)
 The baseline module is ``git show <rev>:distributed-training-sandbox_amd/zero_amd/zero3.py`` (r02:
 1653aab, r03: 3d19026 — the runtimes profiles/r03_z3_host_ab*.json and r04_z3_host_ab.json compare),
 written to tools/.baselines/ (git-ignored, so it travels to the GPU box, which has no git history):
@@ -52,7 +54,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--baseline", default="r03", choices=sorted(BASELINE_REVS))
+    ap.add_argument("--baseline", default="none", choices=["none"] + sorted(BASELINE_REVS))
     ap.add_argument("--extract-only", action="store_true",
                     help="write the baseline module under tools/.baselines/ and exit (no GPU)")
     ap.add_argument("--out", default=None)
@@ -62,8 +64,11 @@ def main():
                     help="also time the current runtime with side_stream=False")
     ap.add_argument("--no-hostext", action="store_true",
                     help="also time the current runtime without the C++ install / release")
+    ap.add_argument("--no-counting", action="store_true",
+                    help="also time the current runtime with per-parameter Python post-accumulate "
+                         "hooks instead of the C++ gradient counters")
     args = ap.parse_args()
-    path = baseline_file(args.baseline)
+    path = baseline_file(args.baseline) if args.baseline != "none" else None
     if args.extract_only:
         print(path)
         return
@@ -77,12 +82,14 @@ def main():
     from zero_amd.paramset import ParamSetModel, decoder_layer_groups
     from zero_amd.shapes import CONFIGS
 
-    base = "round2" if args.baseline == "r02" else "round3"
-    spec = importlib.util.spec_from_file_location(f"zero_amd._zero3_{args.baseline}", path)
-    z3_old = importlib.util.module_from_spec(spec)
-    sys.modules[spec.name] = z3_old
-    spec.loader.exec_module(z3_old)
-    assert z3_old.__package__ == zero_amd.__name__
+    base = {"r02": "round2", "r03": "round3"}.get(args.baseline)
+    z3_old = None
+    if path is not None:
+        spec = importlib.util.spec_from_file_location(f"zero_amd._zero3_{args.baseline}", path)
+        z3_old = importlib.util.module_from_spec(spec)
+        sys.modules[spec.name] = z3_old
+        spec.loader.exec_module(z3_old)
+        assert z3_old.__package__ == zero_amd.__name__
 
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", str(bench._free_port()))
@@ -103,11 +110,19 @@ def main():
         mod.get = lambda what, dm=None: {"ws": ws, "rank": 0}.get(what) if what in ("ws", "rank") \
             else real_get(what, dm)
         use_hostext = okw.pop("use_hostext", True)
-        opt = mod.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
-                                   sync=False, comm=bench._NoComm(ws), **okw)
-        if hasattr(opt, "runtime") and opt.runtime is not None:
-            opt.runtime.use_hostext = use_hostext
-        mod.register_zero3_hooks(model, opt.param_managers)
+        counting = okw.pop("counting", True)
+        saved = getattr(mod, "HOSTEXT_COUNTING", None)
+        if saved is not None:
+            mod.HOSTEXT_COUNTING = counting
+        try:
+            opt = mod.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
+                                       sync=False, comm=bench._NoComm(ws), **okw)
+            if hasattr(opt, "runtime") and opt.runtime is not None:
+                opt.runtime.use_hostext = use_hostext
+            mod.register_zero3_hooks(model, opt.param_managers)
+        finally:
+            if saved is not None:
+                mod.HOSTEXT_COUNTING = saved
         x = torch.zeros(1, device=dev, requires_grad=True)
 
         def step():
@@ -116,7 +131,10 @@ def main():
             opt.step()
         return step
 
-    variants = {base: build(z3_old, 0), "current": build(z3_new, 0)}
+    variants = {base: build(z3_old, 0)} if z3_old is not None else {}
+    variants["current"] = build(z3_new, 0)
+    if args.no_counting:  # the current runtime with per-parameter Python post-accumulate hooks
+        variants["current_no_counting"] = build(z3_new, 0, counting=False)
     if args.events:  # the current runtime ordered by HIP events instead of stream flags
         variants["current_events"] = build(z3_new, 0, stream_sync="event")
     if args.single:  # the current runtime with its collectives on the compute stream
