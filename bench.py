@@ -311,6 +311,14 @@ class _stdout_to_stderr:
 def _phase(name: str) -> None:
     _PHASE[0] = name
     log(f"[bench] phase: {name}")
+    # test hook (a rehearsal of a hung collective): rank ZS_BENCH_INJECT_RANK stops at the first
+    # phase whose name starts with ZS_BENCH_INJECT_HANG, so its peers wait in their next collective
+    hang = os.environ.get("ZS_BENCH_INJECT_HANG")
+    if hang and name.startswith(hang) and \
+            os.environ.get("RANK", "0") == os.environ.get("ZS_BENCH_INJECT_RANK", "1"):
+        log(f"[bench] ZS_BENCH_INJECT_HANG: rank {os.environ.get('RANK', '0')} stops in '{name}'")
+        while True:
+            time.sleep(3600)
 
 
 # The driver kills a bench run after 600 s of its own clock (BENCH_r05.json run.timeout_s), and a

@@ -7,6 +7,7 @@ local gradients per rank and step (tests/golden/traj_*.npz, ``r{rank}_t{t}_lg{i}
 from __future__ import annotations
 
 import os
+import time
 
 import numpy as np
 import torch
@@ -162,8 +163,33 @@ def run_backward(z, variant: int, rank: int, ws: int, device, comm=None, tol=1e-
     return opt
 
 
-def _shifted(i, fn, args):
+def _shifted(i, fn, args, env=None):
+    _apply_env(env)
     fn(i + 1, *args)
+
+
+# How the ranks beside this process are started.  "forkserver" (default): forked from a server
+# process that has already imported torch, numpy and zero_amd (and never touches the GPU), so a
+# rank does not pay the imports — a spawned rank spent ~2-3 s of CPU importing, and the suite
+# starts ~40 sets of ranks; "spawn": a fresh interpreter per rank.  A forked rank starts from the
+# server's environment, so the caller's environment at start time is passed and applied first
+# (GPU_MAX_HW_QUEUES, NCCL_*, ZS_TEST_COMM are read after that, at HIP / RCCL init or in the case).
+START_METHOD = os.environ.get("ZS_START_METHOD", "forkserver")
+_PRELOAD = ["numpy", "torch", "torch.distributed", "zero_amd", "zero_amd.zero2", "zero_amd.zero3"]
+
+
+def _start_method():
+    if START_METHOD == "forkserver":
+        import multiprocessing as mpm
+
+        mpm.set_forkserver_preload(_PRELOAD)  # (only read when the server starts)
+    return START_METHOD
+
+
+def _apply_env(env):
+    if env is not None:
+        os.environ.clear()
+        os.environ.update(env)
 
 
 # Environment of the ranks a multi-rank GPU test spawns beside this process.  Up to 8 processes
@@ -195,10 +221,11 @@ class child_env:
         return False
 
 
-def _child(i, fn, args, deadline_s):
+def _child(i, fn, args, deadline_s, env=None):
     import faulthandler
     import sys
 
+    _apply_env(env)
     # a rank stuck in a device-side wait (a peer died inside a collective) dumps its stack and
     # exits on its own instead of holding the GPU
     faulthandler.dump_traceback_later(deadline_s, exit=True, file=sys.stderr)
@@ -215,8 +242,8 @@ def spawn_all_ranks(fn, ws: int, args=(), deadline_s: float = 150.0):
     import torch.multiprocessing as mp
 
     with child_env():
-        ctx = mp.start_processes(_child, args=(fn, args, deadline_s), nprocs=ws, join=False,
-                                 start_method="spawn")
+        ctx = mp.start_processes(_child, args=(fn, args, deadline_s, dict(os.environ)), nprocs=ws,
+                                 join=False, start_method=_start_method())
     t_end = time.time() + deadline_s + 30
     try:
         while not ctx.join(timeout=1.0):  # raises (and kills the rest) when a rank fails
@@ -232,8 +259,13 @@ def _run_seq(rank, calls):
     from _gloo_comm import close_comm_scope, open_comm_scope
 
     open_comm_scope()  # (every rank: the batch's cases share one RCCL communicator per rank)
+    log = os.environ.get("ZS_CASE_LOG") if rank == 0 else None  # per-case seconds (suite budget)
     for fn, args in calls:
+        t0 = time.perf_counter()
         fn(rank, *args)
+        if log:
+            with open(log, "a") as f:
+                f.write(f"{time.perf_counter() - t0:8.2f} s  ws={args[0]}  {fn.__name__}{args[2:]}\n")
     # (closed only after success: a failed case may have left a collective a dead peer never joins)
     close_comm_scope()
 
@@ -270,8 +302,8 @@ def spawn_ranks(fn, ws: int, args=()):
         fn(0, *args)
         return
     with child_env():
-        ctx = mp.start_processes(_shifted, args=(fn, args), nprocs=ws - 1, join=False,
-                                 start_method="spawn")
+        ctx = mp.start_processes(_shifted, args=(fn, args, dict(os.environ)), nprocs=ws - 1,
+                                 join=False, start_method=_start_method())
     try:
         fn(0, *args)
     except BaseException:

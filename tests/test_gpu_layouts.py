@@ -88,8 +88,9 @@ def test_layout_matches_reference_zero2(gpu, ws):
     every parameter's chunk split across buckets), one after another in one set of processes."""
     cases = [(_worker, (layout, f"traj_z2_ws{w}_d16_{mode}.npz", buckets, 64))
              for layout, w, mode, buckets in CASES if w == ws]
-    # Layout F in the flat parameter arena (64-element rounds: many rounds, straddling params)
-    cases.append((_worker, ("flat", f"traj_z2_ws{ws}_d16_distinct.npz", "ragged", 64, "flat")))
+    # Layout F in the flat parameter arena (128-element rounds: several rounds, straddling params;
+    # every round is a gloo-staged group per owner here, so not more rounds than that)
+    cases.append((_worker, ("flat", f"traj_z2_ws{ws}_d16_distinct.npz", "ragged", 128, "flat")))
     if ws == 4:
         cases.append((_worker, ("chunk", "traj_z2_ws4_d64_distinct.npz", "ragged", 64)))
     for _, (_, name, *_rest) in cases:

@@ -78,7 +78,7 @@ def _zero12_cases(ws):
                   (ov_worker, (2, "traj_z2_ws4_d16_distinct.npz", True, "flat")),
                   (layout_worker, ("chunk", "traj_z2_ws4_d64_distinct.npz", "ragged", 64))]
     if ws in (2, 8):  # the layout ablation's balanced Layout F in the flat arena (bench.py N > 1)
-        cases += [(layout_worker, ("flat", f"traj_z2_ws{ws}_d16_distinct.npz", "ragged", 64, "flat"))]
+        cases += [(layout_worker, ("flat", f"traj_z2_ws{ws}_d16_distinct.npz", "ragged", 128, "flat"))]
     if ws == 8:
         cases += [(_bf16comm_worker, ("zero2",))]
     return cases
@@ -186,6 +186,12 @@ def test_bench_share_gpu_exchange_check(gpu, zero):
     assert set(checks) == {"flat", "buckets"} and set(out["arena_calibration_ms_per_step"]) == set(checks)
     for kind, c in checks.items():
         assert c["all_ranks_ok"], (kind, c)
+    if zero == 2:  # the balanced Layout F timed beside the reference layout
+        lab = out["layout_ablation"]
+        assert lab["exchange_check"]["all_ranks_ok"] and lab["ms_per_step"] > 0, lab
+        assert lab["exchange_check"]["owned_pieces"] >= 1 and lab["rounds"] >= 1
+        assert set(lab["expected"]) == {"reference_flat_arena", "balanced_F_flat_arena",
+                                        "chunk_Z_bucket_arena"}
 
 
 def test_bench_share_gpu_zero3_paramset(gpu):
@@ -283,5 +289,5 @@ def test_bench_share_gpu_n8_both_arenas(gpu):
 
     argv = ["--gpus", "8", "--share-gpu", "--no-cpu-baseline", "--watchdog-s", "0", "--config", "C4",
             "--set-layers", "4", "--zero", "2", "--arena", "auto", "--steps", "2", "--warmup", "1",
-            "--no-comm-sweep"]
+            "--no-comm-sweep", "--no-layout-ablation"]  # (the ablation leg: the N = 2 test)
     spawn_ranks(_bench_rank, 8, (8, free_port(), argv))
