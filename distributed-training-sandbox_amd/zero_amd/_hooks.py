@@ -11,6 +11,7 @@ its owner is gone is a no-op.
 """
 from __future__ import annotations
 
+import functools
 import weakref
 
 
@@ -50,3 +51,36 @@ class WeakArgCall:
         owner = self._ref()
         if owner is not None:
             getattr(owner, self._name)(*self._args, *call_args)
+
+
+def _first_param_device(obj):
+    """The device of the first parameter a wrapper (or its optimizer) manages, or None."""
+    opt = obj if hasattr(obj, "param_groups") else getattr(obj, "optimizer", None)
+    if opt is None:
+        return None
+    for g in opt.param_groups:
+        for p in g["params"]:
+            return p.device
+    return None
+
+
+def on_param_device(fn):
+    """Run a wrapper's method with the parameters' GPU as the current device.  The library
+    allocates its device tables (hipMalloc), creates its RCCL communicator (ncclCommInitRank) and
+    its HIP events on the *current* device; a caller that keeps its parameters on cuda:k without
+    ``torch.cuda.set_device(k)`` (the reference always sets it, zero1.py:206-207) would otherwise
+    put them on cuda:0.  No device switch when it already is the current one."""
+    import torch
+
+    @functools.wraps(fn)
+    def wrapped(self, *args, **kw):
+        dev = getattr(self, "_param_device", None)
+        if dev is None:
+            src = (args[0] if args else kw.get("optimizer")) if fn.__name__ == "__init__" else self
+            dev = _first_param_device(src) if src is not None else None
+        if dev is None or dev.type != "cuda" or dev.index is None or \
+                dev.index == torch.cuda.current_device():
+            return fn(self, *args, **kw)
+        with torch.cuda.device(dev):
+            return fn(self, *args, **kw)
+    return wrapped

@@ -18,6 +18,7 @@ import torch.distributed as dist
 from torch.optim import Optimizer
 
 from . import checkpoint as ckpt
+from ._hooks import on_param_device
 from .engine import ShardEngine
 from .training_utils.utils import get
 
@@ -40,6 +41,7 @@ class ShardedOptimizerBase:
     _carry = False
     _variant = 2
 
+    @on_param_device
     def __init__(self, optimizer: Optimizer, *, layout: str = "reference",
                  bucket_mb: float | None = None, comm=None, sync: bool = True, buckets: str = "ragged",
                  overlap: bool = False, overlap_bucket_mb: float = 64.0, master: str = "split",
@@ -52,6 +54,7 @@ class ShardedOptimizerBase:
         self.optimizer = optimizer
         self.original_param_groups = optimizer.param_groups
         self.params = [p for group in self.original_param_groups for p in group["params"]]
+        self._param_device = self.params[0].device if self.params else None  # (on_param_device)
         self._group_of = [gi for gi, group in enumerate(self.original_param_groups)
                           for _ in group["params"]]
         # references to the unfiltered groups' hyper-parameter dicts (lr schedulers mutate these)
@@ -189,6 +192,7 @@ class ShardedOptimizerBase:
                 st["step"] = t
 
     # ------------------------------------------------------------------------------------------
+    @on_param_device
     def step(self, closure=None):
         loss = None
         if closure is not None:
@@ -240,6 +244,7 @@ class ShardedOptimizerBase:
         for p in self.params:
             p.grad = None
 
+    @on_param_device
     def zero_grad(self, set_to_none: bool = True):
         if self._flat():
             # ZeRO-2 (and ZeRO-1 at ws = 1, which has no carry): None, as the reference's —
@@ -280,6 +285,7 @@ class ShardedOptimizerBase:
             views["zero1_carry"] = eng.carry[so:so + self.params[i].numel()].view(self.params[i].shape)
         return views
 
+    @on_param_device
     def state_dict(self):
         """The inner optimizer's state dict in torch's format (indices over the owned parameters,
         as the reference's ``opt.optimizer.state_dict()``), every tensor a copy of the engine's
@@ -301,6 +307,7 @@ class ShardedOptimizerBase:
         sd["zero_amd"] = self._ckpt_header()
         return sd
 
+    @on_param_device
     def load_state_dict(self, state_dict):
         """Restore a ``state_dict()`` of this rank (or a plain torch Adam state dict over the same
         owned parameters): hyper-parameters through torch's loader, state copied into the flat

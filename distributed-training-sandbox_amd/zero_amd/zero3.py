@@ -50,7 +50,7 @@ from torch.utils.weak import WeakIdKeyDictionary
 from . import _lib
 from ._lib import ZS_BF16, ZS_BF16_SPLIT, ZS_F32
 from . import checkpoint as ckpt
-from ._hooks import WeakArgCall, WeakCall
+from ._hooks import WeakArgCall, WeakCall, on_param_device
 from ._sharded import adam_group_hparams
 from .comm import STREAM_SYNC, RcclComm, Sync, comm_stream, sync_kind, zs_dtype
 from .engine import ALIGN_ELEMS, probed_zeros
@@ -1467,6 +1467,7 @@ GATHER_WAVE = 1
 class ShardedOptimizer:
     """zero3.py:81-168 with ``update`` selecting reference (no-op) or real ZeRO-3 updates."""
 
+    @on_param_device
     def __init__(self, optimizer: Optimizer, *, update: bool = False, comm=None, sync: bool = True,
                  gather_dtype=None, bucket_mb: float = RS_BUCKET_MB, grad_comm: str | None = None,
                  gather_wave: int = GATHER_WAVE, side_stream: bool = True,
@@ -1476,6 +1477,7 @@ class ShardedOptimizer:
         self.optimizer = optimizer
         self.original_param_groups = optimizer.param_groups
         self.params = [p for group in self.original_param_groups for p in group["params"]]
+        self._param_device = self.params[0].device if self.params else None  # (on_param_device)
         self._group_of = [gi for gi, g in enumerate(self.original_param_groups) for _ in g["params"]]
         self._groups = list(self.original_param_groups)
         world_size = get("ws")
@@ -1753,6 +1755,7 @@ class ShardedOptimizer:
         red.reset()
         return done
 
+    @on_param_device
     def step(self, closure=None):
         loss = None
         if closure is not None:
@@ -1814,6 +1817,7 @@ class ShardedOptimizer:
     def _ckpt_header(self):
         return ckpt.header(3, self.world_size, self.rank, self.local_param_indices, update=self.update)
 
+    @on_param_device
     def state_dict(self):
         """The inner optimizer's state dict in torch's format; update mode: every parameter's
         entry is this rank's dim-0 chunk of its state (copies of the flat state, incl. the split
@@ -1832,6 +1836,7 @@ class ShardedOptimizer:
         sd["zero_amd"] = self._ckpt_header()
         return sd
 
+    @on_param_device
     def load_state_dict(self, state_dict):
         """Restore this rank's ``state_dict()``: hyper-parameters through torch's loader, the
         chunk state copied into the flat buffers.  The parameters themselves (this rank's chunks)

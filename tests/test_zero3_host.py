@@ -245,3 +245,46 @@ def test_tensor_hooks_release_their_managers():
     gc.collect()
     assert ref() is None
     del params
+
+
+def test_on_param_device_switches_to_the_parameters_gpu(monkeypatch):
+    """The optimizers' entry points run with the parameters' GPU current (the library's tables,
+    RCCL communicator and events are created on the current device): a wrapper whose parameters
+    sit on cuda:3 while cuda:0 is current enters torch.cuda.device(cuda:3); no switch when it is
+    already current, none for CPU tensors."""
+    import contextlib
+
+    from zero_amd._hooks import on_param_device
+
+    entered = []
+
+    @contextlib.contextmanager
+    def fake_device(dev):
+        entered.append(dev)
+        yield
+
+    cur = [0]
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: cur[0])
+    monkeypatch.setattr(torch.cuda, "device", fake_device)
+
+    class Opt:
+        @on_param_device
+        def __init__(self, optimizer):
+            self.optimizer = optimizer
+
+        @on_param_device
+        def step(self):
+            return "stepped"
+
+    class FakeParam:
+        device = torch.device("cuda", 3)
+
+    inner = type("Inner", (), {"param_groups": [{"params": [FakeParam()]}]})()
+    o = Opt(inner)
+    assert entered == [torch.device("cuda", 3)]
+    o._param_device = torch.device("cuda", 3)
+    assert o.step() == "stepped" and len(entered) == 2
+    cur[0] = 3
+    assert o.step() == "stepped" and len(entered) == 2  # already current: no switch
+    o._param_device = torch.device("cpu")
+    assert o.step() == "stepped" and len(entered) == 2
