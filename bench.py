@@ -327,6 +327,8 @@ def _phase(name: str) -> None:
 # run that dies says where it was and what it had measured: every thread's Python stack on stderr
 # and, on rank 0, one JSON line with "value": null, the phase and the partial results.
 WATCHDOG_BUDGET_S = 540.0
+_DEADLINE = [None]  # time.monotonic() at which the watchdog fires (None: no watchdog)
+_SKIPPED = {}     # optional legs left out because they would not fit before the watchdog
 _PARTIAL = {}     # what this run has measured so far (dicts are shared: later updates show)
 _OUT_FD = [None]  # a duplicate of the original stdout (fd 1 may be pointed at stderr for a block)
 _EMITTED = [False]
@@ -339,6 +341,25 @@ def watchdog_seconds(requested, now=None) -> float:
         return float(requested)
     elapsed = (time.monotonic() if now is None else now) - _T0
     return max(30.0, WATCHDOG_BUDGET_S - elapsed)
+
+
+def _time_left() -> float:
+    return float("inf") if _DEADLINE[0] is None else _DEADLINE[0] - time.monotonic()
+
+
+def leg_fits(name: str, est_s: float) -> bool:
+    """An optional leg (the other hand-off, the fp32-master step, the layout ablation, the sweep)
+    runs only when twice its estimate plus 30 s fits in what is left before the watchdog: on a slow
+    interconnect the headline line is printed without it rather than lost to the watchdog (the
+    driver's K timed steps are never cut).  A skipped leg is listed in the line's
+    ``skipped_legs``."""
+    left = _time_left()
+    if 2.0 * est_s + 30.0 <= left:
+        return True
+    _SKIPPED[name] = {"estimated_s": round(est_s, 1), "time_left_s": round(left, 1)}
+    log(f"[bench] skipping the {name} leg: ~{est_s:.0f} s estimated, {left:.0f} s left before the "
+        "watchdog")
+    return False
 
 
 def partial_line(failure: str, error=None) -> dict:
@@ -1639,11 +1660,16 @@ def main(argv=None):
         args.warmup = 2 if args.train else 5
     if args.dtype is None:
         args.dtype = "fp32" if (args.zero == 3 and args.config in ("C2", "C3")) else "bf16"
+    _DEADLINE[0] = None
+    _SKIPPED.clear()
     if not _IN_PROCESS[0]:
         _OUT_FD[0] = os.dup(1)
         if env_world is not None and int(env_world) > 1:
             _install_term_handler()
-        _start_watchdog(watchdog_seconds(args.watchdog_s))
+        wd = watchdog_seconds(args.watchdog_s)
+        _start_watchdog(wd)
+        if wd > 0:
+            _DEADLINE[0] = time.monotonic() + wd
     _PARTIAL.clear()
     _EMITTED[0] = False
     _PARTIAL["config"] = {"workload": args.config, "zero": args.zero, "arena_requested": args.arena,
@@ -1943,7 +1969,8 @@ def _main(args):
                  "reduced": getattr(eng, "reduced_placement", None)}
     bucket_mb, n_buckets = opt._bucket_bytes / (1 << 20), eng.K
     other_leg = None
-    if not args.no_default_leg and args.simulate_ws <= 1:
+    if not args.no_default_leg and args.simulate_ws <= 1 and \
+            leg_fits("other hand-off", (args.warmup + min(args.steps, 300)) * ms / 1e3 * 1.2):
         # the same optimizer through the other gradient hand-off, beside the headline's
         other = "views" if handoff_used == "default" else "default"
         _phase(f"{other} hand-off leg")
@@ -1966,7 +1993,8 @@ def _main(args):
         torch.cuda.synchronize()
     fp32_master = None
     if (world == 1 and args.simulate_ws <= 1 and args.dtype == "bf16" and args.master == "split"
-            and not args.no_fp32_master_line):
+            and not args.no_fp32_master_line
+            and leg_fits("fp32-master", 30.0 + (args.warmup + min(args.steps, 300)) * ms / 1e3 * 1.2)):
         # the same step with the exact fp32 master (28 B/elem) beside the split-master headline
         # (26 B/elem, an exact tie stored 1 ulp toward zero: DESIGN §2)
         _phase("fp32-master comparison")
@@ -2005,14 +2033,15 @@ def _main(args):
     collectives = None
     if world > 1:
         collectives = collective_summary(comm_events, args.steps, world, red_dev)
-        if args.comm in ("rccl", "c10d") and not args.no_comm_sweep:
+        if args.comm in ("rccl", "c10d") and not args.no_comm_sweep and leg_fits("bucket-size sweep", 15.0):
             _phase("bucket-size sweep")
             sweep_buf = eng.arena if getattr(eng, "arena", None) is not None else eng.R
             collectives["sweep"] = comm_sweep(opt._comm, sweep_buf, world, red_dev)
 
     layout_ablation = None
     if (world > 1 and args.zero == 2 and args.layout == "reference" and args.simulate_ws <= 1
-            and not args.no_layout_ablation):
+            and not args.no_layout_ablation
+            and leg_fits("layout ablation", 30.0 + (2 + args.warmup + min(args.steps, 50)) * ms / 1e3 * 1.5)):
         # what the reference's whole-parameter ownership costs: the same step with
         # the balanced Layout F in the flat arena — its own exchange check, then timed — after
         # everything of the headline's (its memory is freed first)
@@ -2163,6 +2192,8 @@ def _main(args):
                 shapes, args.cpu_sample, split=args.dtype == "bf16" and args.master == "split")
         if _REHEARSAL[0]:
             out["rehearsal"] = _REHEARSAL[0]
+        if _SKIPPED:
+            out["skipped_legs"] = dict(_SKIPPED)
         print(json.dumps(out), flush=True)
     _teardown(opt)
     dist.destroy_process_group()

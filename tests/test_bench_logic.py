@@ -325,3 +325,18 @@ def test_layout_costs_of_reference_ownership_at_c4_n8():
     assert z["hbm_gb_per_rank"] > r["hbm_gb_per_rank"]  # pack + unpack outweigh the balance
     e = bench._expected_block(c4, 2, "flat", 8, 2, 26, 1024.0, measured_ms=20.0)
     assert e["layouts"] == lc and e["curve"]["8"]["max_rank_adam_gb"] == r["max_rank_adam_gb"]
+
+
+def test_optional_legs_yield_to_the_watchdog(monkeypatch):
+    """On a slow interconnect the optional legs are skipped (and listed) rather than letting the
+    watchdog kill the run before the headline line is printed; without a watchdog they all run."""
+    import time
+
+    monkeypatch.setattr(bench, "_SKIPPED", {})
+    monkeypatch.setattr(bench, "_DEADLINE", [None])
+    assert bench.leg_fits("layout ablation", 1e6) and not bench._SKIPPED
+    monkeypatch.setattr(bench, "_DEADLINE", [time.monotonic() + 200.0])
+    assert bench.leg_fits("bucket-size sweep", 15.0)           # 2 x 15 + 30 <= 200
+    assert not bench.leg_fits("other hand-off", 90.0)           # 2 x 90 + 30 > 200
+    assert set(bench._SKIPPED) == {"other hand-off"}
+    assert bench._SKIPPED["other hand-off"]["estimated_s"] == 90.0
