@@ -22,6 +22,10 @@ What it captures (SURVEY.md §8(c) "Golden vectors to capture"):
 3. ``adam_kat.npz`` — ``torch.optim.Adam`` / ``AdamW`` CPU (single-tensor path, torch 2.10;
    the reference pins 2.4.1 whose non-capturable math is the same, adam.py:457-547)
    known-answer trajectories for several hyper-parameter sets.
+2b. ``c1_z{1,2}_ws2_sampled.npz`` (``make_golden.py c1``) — BASELINE configs[0] at its real
+   width: the reference's 6 × Linear(10000, 10000) model and ShardedOptimizer at ws = 2 on gloo,
+   3 steps of the exact hash gradients of tests/_c1.py; sampled elements and fp64 sums per
+   parameter (tests/_c1.py says why).
 4. ``collective_kat.npz`` — the 2-rank known answers from 02-operations.ipynb:1853-2109
    (rank r holds [0+r, 1+r, 2+r]): all_reduce → [1,3,5], all_gather → [[0,1,2],[1,2,3]].
 
@@ -269,6 +273,87 @@ def make_traj(variant, ws, D, mode):
 
 
 # ----------------------------------------------------------------------------------------------
+# 2b. configs[0] at its real width, sampled (tests/_c1.py)
+# ----------------------------------------------------------------------------------------------
+def _c1_worker(rank, ws, port, variant, tmpdir):
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, str(OUT.parent))
+    import _c1
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(4)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    mod = _load_ref(variant)
+    model = _c1.make_model()
+    params = list(model.parameters())
+    idx = [_c1.sample_idx(i, p.numel()) for i, p in enumerate(params)]
+    rec = {}
+
+    def sample(t, i):
+        return t.detach().reshape(-1)[torch.from_numpy(idx[i])].numpy().copy()
+
+    def sums(t):
+        a = t.detach().reshape(-1).double()
+        return np.array([a.sum().item(), a.abs().sum().item()], np.float64)
+
+    for i, p in enumerate(params):
+        rec[f"idx_{i}"] = idx[i]
+        rec[f"init_{i}"] = sample(p, i)
+        rec[f"initsum_{i}"] = sums(p)
+    opt = mod.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3))
+    rec["local"] = np.array(opt.local_param_indices, np.int64)
+    for t in range(_c1.STEPS):
+        opt.zero_grad()
+        for i, p in enumerate(params):  # what backward's AccumulateGrad does with these grads
+            g = _c1.grad_torch(t, rank, i, p.shape)
+            if p.grad is None:
+                p.grad = g
+            else:
+                p.grad.add_(g)
+        opt.step()
+        for i, p in enumerate(params):
+            rec[f"t{t}_p{i}"] = sample(p, i)
+            rec[f"t{t}_psum{i}"] = sums(p)
+    for i, p in enumerate(params):
+        st = opt.optimizer.state.get(p, {})
+        if st:
+            rec[f"state_{i}_step"] = np.array(float(st["step"]))
+            rec[f"state_{i}_exp_avg"] = sample(st["exp_avg"], i)
+            rec[f"state_{i}_exp_avg_sq"] = sample(st["exp_avg_sq"], i)
+    np.savez(Path(tmpdir) / f"rank{rank}.npz", **rec)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def make_c1(variant):
+    import torch.multiprocessing as mp
+
+    sys.path.insert(0, str(OUT.parent))
+    import _c1
+
+    _PORT[0] += 1
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(_c1_worker, args=(_c1.WS, _PORT[0], variant, td), nprocs=_c1.WS, join=True)
+        merged = {"ws": np.array(_c1.WS), "D": np.array(_c1.D), "steps": np.array(_c1.STEPS)}
+        for r in range(_c1.WS):
+            with np.load(Path(td) / f"rank{r}.npz") as z:
+                for k in z.files:
+                    if k.startswith(("idx_", "init_", "initsum_")):
+                        if r == 0:
+                            merged[k] = z[k]
+                        else:  # every rank built the same model
+                            assert np.array_equal(merged[k], z[k]), k
+                        continue
+                    merged[f"r{r}_{k}"] = z[k]
+    name = f"c1_z{variant}_ws{_c1.WS}_sampled.npz"
+    np.savez_compressed(OUT / name, **merged)
+    print(name, len(merged), "arrays")
+
+
+# ----------------------------------------------------------------------------------------------
 # 3. Adam known answers
 # ----------------------------------------------------------------------------------------------
 ADAM_CASES = {
@@ -331,6 +416,9 @@ def main():
         make_adam_kat()
     if "coll" in which:
         make_collective_kat()
+    if "c1" in which:  # not in the default set: two 600M-parameter ranks, ~20 GB of host memory
+        make_c1(1)
+        make_c1(2)
     if "traj" in which:
         for variant in (1, 2, 3):
             for ws in (1, 2, 3, 4, 8):

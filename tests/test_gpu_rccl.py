@@ -93,6 +93,15 @@ def test_rccl_zero12(gpu, rccl_env, ws):
     _batch(ws, _zero12_cases(ws))
 
 
+def test_rccl_c1_full_width(gpu, rccl_env):
+    """BASELINE configs[0] at its real width (6 × Linear(10000, 10000), 600M fp32 params) at
+    ws = 2 through real RCCL, ZeRO-1 (carry) and ZeRO-2, against the reference's sampled run
+    (tests/_c1.py, test_gpu_parity._c1_worker): 2.4 GB reduced and broadcast per step."""
+    from test_gpu_parity import _c1_worker
+
+    spawn_batch(2, [(_c1_worker, (1,)), (_c1_worker, (2,))], all_spawned=True, deadline_s=300)
+
+
 def _zero3_cases(ws):
     from test_gpu_fp8 import _mr as fp8_worker
     from test_gpu_parity import _bf16comm_worker

@@ -110,6 +110,38 @@ def test_simulate_with_fixture_grads(golden, variant):
                 assert rel(v, z[f"r{r}_state_{i}_exp_avg_sq"]) <= 1e-6
 
 
+@pytest.mark.parametrize("variant", [1, 2])
+def test_simulate_c1_full_width_samples(golden, variant):
+    """BASELINE configs[0] at its real width (6 × Linear(10000, 10000), ws = 2, 3 steps of the
+    exact hash gradients, tests/_c1.py): the restated step run on the fixture's sampled elements
+    alone reproduces the reference's sampled params on both ranks after every step (incl. ZeRO-1's
+    carry) and the owned params' Adam state, within 1e-6 — and the hash gradients themselves are
+    the ones the reference consumed (their sampled values, recomputed here, drive the match)."""
+    import _c1
+
+    z = golden(f"c1_z{variant}_ws2_sampled.npz")
+    ws, steps = int(z["ws"]), int(z["steps"])
+    assert (ws, steps, int(z["D"])) == (_c1.WS, _c1.STEPS, _c1.D)
+    idx = [z[f"idx_{i}"] for i in range(12)]
+    for i, s in enumerate(_c1.shapes()):  # the fixture's sample is the one tests/_c1.py draws
+        assert np.array_equal(idx[i], _c1.sample_idx(i, int(np.prod(s))))
+    init = [z[f"init_{i}"] for i in range(12)]
+    out = zo.simulate(variant, ws, init, steps=steps,
+                      local_grads=lambda t, r, i: _c1.grad_np(t, r, i, idx[i]))
+    for t in range(steps):
+        for r in range(ws):
+            for i in range(12):
+                assert rel(out["params"][t][r][i], z[f"r{r}_t{t}_p{i}"]) <= 1e-6, (t, r, i)
+    for r in range(ws):
+        assert z[f"r{r}_local"].tolist() == list(range(*zo.owner_range(12, ws, r)))
+        for i, (st, m, v, _) in out["state"][r].items():
+            assert int(z[f"r{r}_state_{i}_step"]) == st == steps
+            assert rel(m, z[f"r{r}_state_{i}_exp_avg"]) <= 1e-6
+            assert rel(v, z[f"r{r}_state_{i}_exp_avg_sq"]) <= 1e-6
+    # the update moved every parameter (a fixture of unchanged params would pin nothing)
+    assert all(not np.array_equal(z[f"r0_t{steps - 1}_p{i}"], init[i]) for i in range(12))
+
+
 def test_simulate_zero3_reference_mode(golden):
     """ZeRO-3 reference: params never change (zero3.py:150-153 for-else) and the reduced shards
     are Σ_r chunk_r(grad_r)/ws, bit-compatible within 1e-6 of the reference's all_reduce."""
