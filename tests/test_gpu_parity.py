@@ -361,13 +361,13 @@ def _carry_worker(rank, ws, port, clear):
     sys.stdout.flush()
 
 
-def _c1_worker(rank, ws, port, variant):
+def _c1_worker(rank, ws, port, variants=(1, 2)):
     """BASELINE configs[0] at its real width against the reference (tests/_c1.py): the reference's
-    6 × Linear(10000, 10000) (600,060,000 fp32 params, its own init) through ZeRO-``variant`` at
+    6 × Linear(10000, 10000) (600,060,000 fp32 params, its own init) through ZeRO-1 and ZeRO-2 at
     ws = 2 for 3 steps of the exact hash gradients; every parameter's sampled elements on this
     rank after every step, and the owned parameters' Adam state, within 1e-6 of the reference's
     (tests/golden/c1_z{1,2}_ws2_sampled.npz), and every parameter's fp64 sum within 1e-6 of
-    Σ|p|."""
+    Σ|p|.  The model is built once (on the CPU, as the reference's) for both variants."""
     import sys
     from conftest import PKG, REPO  # noqa: F401
     from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
@@ -377,44 +377,47 @@ def _c1_worker(rank, ws, port, variant):
     torch.cuda.set_device(0)
     init_pg(rank, ws, port)
     dev = torch.device("cuda:0")
-    z = np.load(GOLDEN / f"c1_z{variant}_ws2_sampled.npz")
-    assert int(z["ws"]) == ws
-    idx = [torch.from_numpy(z[f"idx_{i}"]).to(dev) for i in range(12)]
     model = _c1.make_model()  # the reference's init (torch.manual_seed(0), CPU)
-    params = []
-    for i, p in enumerate(model.parameters()):
-        flat = p.detach().reshape(-1)
-        assert np.array_equal(flat[torch.from_numpy(z[f"idx_{i}"])].numpy(), z[f"init_{i}"]), i
-        params.append(torch.nn.Parameter(p.detach().to(dev)))
-    del model, flat, p
-    s0 = params[0].detach().reshape(-1).double().sum().item()
-    assert abs(s0 - z["initsum_0"][0]) <= 1e-9 * z["initsum_0"][1]
+    init = [p.detach() for p in model.parameters()]
+    del model
+    for variant in variants:
+        z = np.load(GOLDEN / f"c1_z{variant}_ws2_sampled.npz")
+        assert int(z["ws"]) == ws
+        idx = [torch.from_numpy(z[f"idx_{i}"]).to(dev) for i in range(12)]
+        for i, p in enumerate(init):
+            assert np.array_equal(p.reshape(-1)[torch.from_numpy(z[f"idx_{i}"])].numpy(),
+                                  z[f"init_{i}"]), i
+        params = [torch.nn.Parameter(p.to(dev)) for p in init]
+        s0 = params[0].detach().reshape(-1).double().sum().item()
+        assert abs(s0 - z["initsum_0"][0]) <= 1e-9 * z["initsum_0"][1]
 
-    def sampled(t, i):
-        return t.detach().reshape(-1)[idx[i]].cpu().numpy()
+        def sampled(t, i):
+            return t.detach().reshape(-1)[idx[i]].cpu().numpy()
 
-    opt = module_for(variant).ShardedOptimizer(torch.optim.Adam(params, lr=1e-3), comm=test_comm())
-    assert opt.local_param_indices == z[f"r{rank}_local"].tolist()
-    for t in range(int(z["steps"])):
-        opt.zero_grad()
+        opt = module_for(variant).ShardedOptimizer(torch.optim.Adam(params, lr=1e-3),
+                                                   comm=test_comm())
+        assert opt.local_param_indices == z[f"r{rank}_local"].tolist()
+        for t in range(int(z["steps"])):
+            opt.zero_grad()
+            for i, p in enumerate(params):
+                set_grad(p, _c1.grad_torch(t, rank, i, p.shape, dev))
+            opt.step()
+            for i, p in enumerate(params):
+                e = rel(sampled(p, i), z[f"r{rank}_t{t}_p{i}"])
+                assert e <= 1e-6, (variant, rank, t, i, e)
+                d = p.detach().reshape(-1).double()
+                s, a = z[f"r{rank}_t{t}_psum{i}"]
+                assert abs(d.sum().item() - s) <= 1e-6 * a, (variant, rank, t, i, d.sum().item(), s)
+                del d
         for i, p in enumerate(params):
-            set_grad(p, _c1.grad_torch(t, rank, i, p.shape, dev))
-        opt.step()
-        for i, p in enumerate(params):
-            e = rel(sampled(p, i), z[f"r{rank}_t{t}_p{i}"])
-            assert e <= 1e-6, (variant, rank, t, i, e)
-            d = p.detach().reshape(-1).double()
-            s, a = z[f"r{rank}_t{t}_psum{i}"]
-            assert abs(d.sum().item() - s) <= 1e-6 * a, (variant, rank, t, i, d.sum().item(), s)
-    for i, p in enumerate(params):
-        key = f"r{rank}_state_{i}_exp_avg"
-        if key in z.files:
-            st = opt.optimizer.state[p]
-            assert int(st["step"].item()) == int(z[f"r{rank}_state_{i}_step"])
-            assert rel(sampled(st["exp_avg"], i), z[key]) <= 1e-6
-            assert rel(sampled(st["exp_avg_sq"], i), z[f"r{rank}_state_{i}_exp_avg_sq"]) <= 1e-6
-    del opt, params
-    torch.cuda.empty_cache()
+            key = f"r{rank}_state_{i}_exp_avg"
+            if key in z.files:
+                st = opt.optimizer.state[p]
+                assert int(st["step"].item()) == int(z[f"r{rank}_state_{i}_step"])
+                assert rel(sampled(st["exp_avg"], i), z[key]) <= 1e-6
+                assert rel(sampled(st["exp_avg_sq"], i), z[f"r{rank}_state_{i}_exp_avg_sq"]) <= 1e-6
+        del opt, params
+        torch.cuda.empty_cache()
     dist.barrier()
     dist.destroy_process_group()
     sys.stdout.flush()

@@ -99,7 +99,7 @@ def test_rccl_c1_full_width(gpu, rccl_env):
     (tests/_c1.py, test_gpu_parity._c1_worker): 2.4 GB reduced and broadcast per step."""
     from test_gpu_parity import _c1_worker
 
-    spawn_batch(2, [(_c1_worker, (1,)), (_c1_worker, (2,))], all_spawned=True, deadline_s=300)
+    spawn_batch(2, [(_c1_worker, ())], all_spawned=True, deadline_s=300)
 
 
 def _zero3_cases(ws):

@@ -29,6 +29,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--single", action="store_true")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--floor", action="store_true",
+                    help="also time the synthetic model alone (full parameters, no ZeRO-3 hooks, no "
+                         "optimizer): zero_grad + forward + backward, the host floor of the iteration")
+    ap.add_argument("--cprofile", type=int, default=0,
+                    help="after the timed block, N more iterations under cProfile (main thread "
+                         "and autograd's: threading.setprofile is not enough, so the profiler is "
+                         "enabled from the hooks' thread too); prints the top functions by own time")
     args = ap.parse_args()
 
     import torch
@@ -117,10 +124,85 @@ def main():
            "backward_wall_ms": bwd[0] / n * 1e3,
            "parts_thread_cpu_ms": {k: round(v / n * 1e3, 4) for k, v in sorted(acc.items())},
            "calls_per_iteration": {k: v / n for k, v in sorted(calls.items())}}
+    if args.cprofile:
+        res["cprofile_top"] = profile_iters(step, args.cprofile)
+    if args.floor:
+        res["model_only"] = model_floor(model, params, x, args.warmup, n)
     print(json.dumps(res, indent=1), flush=True)
     if args.out:
         Path(args.out).write_text(json.dumps(res, indent=1) + "\n")
     dist.destroy_process_group()
+
+
+def profile_iters(step, n):
+    """Own time per function over n iterations, both threads (cProfile per thread, merged)."""
+    import cProfile
+    import pstats
+    import threading
+
+    import torch
+
+    profs = {}
+
+    def enable_here():
+        tid = threading.get_ident()
+        if tid not in profs:
+            profs[tid] = cProfile.Profile()
+            profs[tid].enable()
+
+    # autograd's device thread: enable its profiler from the first hook that runs there
+    from zero_amd import zero3
+    orig = zero3._GatherRuntime.materialize
+
+    def mat(self, *a, **k):
+        enable_here()
+        return orig(self, *a, **k)
+    zero3._GatherRuntime.materialize = mat
+    enable_here()
+    for _ in range(n):
+        step()
+    torch.cuda.synchronize()
+    for p in profs.values():
+        p.disable()
+    zero3._GatherRuntime.materialize = orig
+    st = None
+    for p in profs.values():
+        st = pstats.Stats(p) if st is None else st.add(p)
+    rows = []
+    for (fn, line, name), (cc, nc, tt, ct, _) in st.stats.items():
+        rows.append((tt, ct, nc, f"{Path(fn).name}:{line}:{name}"))
+    rows.sort(reverse=True)
+    return [{"fn": r[3], "own_ms_per_iter": round(r[0] / n * 1e3, 4),
+             "cum_ms_per_iter": round(r[1] / n * 1e3, 4), "calls_per_iter": r[2] / n}
+            for r in rows[:45]]
+
+
+def model_floor(model, shards, x, warmup, n):
+    """The same ParamSetModel over full-size parameters with no hooks and no optimizer."""
+    import torch
+
+    from zero_amd.paramset import ParamSetModel
+
+    full = [torch.nn.Parameter(torch.zeros(tuple(g.shape), device=g.device, dtype=g.dtype))
+            for g in (src for layer in model.layers for src in layer.grads())]
+    del shards
+    m2 = ParamSetModel(full, model.groups)
+    m2.set_grad_source([src for layer in model.layers for src in layer.grads()])
+
+    def it():
+        for p in full:
+            p.grad = None
+        m2(x).sum().backward()
+
+    for _ in range(warmup):
+        it()
+    torch.cuda.synchronize()
+    w0, c0 = time.perf_counter(), time.process_time()
+    for _ in range(n):
+        it()
+    torch.cuda.synchronize()
+    return {"wall_ms": (time.perf_counter() - w0) / n * 1e3,
+            "process_cpu_ms": (time.process_time() - c0) / n * 1e3}
 
 
 if __name__ == "__main__":
