@@ -54,7 +54,8 @@ class ParamLayer(nn.Module):
         return self.grad_source()
 
     def forward(self, x):
-        return _PassThrough.apply(x, self, *(getattr(self, f"p{k}") for k in range(self.n)))
+        # the registered parameters p0 … p{n-1} in order (the dict itself: no per-name lookups)
+        return _PassThrough.apply(x, self, *self._parameters.values())
 
 
 class ParamSetModel(nn.Module):

@@ -179,7 +179,7 @@ def _release_group(ms):
     if ent is not None and ent[0] is ms and ent[1] is not None:
         ent[1].release()
         for m in ms:
-            m.full_data = None
+            m._full = None  # (full_data = None, without the property call)
         return
     for m in ms:
         m.release()
@@ -249,6 +249,7 @@ class _GatherRuntime:
         # installed from its gathered allocation and released to their shards in one C++ call
         self._vplans = {}
         self.use_hostext = True  # (False: per-parameter install / release, for A/B)
+        self._sync_wait = _lib.lib.zs_sync_wait  # (the bound foreign function, looked up once)
 
     def _ready_sync(self, key, cur_h) -> Sync:
         """The sync the consumer stream ``cur_h`` records before ``key``'s gather (one per stream:
@@ -618,8 +619,11 @@ class _GatherRuntime:
             if p is not None:
                 self.pos = p + 1
                 w = p // self.wave
-                self._ensure_wave(w, cur_h)      # (normally launched as the previous prefetch)
-                self._ensure_wave(w + 1, cur_h)  # the next wave, while this one computes
+                launched = self._waves_launched
+                if w not in launched:  # (normally launched as the previous prefetch)
+                    self._ensure_wave(w, cur_h)
+                if w + 1 not in launched:  # the next wave, while this one computes
+                    self._ensure_wave(w + 1, cur_h)
             else:
                 self._prefetch(self.pos, cur_h)
         if key in self.pending:
@@ -632,7 +636,7 @@ class _GatherRuntime:
             return
         if wait_h is not None:
             if self._waited.get(wait_h) != cur_h:  # once per wave and consuming stream
-                rc = _lib.lib.zs_sync_wait(wait_h, cur_h)
+                rc = self._sync_wait(wait_h, cur_h)
                 if rc:
                     _lib.check(rc, "zs_sync_wait")
                 self._waited[wait_h] = cur_h
@@ -1001,8 +1005,10 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
     n_req, param_mods, hooked_params = {}, {}, set()
     trainable_sig = [None]
 
+    managed_params = [mg.param for mg in managed]
+
     def recount():
-        sig = tuple(mg.param.requires_grad for mg in managed)
+        sig = tuple([p.requires_grad for p in managed_params])
         if sig == trainable_sig[0]:
             return
         trainable_sig[0] = sig
@@ -1310,9 +1316,10 @@ class _GradReducer:
         if opt._G.dtype != opt.params[0].dtype:  # a bf16 exchange's chunks stay internal
             return
         shapes, views = opt._arena.shard_shapes, self._shard_grad
-        for i in np.nonzero(self.had_grad)[0].tolist():
-            p = opt.params[i]
-            if p.data.shape == shapes[i]:
+        params = opt.params
+        for i in np.flatnonzero(self.had_grad).tolist():
+            p = params[i]
+            if p.shape == shapes[i]:  # (released to its shard; p.shape: no .data tensor built)
                 v = views[i]
                 if v is None:
                     s, n = int(opt._arena.slot[i]), int(opt._arena.ln[i])
@@ -1387,33 +1394,33 @@ class _GradReducer:
                         send[:N].copy_(flat)
             sends.append((i, send))
         single = opt.runtime.stream is None
-        tab = self._rs_table(k) if hasattr(opt.comm, "reduce_scatter_group") else None
-        if single and tab is not None and tab[5] is not None and self.timing is None:
-            # single-stream mode: the bucket's RCCL group on the stream that produced the grads
+        tab = self._rs_tables.get(k) or (self._rs_table(k) if hasattr(opt.comm, "reduce_scatter_group")
+                                         else None)
+        if tab is not None and tab[5] is not None and self.timing is None:
             recv, count, dt, sp, raw, ordered = tab
             for j, (_, t) in enumerate(sends):
                 sp[j] = t.data_ptr()
-            ordered(cur_h, 0, cur_h, 0)
-            for i, _ in sends:
-                opt.params[i].grad = None
+            params = opt.params
+            if single:
+                # single-stream mode: the bucket's RCCL group on the stream that produced the grads
+                ordered(cur_h, 0, cur_h, 0)
+                for i, _ in sends:
+                    params[i].grad = None
+                return
+            # ONE library call: ready sync on the stream that produced the grads, the side
+            # stream's wait, the bucket's RCCL group of reduce-scatters, the done sync; only the
+            # last bucket's done is waited on (step(), the shard grads): the side stream runs the
+            # buckets in order, so the others need no record
+            ordered(cur_h, self._ready_sync(k, cur_h).h, self._cs_h,
+                    self._done_h[k] if k == self.K - 1 else 0)
+            cs = opt.runtime.stream
+            for i, send in sends:
+                send.record_stream(cs)
+                params[i].grad = None
             return
         if cur is None:
             cur = torch.cuda.current_stream(dev)
         cs = cur if single else opt.runtime.stream
-        if tab is not None and tab[5] is not None and self.timing is None:
-            # ONE library call: ready sync on the stream that produced the grads, the side
-            # stream's wait, the bucket's RCCL group of reduce-scatters, the done sync
-            recv, count, dt, sp, raw, ordered = tab
-            for j, (_, t) in enumerate(sends):
-                sp[j] = t.data_ptr()
-            # only the last bucket's done is waited on (step(), the shard grads): the side stream
-            # runs the buckets in order, so the others need no record
-            ordered(cur_h, self._ready_sync(k, cur_h).h, self._cs_h,
-                    self._done_h[k] if k == self.K - 1 else 0)
-            for i, send in sends:
-                send.record_stream(cs)
-                opt.params[i].grad = None
-            return
         cs_h = cs.cuda_stream
         ready = self._ready_sync(k, cur_h)
         ready.record(cur_h)

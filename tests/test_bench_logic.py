@@ -1,5 +1,6 @@
 """bench.py's host-side logic on the CPU: the exchange check's bit checksums (chunked, so a large
 arena needs no full-size int64 temporaries) and the xGMI denominators of the busBW fractions."""
+import pytest
 import numpy as np
 import torch
 
@@ -194,7 +195,7 @@ def test_default_watchdog_fires_inside_the_drivers_limit():
     process start (the first import torch on a fresh box is part of the driver's clock)."""
     assert bench.WATCHDOG_BUDGET_S <= 540.0
     assert bench.watchdog_seconds(None, now=bench._T0) == bench.WATCHDOG_BUDGET_S < 600.0
-    assert bench.watchdog_seconds(None, now=bench._T0 + 120.0) == bench.WATCHDOG_BUDGET_S - 120.0
+    assert bench.watchdog_seconds(None, now=bench._T0 + 120.0) == pytest.approx(bench.WATCHDOG_BUDGET_S - 120.0)
     assert bench.watchdog_seconds(None, now=bench._T0 + 1e4) == 30.0  # (late start: still fires)
     assert bench.watchdog_seconds(250.0) == 250.0 and bench.watchdog_seconds(0) == 0.0
 

@@ -76,10 +76,19 @@ def test_install_refuses_a_short_or_foreign_allocation():
 def test_release_group_uses_the_module_plan_or_falls_back():
     from zero_amd import zero3
 
-    class M:  # the manager surface _release_group touches
+    class M:  # the manager surface _release_group touches (full_data stored as _full, as
+        # Zero3ParamManager's property does: the plan path clears _full directly)
         def __init__(self, p, rt):
-            self.param, self.shard, self.runtime, self.full_data = p, p.data, rt, None
+            self.param, self.shard, self.runtime, self._full = p, p.data, rt, None
             self.released = 0
+
+        @property
+        def full_data(self):
+            return self._full
+
+        @full_data.setter
+        def full_data(self, v):
+            self._full = v
 
         def release(self):
             self.released += 1

@@ -13,7 +13,8 @@ Usage: python tools/z3_host_ab.py [--config C5] [--ws 8] [--iters 20] [--blocks 
        post-accumulate hooks instead of the C++ gradient counters, round 6)
 The baseline module is ``git show <rev>:distributed-training-sandbox_amd/zero_amd/zero3.py`` (r02:
 1653aab, r03: 3d19026 — the runtimes profiles/r03_z3_host_ab*.json and r04_z3_host_ab.json compare),
-written to tools/.baselines/ (git-ignored, so it travels to the GPU box, which has no git history):
+written to tools/_baselines/ (git-ignored, but not gpurun-ignored, so it travels to the GPU box,
+which has no git history; delete it after the A/B):
 run ``python tools/z3_host_ab.py --baseline r03 --extract-only`` here before the gpurun call.
 """
 from __future__ import annotations
@@ -29,15 +30,15 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO / "distributed-training-sandbox_amd"))
 sys.path.insert(0, str(REPO))
-BASELINE_REVS = {"r02": "1653aab", "r03": "3d19026"}
+BASELINE_REVS = {"r02": "1653aab", "r03": "3d19026", "r06a": "994a673"}
 ZERO3_PATH = "distributed-training-sandbox_amd/zero_amd/zero3.py"
 
 
 def baseline_file(tag: str) -> Path:
-    """tools/.baselines/_zero3_<tag>.py, extracted from git history when it is not there yet."""
+    """tools/_baselines/_zero3_<tag>.py, extracted from git history when it is not there yet."""
     import subprocess
 
-    out = REPO / "tools" / ".baselines" / f"_zero3_{tag}.py"
+    out = REPO / "tools" / "_baselines" / f"_zero3_{tag}.py"
     if not out.exists():
         src = subprocess.run(["git", "-C", str(REPO), "show", f"{BASELINE_REVS[tag]}:{ZERO3_PATH}"],
                              check=True, capture_output=True, text=True).stdout
@@ -56,7 +57,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--baseline", default="none", choices=["none"] + sorted(BASELINE_REVS))
     ap.add_argument("--extract-only", action="store_true",
-                    help="write the baseline module under tools/.baselines/ and exit (no GPU)")
+                    help="write the baseline module under tools/_baselines/ and exit (no GPU)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--events", action="store_true",
                     help="also time the current runtime with stream_sync='event'")
