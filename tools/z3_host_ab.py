@@ -83,7 +83,7 @@ def main():
     from zero_amd.paramset import ParamSetModel, decoder_layer_groups
     from zero_amd.shapes import CONFIGS
 
-    base = {"r02": "round2", "r03": "round3"}.get(args.baseline)
+    base = {"r02": "round2", "r03": "round3"}.get(args.baseline, args.baseline)
     z3_old = None
     if path is not None:
         spec = importlib.util.spec_from_file_location(f"zero_amd._zero3_{args.baseline}", path)
