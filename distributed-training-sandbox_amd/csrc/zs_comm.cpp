@@ -47,6 +47,10 @@ int& zs::sync_host_flags() {  // (zs_tune "sync_host_flags"; zs_common.h)
   return mode;
 }
 
+namespace zs {
+hipError_t flag_write(uint64_t* flag, uint64_t value, hipStream_t st);  // zs_kernels.hip
+}
+
 extern "C" {
 
 int zs_comm_unique_id(void* out128) {
@@ -457,7 +461,10 @@ int zs_sync_record(zs_sync* s, uintptr_t stream) {
     // another stream than the last record's: order this write after that one's, or the word
     // could go back from epoch + 1 to epoch when the two streams run in the other order
     if (s->epoch > 0 && st != s->last_stream) ZS_HIP(flag_wait(s, st, s->epoch));
-    ZS_HIP(hipStreamWriteValue64(st, s->flag, s->epoch + 1, 0));
+    if (zs::sync_write_kernel())
+      ZS_HIP(zs::flag_write(s->flag, s->epoch + 1, st));
+    else
+      ZS_HIP(hipStreamWriteValue64(st, s->flag, s->epoch + 1, 0));
     ++s->epoch;
     s->last_stream = st;
   }

@@ -15,6 +15,10 @@ void set_error(const char* fmt, ...);
 // (the fallback when pinned memory is refused; zs_comm.cpp)
 int& sync_host_flags();
 
+// zs_tune("sync_write_kernel"): 1 (default) = a flag record is flag_write_kernel (zs_kernels.hip),
+// 0 = hipStreamWriteValue64; flag_write enqueues the former (declared where hip types are known)
+int& sync_write_kernel();
+
 inline int fail(int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;

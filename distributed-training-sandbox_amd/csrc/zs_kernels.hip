@@ -1745,6 +1745,33 @@ int zs_adamset_stats(const zs_adamset* as, int64_t* elems, int64_t* bytes) {
   return ZS_OK;
 }
 
+}  // extern "C"
+
+// A stream-flag record (zs_comm.cpp zs_sync_record): one wave whose lane 0 stores the epoch with a
+// system-scope release (a vector store: global_store … sc0 sc1).  In stream order like any launch
+// (the dispatch waits for the stream's earlier work, whose writes its end-of-kernel release made
+// visible), so the word reaches `value` only after everything recorded before it — what
+// hipStreamWriteValue64 does, without the runtime's stream-operation command: on this stack that
+// command costs a HIP runtime thread ~20 us of CPU per record (profiles/r06_z3_thr_*.json: 1.5 ms
+// of the simulated ws = 8 C5 iteration's 102 records), a kernel launch does not.
+__global__ __launch_bounds__(64) void flag_write_kernel(uint64_t* flag, uint64_t value) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+namespace zs {
+int& sync_write_kernel() {  // zs_tune("sync_write_kernel"): 1 = flag_write_kernel, 0 = hipStreamWriteValue64
+  static int v = 1;
+  return v;
+}
+
+hipError_t flag_write(uint64_t* flag, uint64_t value, hipStream_t st) {
+  hipLaunchKernelGGL(flag_write_kernel, dim3(1), dim3(64), 0, st, flag, value);
+  return hipGetLastError();
+}
+}  // namespace zs
+
+extern "C" {
+
 int zs_tune(const char* key, int64_t value, int64_t* previous) {
   ZS_REQUIRE(key != nullptr, "zs_tune: key is NULL");
   int* slot = nullptr;
@@ -1772,6 +1799,9 @@ int zs_tune(const char* key, int64_t value, int64_t* previous) {
     ok = value >= 0 && value <= 1024;
   } else if (std::strcmp(key, "sync_host_flags") == 0) {
     slot = &zs::sync_host_flags();
+    ok = value == 0 || value == 1;
+  } else if (std::strcmp(key, "sync_write_kernel") == 0) {
+    slot = &zs::sync_write_kernel();
     ok = value == 0 || value == 1;
   } else {
     return zs::fail(ZS_ERR_INVALID, "zs_tune: unknown key '%s'", key);

@@ -12,8 +12,19 @@ pytestmark = pytest.mark.gpu
 SLEEP_CYCLES = 50_000_000  # ~20 ms of a spinning kernel: the producer is far behind the host
 
 
+@pytest.fixture(params=["store_kernel", "write_value"])
+def flag_record(request):
+    """How a flag sync's record writes its word: the library's one-wave store kernel (default,
+    round 6) or hipStreamWriteValue64 (zs_tune sync_write_kernel 0); both must order alike."""
+    from zero_amd import _lib
+
+    _lib.call("zs_tune", b"sync_write_kernel", int(request.param == "store_kernel"), None)
+    yield request.param
+    _lib.call("zs_tune", b"sync_write_kernel", 1, None)
+
+
 @pytest.mark.parametrize("kind", ["flag", "event"])
-def test_sync_orders_consumer_after_producer(gpu, kind):
+def test_sync_orders_consumer_after_producer(gpu, kind, flag_record):
     from zero_amd.comm import StreamEvent
 
     prod, cons = torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)
@@ -65,7 +76,7 @@ def test_unrecorded_sync_waits_for_nothing(gpu):
 
 
 @pytest.mark.parametrize("kind", ["flag", "event"])
-def test_wait_after_producer_finished(gpu, kind):
+def test_wait_after_producer_finished(gpu, kind, flag_record):
     """The producer's record has executed before the wait is asked for: the flag wait is then
     skipped on the host (the word already holds the epoch) and the consumer still sees the data."""
     from zero_amd.comm import StreamEvent
@@ -87,7 +98,7 @@ def test_wait_after_producer_finished(gpu, kind):
 
 
 @pytest.mark.parametrize("busy", [True, False])
-def test_synced_prologue_orders_after_stream(gpu, busy):
+def test_synced_prologue_orders_after_stream(gpu, busy, flag_record):
     """zs_all_gather_group_synced with no collective (n = 0): `stream` runs after everything
     enqueued on after_stream, busy or already idle, and `done` orders a third stream after
     `stream`."""
@@ -122,7 +133,7 @@ def test_synced_prologue_orders_after_stream(gpu, busy):
 
 
 @pytest.mark.parametrize("kind", ["flag", "event"])
-def test_device_flag_words_order_streams(gpu, kind):
+def test_device_flag_words_order_streams(gpu, kind, flag_record):
     """The fallback flag words in device memory (zs_tune("sync_host_flags", 0): every wait
     enqueued, none skipped on the host) order streams as the pinned host words do."""
     from zero_amd import _lib
@@ -164,7 +175,7 @@ def _flag_syncs(host_words: bool, n: int):
 
 
 @pytest.mark.parametrize("host_words", [True, False], ids=["host_word", "device_word"])
-def test_flag_epochs_cross_2_pow_32(gpu, host_words):
+def test_flag_epochs_cross_2_pow_32(gpu, host_words, flag_record):
     """a flag sync seeded at epoch 2^32 - 3 orders a slow producer before its
     consumer on every record across 2^32 (ABI v13: 64-bit words; v12's 32-bit epoch wrapped there,
     the GPU's unsigned >= was then satisfied by the stale pre-wrap word and the host skipped the
@@ -193,7 +204,7 @@ def test_flag_epochs_cross_2_pow_32(gpu, host_words):
 
 
 @pytest.mark.parametrize("host_words", [True, False], ids=["host_word", "device_word"])
-def test_flag_record_from_two_streams_keeps_epochs_in_order(gpu, host_words):
+def test_flag_record_from_two_streams_keeps_epochs_in_order(gpu, host_words, flag_record):
     """a record from a second stream while the first stream's record is still pending.
     The second write waits for the first, so the word ends at the latest epoch (v12 let the slow
     first write land last and move the word back, so a later wait for the latest epoch could never

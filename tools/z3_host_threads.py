@@ -42,6 +42,16 @@ def main():
                     help="DIAGNOSTIC: the ordered library calls and the consumer's stream wait "
                          "become no-ops (no HIP event record / wait at all): how much of the "
                          "runtime threads' CPU the stream ordering costs")
+    ap.add_argument("--device-flags", action="store_true",
+                    help="stream-flag words in device memory (zs_tune sync_host_flags 0: every wait "
+                         "enqueued) instead of pinned host memory")
+    ap.add_argument("--no-record-stream", action="store_true",
+                    help="DIAGNOSTIC (unsafe: blocks may be reused while another stream reads them; "
+                         "the simulated iteration checks no data): Tensor.record_stream a no-op — "
+                         "how much CPU the caching allocator's cross-stream events cost")
+    ap.add_argument("--write-value", action="store_true",
+                    help="flag records through hipStreamWriteValue64 (zs_tune sync_write_kernel 0) "
+                         "instead of the library's one-wave store kernel")
     args = ap.parse_args()
 
     import psutil
@@ -70,6 +80,16 @@ def main():
     zero3.get = lambda what, dm=None: {"ws": ws, "rank": 0}.get(what) if what in ("ws", "rank") \
         else real_get(what, dm)
     comm = bench._NoComm(ws)
+    if args.no_record_stream:
+        torch.Tensor.record_stream = lambda self, stream: None
+    if args.write_value:
+        from zero_amd import _lib
+
+        _lib.call("zs_tune", b"sync_write_kernel", 0, None)
+    if args.device_flags:
+        from zero_amd import _lib
+
+        _lib.call("zs_tune", b"sync_host_flags", 0, None)
     if args.no_events:
         from zero_amd import _lib
 
@@ -140,6 +160,8 @@ def main():
     summ = {"config": args.config, "simulated_ws": ws, "iters_per_block": args.iters,
             "no_events": args.no_events, "side_stream": not args.single, "gather_wave": opt.runtime.wave,
             "stream_sync": "flag" if opt.runtime.sync_kind == 1 else "event",
+            "device_flags": args.device_flags, "no_record_stream": args.no_record_stream,
+            "flag_record": "hipStreamWriteValue64" if args.write_value else "store kernel",
             "bucket_mb": args.bucket_mb,
             "autograd_thread_is_main": bool(bwd_tid and bwd_tid <= {main_tid}),
             "median": {k: med(k) for k in ("wall_ms", "cpu_ms", "main_thread_ms",
