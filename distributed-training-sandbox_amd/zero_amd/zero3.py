@@ -40,7 +40,7 @@ import contextlib
 import os
 import time
 import weakref
-from collections import OrderedDict
+from collections import OrderedDict, deque
 
 import numpy as np
 import torch
@@ -67,6 +67,16 @@ if os.environ.get("ZERO_AMD_HOSTEXT", "1") == "0":  # A/B switch (tools/z3_host_
 # hooks when the extension has them; False: one Python post-accumulate hook per parameter and
 # counter (read when hooks are registered; tools/z3_host_ab.py --no-counting)
 HOSTEXT_COUNTING = True
+# Side-stream gathers: at most this many gathered allocations the GPU has not released yet.  Each
+# module's allocation is made on the side stream and its consumer's use recorded on it, so the
+# caching allocator reuses a block only once the consumer stream has passed its release; a host
+# that runs ahead of the GPU (a GPU-bound iteration) kept allocating new blocks, ~68 per C5
+# iteration, until hipMalloc failed and the allocator synchronised the device and freed its cache
+# — single host iterations of 1.4-5 s (profiles/r06_z3_thr_stall.json, stacks in torch.empty of
+# _side_empty).  The runtime records a release marker on the consumer stream every
+# GATHER_INFLIGHT // 2 releases, and before a new allocation waits on the host for the oldest
+# marker while GATHER_INFLIGHT allocations are outstanding (FSDP's all-gather rate limit).
+GATHER_INFLIGHT = int(os.environ.get("ZERO_AMD_GATHER_INFLIGHT", "8"))
 
 
 def _chunk_geom(d0: int, ws: int, rank: int):
@@ -180,9 +190,13 @@ def _release_group(ms):
         ent[1].release()
         for m in ms:
             m._full = None  # (full_data = None, without the property call)
+        if getattr(rt, "_throttled", False):
+            rt.note_release()
         return
     for m in ms:
         m.release()
+    if getattr(rt, "_throttled", False):
+        rt.note_release()
 
 
 class _GatherRuntime:
@@ -250,6 +264,59 @@ class _GatherRuntime:
         self._vplans = {}
         self.use_hostext = True  # (False: per-parameter install / release, for A/B)
         self._sync_wait = _lib.lib.zs_sync_wait  # (the bound foreign function, looked up once)
+        # the gather rate limit (GATHER_INFLIGHT): on for an optimizer's side-stream runtime, whose
+        # allocations are released through _release_group
+        self._throttled = False
+        self.max_inflight = max(2, GATHER_INFLIGHT)
+        self._marker_every = max(1, self.max_inflight // 2)
+        self._outstanding = 0       # gathered allocations not known to be released on the GPU
+        self._markers = deque()     # (flag sync, epoch, releases it covers), oldest first
+        self._rel_syncs = {}        # consumer stream handle -> [flag sync, its latest epoch]
+        self._rel_n = 0             # releases since the last marker
+        self._counted = set()       # pending keys counted in _outstanding
+        self.n_throttle_waits = 0
+
+    # -- the gather rate limit (GATHER_INFLIGHT) ------------------------------------------------
+    def note_release(self):
+        """A module's gathered parameters were released (on the current stream): every
+        ``_marker_every`` releases one marker recorded there."""
+        self._rel_n += 1
+        if self._rel_n >= self._marker_every:
+            self._record_marker()
+
+    def _record_marker(self):
+        if not self._rel_n:
+            return
+        h = self._cur_h()
+        ent = self._rel_syncs.get(h)
+        if ent is None:  # a flag sync of its own per consumer stream: its epochs only grow
+            ent = self._rel_syncs[h] = [Sync(_lib.ZS_SYNC_FLAG), 0]
+        ent[0].record(h)
+        ent[1] += 1
+        self._markers.append((ent[0], ent[1], self._rel_n))
+        self._rel_n = 0
+
+    def _throttle(self, key, k: int = 1):
+        """Before ``k`` new gathered allocations: while that would exceed ``max_inflight``
+        outstanding, wait on the host for the oldest release marker (everything before a marker on
+        its stream is enqueued already, so it completes without anything this host still has to
+        enqueue).  No marker left: go ahead (nothing to wait for)."""
+        while self._outstanding + k > self.max_inflight and self._markers:
+            sy, e, n = self._markers.popleft()
+            if sy.query()[1] < e:
+                self.n_throttle_waits += 1
+                while sy.query()[1] < e:
+                    time.sleep(20e-6)
+            self._outstanding -= n
+        self._outstanding += k
+        self._counted.add(key)
+
+    def _drop_pending(self):
+        """Gathers prefetched but never consumed are dropped (their memory goes back once the side
+        stream is past them): no longer outstanding."""
+        self._outstanding -= len(self._counted.intersection(self.pending))
+        self._counted.clear()
+        self.pending.clear()
 
     def _ready_sync(self, key, cur_h) -> Sync:
         """The sync the consumer stream ``cur_h`` records before ``key``'s gather (one per stream:
@@ -315,6 +382,8 @@ class _GatherRuntime:
         self._waited.pop(ev_h, None)  # re-recorded below: no consumer has waited on this record
         timed = self.gather_events is not None and self.ws > 1
         plan = self._tables[key] if key in self._tables else self._table(key, managers)
+        if self._throttled:
+            self._throttle(key)
         if plan is not None and plan[-1] is not None and not timed and self.stream is None:
             # single-stream mode: the RCCL group on the consumer's stream, nothing to order
             send, count, offs, total, dt, es, views, recv, raw, ordered = plan
@@ -582,6 +651,8 @@ class _GatherRuntime:
             if single:
                 hold = torch.empty(total, dtype=ms[0].shard.dtype, device=self.device)
             else:  # written by the side stream: allocated there (see _take_ready)
+                if self._throttled:
+                    self._throttle(k)
                 hold = self._side_empty(total, ms[0].shard.dtype)
             np.add(offs, np.uint64(hold.data_ptr()), out=recv)
             ordered(cur_h, ready_h if j == 0 else 0, side_h, done_h if j == last else 0)
@@ -630,6 +701,7 @@ class _GatherRuntime:
             self.n_prefetch_hits += 1
         self.launch(key, managers, cur_h)
         out, ev, hold, alloc_h, wait_h = self.pending.pop(key)
+        self._counted.discard(key)
         if ev is None and hold is None:  # ws == 1
             for m, full in out:
                 m._install_full(full)
@@ -670,7 +742,7 @@ class _GatherRuntime:
         and gathers prefetched before the change — they read the old shards — are dropped, so
         their modules gather again on demand."""
         self._inputs_dirty = True
-        self.pending.clear()
+        self._drop_pending()
 
     def end_iteration(self):
         for fn in self.iteration_callbacks:
@@ -678,7 +750,10 @@ class _GatherRuntime:
         self._inputs_dirty = True  # step() has updated the shards
         if self.sequence:
             self.recording = False
-        self.pending.clear()
+        self._drop_pending()
+        if self._throttled:  # every consumed allocation is released by now: the markers cover them
+            self._record_marker()
+            self._outstanding = sum(n for _, _, n in self._markers)
         self._waves_launched.clear()
         self._waited.clear()
         self.pos = 0
@@ -1520,6 +1595,8 @@ class ShardedOptimizer:
         self.runtime = _GatherRuntime(world_size, rank, comm, dev, wave=gather_wave,
                                       stream_sync=stream_sync,
                                       side_stream=side_stream)
+        # the gather rate limit: the hooks release every module through _release_group
+        self.runtime._throttled = self.runtime.stream is not None and world_size > 1
         # zero3.py:104-110: every param becomes its dim-0 chunk — here a view of the chunk arena
         # (the full tensor is released); one manager per param
         self._arena = _ChunkArena(self.params, world_size, rank)

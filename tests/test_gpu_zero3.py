@@ -495,3 +495,67 @@ def test_c5_paramset_step_rank0_of_ws8(gpu, monkeypatch, ws):
             assert np.array_equal(opt._lo[s:s + n][idx].cpu().numpy().view(np.uint16), lo), i
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("throttled", [True, False])
+def test_gather_rate_limit_bounds_allocations_when_the_host_runs_ahead(gpu, monkeypatch, throttled):
+    """Side-stream gathers of a GPU-bound iteration (a sleep kernel per module: the host runs far
+    ahead): with the rate limit the gathered allocations the GPU has not released stay within
+    GATHER_INFLIGHT + one marker's worth (+ the module in use and its prefetch) — the reserved
+    memory grows by no more than that many allocations — and the host waited; without it (the round-5 code path) they pile up with the host's lead — what ended in
+    hipMalloc failing and the allocator synchronising the device (profiles/r06_z3_thr_stall.json).
+    Rank 0 of a simulated ws = 8 job (bench._NoComm: the product's one-call synced gathers with
+    the collective left out)."""
+    import bench
+    import zero_amd.zero3 as z3
+    from zero_amd.paramset import ParamSetModel
+
+    ws, n_layers, D = 8, 12, 4096
+    init_pg(0, 1, _port())
+    real_get = z3.get
+    monkeypatch.setattr(z3, "get", lambda what, dm=None: {"ws": ws, "rank": 0}[what]
+                        if what in ("ws", "rank") else real_get(what, dm))
+    try:
+        params = [torch.nn.Parameter(torch.randn(D, D, device=gpu).to(torch.bfloat16))
+                  for _ in range(n_layers)]
+        grads = [torch.randn(D, D, device=gpu).to(torch.bfloat16) * 1e-3 for _ in range(n_layers)]
+        model = ParamSetModel(params, [[i] for i in range(n_layers)])
+        model.set_grad_source(grads)
+        for layer in model.layers:  # ~0.5 ms of GPU per module and pass: the GPU is the bottleneck
+            layer.register_forward_pre_hook(lambda m, a: torch.cuda._sleep(1_000_000))
+        opt = z3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
+                                  comm=bench._NoComm(ws), sync=False)
+        rt = opt.runtime
+        assert rt._throttled and rt.stream is not None
+        rt._throttled = throttled
+        z3.register_zero3_hooks(model, opt.param_managers)
+        x = torch.zeros(1, device=gpu, requires_grad=True)
+        hold_bytes = D * D * 2
+
+        def it():
+            opt.zero_grad()
+            model(x).sum().backward()
+            opt.step()
+
+        for _ in range(2):
+            it()
+        torch.cuda.synchronize()
+        # a freed block whose consumer stream has not passed its release is not reusable, so the
+        # allocator reserves new memory for the next gathers: the reserved high-water mark counts
+        # them (allocated bytes drop at the host-side free)
+        base = torch.cuda.memory_reserved()
+        torch.cuda.reset_peak_memory_stats()
+        for _ in range(12):
+            it()
+        grown = torch.cuda.max_memory_reserved() - base
+        torch.cuda.synchronize()
+        held = grown / hold_bytes
+        bound = rt.max_inflight + rt._marker_every + 2
+        if throttled:
+            assert held <= bound, (held, bound)
+            assert rt.n_throttle_waits > 0
+            assert 0 <= rt._outstanding <= rt.max_inflight + rt._marker_every
+        else:
+            assert held > bound, (held, bound)  # (the case the limit exists for)
+    finally:
+        dist.destroy_process_group()

@@ -96,7 +96,7 @@ def test_release_group_uses_the_module_plan_or_falls_back():
             self.full_data = None
 
     class RT:
-        pass
+        _throttled = False  # (the runtime's gather rate limit: not exercised here)
 
     ext = _ext()
     vp, params, shards, _, total = _plan(ext)

@@ -52,7 +52,15 @@ def main():
     ap.add_argument("--write-value", action="store_true",
                     help="flag records through hipStreamWriteValue64 (zs_tune sync_write_kernel 0) "
                          "instead of the library's one-wave store kernel")
+    ap.add_argument("--alternate-write", action="store_true",
+                    help="interleaved A/B in one process: even blocks record flags with the store "
+                         "kernel, odd blocks with hipStreamWriteValue64")
+    ap.add_argument("--stall-ms", type=float, default=0.0,
+                    help="per-iteration host times; an iteration longer than this dumps every "
+                         "thread's Python stack to stderr (first 4 only)")
     args = ap.parse_args()
+
+    import faulthandler
 
     import psutil
     import torch
@@ -130,12 +138,27 @@ def main():
         return {t.id: t.user_time + t.system_time for t in proc.threads()}
 
     rows = []
+    dumps = [0]
+    from zero_amd import _lib as zlib
     for b in range(args.blocks):
+        if args.alternate_write:
+            zlib.call("zs_tune", b"sync_write_kernel", 1 - b % 2, None)
         torch.cuda.synchronize()
         s0, w0, c0 = snap(), time.perf_counter(), time.process_time()
+        its = []
         for _ in range(args.iters):
+            t0 = time.perf_counter()
+            if args.stall_ms and dumps[0] < 4:
+                faulthandler.dump_traceback_later(args.stall_ms / 1e3, exit=False)
             step()
+            if args.stall_ms and dumps[0] < 4:
+                faulthandler.cancel_dump_traceback_later()
+            its.append((time.perf_counter() - t0) * 1e3)
+            if args.stall_ms and its[-1] > args.stall_ms:
+                dumps[0] += 1
+        t_sync = time.perf_counter()
         torch.cuda.synchronize()
+        sync_ms = (time.perf_counter() - t_sync) * 1e3
         w, c, s1 = time.perf_counter() - w0, time.process_time() - c0, snap()
         d = {tid: s1[tid] - s0.get(tid, 0.0) for tid in s1}
         n = args.iters
@@ -150,11 +173,15 @@ def main():
                 names[t] = Path(f"/proc/self/task/{t}/comm").read_text().strip()
             except OSError:
                 names[t] = "?"
-        rows.append({"block": b, "wall_ms": round(w / n * 1e3, 3), "cpu_ms": round(c / n * 1e3, 3),
+        rows.append({"block": b, **({"flag_record": ("store kernel", "hipStreamWriteValue64")[b % 2]}
+                                    if args.alternate_write else {}), "wall_ms": round(w / n * 1e3, 3), "cpu_ms": round(c / n * 1e3, 3),
                      "main_thread_ms": round(main / n * 1e3, 3),
                      "autograd_thread_ms": round(bwd / n * 1e3, 3),
                      "other_threads_ms": round(other / n * 1e3, 3),
-                     "busiest_other_threads_ms": {f"{names.get(t, '?')}[{t}]": v for v, t in busy}})
+                     "busiest_other_threads_ms": {f"{names.get(t, '?')}[{t}]": v for v, t in busy},
+                     "host_iter_ms_max": round(max(its), 2),
+                     "host_iter_ms_median": round(sorted(its)[len(its) // 2], 3),
+                     "host_iters_over_20ms": sum(1 for v in its if v > 20), "final_sync_ms": round(sync_ms, 2)})
         print(json.dumps(rows[-1]), flush=True)
     med = lambda k: sorted(r[k] for r in rows)[len(rows) // 2]  # noqa: E731
     summ = {"config": args.config, "simulated_ws": ws, "iters_per_block": args.iters,
@@ -168,6 +195,12 @@ def main():
                                            "autograd_thread_ms", "other_threads_ms")},
             "gathers_per_iteration": 2 * len(model.layers), "reduce_buckets": opt._reducer.K,
             "blocks": rows}
+    if args.alternate_write:
+        for j, name in enumerate(("store kernel", "hipStreamWriteValue64")):
+            sub = rows[j::2]
+            summ["median_" + name.replace(" ", "_")] = {
+                k: sorted(r[k] for r in sub)[len(sub) // 2]
+                for k in ("wall_ms", "cpu_ms", "main_thread_ms", "autograd_thread_ms", "other_threads_ms")}
     print(json.dumps({k: v for k, v in summ.items() if k != "blocks"}), flush=True)
     if args.out:
         Path(args.out).write_text(json.dumps(summ, indent=1) + "\n")
