@@ -67,16 +67,20 @@ if os.environ.get("ZERO_AMD_HOSTEXT", "1") == "0":  # A/B switch (tools/z3_host_
 # hooks when the extension has them; False: one Python post-accumulate hook per parameter and
 # counter (read when hooks are registered; tools/z3_host_ab.py --no-counting)
 HOSTEXT_COUNTING = True
-# Side-stream gathers: at most this many gathered allocations the GPU has not released yet.  Each
-# module's allocation is made on the side stream and its consumer's use recorded on it, so the
-# caching allocator reuses a block only once the consumer stream has passed its release; a host
-# that runs ahead of the GPU (a GPU-bound iteration) kept allocating new blocks, ~68 per C5
-# iteration, until hipMalloc failed and the allocator synchronised the device and freed its cache
-# — single host iterations of 1.4-5 s (profiles/r06_z3_thr_stall.json, stacks in torch.empty of
-# _side_empty).  The runtime records a release marker on the consumer stream every
-# GATHER_INFLIGHT // 2 releases, and before a new allocation waits on the host for the oldest
-# marker while GATHER_INFLIGHT allocations are outstanding (FSDP's all-gather rate limit).
-GATHER_INFLIGHT = int(os.environ.get("ZERO_AMD_GATHER_INFLIGHT", "8"))
+# Side-stream gathers: at most this many bytes of gathered allocations the GPU has not released
+# yet (0: 1/8 of the device's memory).  Each module's allocation is made on the side stream and its
+# consumer's use recorded on it, so the caching allocator reuses a block only once the consumer
+# stream has passed its release; a host that runs ahead of the GPU (a GPU-bound iteration) kept
+# allocating new blocks, ~68 per C5 iteration, until hipMalloc failed and the allocator
+# synchronised the device and freed its cache — single host iterations of 1.4-5 s
+# (profiles/r06_z3_thr_stall.json, stacks in torch.empty of _side_empty).  The runtime records a
+# release marker on the consumer stream every GATHER_MARKER_EVERY releases, and before a new
+# allocation waits on the host for the oldest marker while the limit would be exceeded (FSDP's
+# all-gather rate limit).  In bytes, not allocations: a limit of a few modules starved a GPU whose
+# iteration ends in a long step (the next forward's releases queue behind it) — the host should
+# stay about an iteration ahead, as far as memory allows (profiles/r06_z3_thr_limit_*.json).
+GATHER_INFLIGHT_BYTES = int(os.environ.get("ZERO_AMD_GATHER_INFLIGHT_BYTES", "0"))
+GATHER_MARKER_EVERY = 4
 
 
 def _chunk_geom(d0: int, ws: int, rank: int):
@@ -191,12 +195,12 @@ def _release_group(ms):
         for m in ms:
             m._full = None  # (full_data = None, without the property call)
         if getattr(rt, "_throttled", False):
-            rt.note_release()
+            rt.note_release(ms)
         return
     for m in ms:
         m.release()
     if getattr(rt, "_throttled", False):
-        rt.note_release()
+        rt.note_release(ms)
 
 
 class _GatherRuntime:
@@ -264,23 +268,33 @@ class _GatherRuntime:
         self._vplans = {}
         self.use_hostext = True  # (False: per-parameter install / release, for A/B)
         self._sync_wait = _lib.lib.zs_sync_wait  # (the bound foreign function, looked up once)
-        # the gather rate limit (GATHER_INFLIGHT): on for an optimizer's side-stream runtime, whose
+        # the gather rate limit (GATHER_INFLIGHT_BYTES): on for an optimizer's side-stream runtime, whose
         # allocations are released through _release_group
         self._throttled = False
-        self.max_inflight = max(2, GATHER_INFLIGHT)
-        self._marker_every = max(1, self.max_inflight // 2)
-        self._outstanding = 0       # gathered allocations not known to be released on the GPU
-        self._markers = deque()     # (flag sync, epoch, releases it covers), oldest first
+        self.max_inflight_bytes = GATHER_INFLIGHT_BYTES or None  # (default set at first use)
+        self._marker_every = GATHER_MARKER_EVERY
+        self._out_bytes = 0         # gathered bytes not known to be released on the GPU
+        self._out_n = 0             # ... and their allocations
+        self._markers = deque()     # (flag sync, epoch, bytes, allocations it covers), oldest first
         self._rel_syncs = {}        # consumer stream handle -> [flag sync, its latest epoch]
-        self._rel_n = 0             # releases since the last marker
-        self._counted = set()       # pending keys counted in _outstanding
+        self._rel_bytes = self._rel_n = 0  # released since the last marker
+        self._counted = {}          # pending key -> its bytes counted in _out_bytes
+        self._nbytes_of = {}        # id(managers list) -> (that list, its gathered bytes)
         self.n_throttle_waits = 0
 
-    # -- the gather rate limit (GATHER_INFLIGHT) ------------------------------------------------
-    def note_release(self):
+    # -- the gather rate limit (GATHER_INFLIGHT_BYTES) ------------------------------------------------
+    def _nbytes(self, managers) -> int:
+        ent = self._nbytes_of.get(id(managers))
+        if ent is None or ent[0] is not managers:
+            n = sum(m.numel for m in managers) * managers[0].shard.element_size() if managers else 0
+            ent = self._nbytes_of[id(managers)] = (managers, n)
+        return ent[1]
+
+    def note_release(self, managers):
         """A module's gathered parameters were released (on the current stream): every
         ``_marker_every`` releases one marker recorded there."""
         self._rel_n += 1
+        self._rel_bytes += self._nbytes(managers)
         if self._rel_n >= self._marker_every:
             self._record_marker()
 
@@ -293,28 +307,38 @@ class _GatherRuntime:
             ent = self._rel_syncs[h] = [Sync(_lib.ZS_SYNC_FLAG), 0]
         ent[0].record(h)
         ent[1] += 1
-        self._markers.append((ent[0], ent[1], self._rel_n))
-        self._rel_n = 0
+        self._markers.append((ent[0], ent[1], self._rel_bytes, self._rel_n))
+        self._rel_bytes = self._rel_n = 0
 
-    def _throttle(self, key, k: int = 1):
-        """Before ``k`` new gathered allocations: while that would exceed ``max_inflight``
-        outstanding, wait on the host for the oldest release marker (everything before a marker on
-        its stream is enqueued already, so it completes without anything this host still has to
-        enqueue).  No marker left: go ahead (nothing to wait for)."""
-        while self._outstanding + k > self.max_inflight and self._markers:
-            sy, e, n = self._markers.popleft()
+    def _throttle(self, key, managers):
+        """Before a new gathered allocation: while it would take the outstanding bytes past
+        ``max_inflight_bytes`` (two allocations always allowed), wait on the host for the oldest
+        release marker — everything before a marker on its stream is enqueued already, so it
+        completes without anything this host still has to enqueue.  No marker left: go ahead."""
+        nb = self._nbytes(managers)
+        if self.max_inflight_bytes is None:
+            self.max_inflight_bytes = torch.cuda.get_device_properties(self.device).total_memory // 8
+        while (self._out_bytes + nb > self.max_inflight_bytes and self._out_n >= 2
+               and self._markers):
+            sy, e, b, n = self._markers.popleft()
             if sy.query()[1] < e:
                 self.n_throttle_waits += 1
                 while sy.query()[1] < e:
                     time.sleep(20e-6)
-            self._outstanding -= n
-        self._outstanding += k
-        self._counted.add(key)
+            self._out_bytes -= b
+            self._out_n -= n
+        self._out_bytes += nb
+        self._out_n += 1
+        self._counted[key] = nb
 
     def _drop_pending(self):
         """Gathers prefetched but never consumed are dropped (their memory goes back once the side
         stream is past them): no longer outstanding."""
-        self._outstanding -= len(self._counted.intersection(self.pending))
+        for key in self.pending:
+            nb = self._counted.pop(key, None)
+            if nb is not None:
+                self._out_bytes -= nb
+                self._out_n -= 1
         self._counted.clear()
         self.pending.clear()
 
@@ -383,7 +407,7 @@ class _GatherRuntime:
         timed = self.gather_events is not None and self.ws > 1
         plan = self._tables[key] if key in self._tables else self._table(key, managers)
         if self._throttled:
-            self._throttle(key)
+            self._throttle(key, managers)
         if plan is not None and plan[-1] is not None and not timed and self.stream is None:
             # single-stream mode: the RCCL group on the consumer's stream, nothing to order
             send, count, offs, total, dt, es, views, recv, raw, ordered = plan
@@ -652,7 +676,7 @@ class _GatherRuntime:
                 hold = torch.empty(total, dtype=ms[0].shard.dtype, device=self.device)
             else:  # written by the side stream: allocated there (see _take_ready)
                 if self._throttled:
-                    self._throttle(k)
+                    self._throttle(k, ms)
                 hold = self._side_empty(total, ms[0].shard.dtype)
             np.add(offs, np.uint64(hold.data_ptr()), out=recv)
             ordered(cur_h, ready_h if j == 0 else 0, side_h, done_h if j == last else 0)
@@ -701,7 +725,7 @@ class _GatherRuntime:
             self.n_prefetch_hits += 1
         self.launch(key, managers, cur_h)
         out, ev, hold, alloc_h, wait_h = self.pending.pop(key)
-        self._counted.discard(key)
+        self._counted.pop(key, None)
         if ev is None and hold is None:  # ws == 1
             for m, full in out:
                 m._install_full(full)
@@ -753,7 +777,8 @@ class _GatherRuntime:
         self._drop_pending()
         if self._throttled:  # every consumed allocation is released by now: the markers cover them
             self._record_marker()
-            self._outstanding = sum(n for _, _, n in self._markers)
+            self._out_bytes = sum(m[2] for m in self._markers)
+            self._out_n = sum(m[3] for m in self._markers)
         self._waves_launched.clear()
         self._waited.clear()
         self.pos = 0
