@@ -330,8 +330,8 @@ int zs_stream_wait_event(uintptr_t stream, uint64_t event) {
 
 // ---------------------------------------------------------------------------------------------
 // Sync objects (ABI v12; 64-bit words since v13): the cross-stream ordering of the engines as either
-// a HIP event or a stream memory operation on a flag word (hipStreamWriteValue64 after the
-// producer's work, hipStreamWaitValue64 >= the recorded epoch before the consumer's).  A record
+// a HIP event or a stream memory operation on a flag word (a one-wave release-store kernel —
+// round 6; hipStreamWriteValue64 with zs_tune "sync_write_kernel" 0 — after the producer's work, hipStreamWaitValue64 >= the recorded epoch before the consumer's).  A record
 // bumps the object's epoch on the host and enqueues its write; a wait enqueues a wait for the epoch
 // of the latest record, the semantics of hipStreamWaitEvent.  Epochs are 64-bit and only grow: at
 // one record per microsecond a word wraps after 584,000 years, so the unsigned >= of the GPU wait

@@ -242,7 +242,8 @@ class RcclComm:
 class Sync:
     """A cross-stream ordering point (``zs_sync``, include/zero_amd.h): a HIP event
     (``kind=_lib.ZS_SYNC_EVENT``) or a stream memory operation on a flag word in pinned host memory
-    (``_lib.ZS_SYNC_FLAG``: hipStreamWriteValue64 of a 64-bit epoch on the producer stream,
+    (``_lib.ZS_SYNC_FLAG``: a 64-bit epoch stored on the producer stream by a one-wave release-store
+    kernel (round 6; ``hipStreamWriteValue64`` with zs_tune "sync_write_kernel" 0),
     hipStreamWaitValue64 >= it on the consumer; a wait whose record has already executed is
     skipped on the host; epochs never wrap).  A wait on a pending HIP event keeps one HIP
     runtime thread polling for as long as it is pending; a flag wait is resolved by the GPU and

@@ -328,8 +328,10 @@ int zs_device_alloc_chunked(int64_t bytes, int64_t chunk_bytes, void** out);
  * "adam_wg_per_cu" (0 = 128 workgroups per CU, the default grid of the fused Adam; k = at most k
  * per CU), "sync_host_flags" (1: flag syncs created from now on take words in pinned host
  * memory, whose satisfied waits the host skips; 0: device words, every wait enqueued — the
- * fallback the library takes by itself when pinned memory is refused).  *previous (may be NULL) gets the
- * old value;
+ * fallback the library takes by itself when pinned memory is refused), "sync_write_kernel" (1: a
+ * flag sync's record is a one-wave kernel storing the epoch with a system-scope release; 0:
+ * hipStreamWriteValue64 — same ordering, the runtime's stream-operation command costs more host
+ * time).  *previous (may be NULL) gets the old value;
  * ZS_ERR_INVALID for an unknown key or value. */
 int zs_tune(const char* key, int64_t value, int64_t* previous);
 
@@ -394,8 +396,9 @@ int zs_reduce_scatter_group_ordered(zs_comm* comm, int64_t n, const uint64_t* se
 int zs_stream_wait_event(uintptr_t stream, uint64_t event);
 /* Sync objects (ABI v12; v13: 64-bit epochs): a cross-stream ordering point that is either a HIP
  * event (ZS_SYNC_EVENT) or a stream memory operation on a flag word in pinned host-coherent memory
- * (ZS_SYNC_FLAG: hipStreamWriteValue64 of an epoch on the producer, hipStreamWaitValue64 >= it on
- * the consumer; epochs only grow and never wrap).  zs_sync_record enqueues the producer side on
+ * (ZS_SYNC_FLAG: the epoch stored on the producer — a one-wave store kernel with a system-scope
+ * release, or hipStreamWriteValue64 (zs_tune "sync_write_kernel") — and hipStreamWaitValue64 >= it
+ * on the consumer; epochs only grow and never wrap).  zs_sync_record enqueues the producer side on
  * `stream`; zs_sync_wait makes `stream` wait for the latest record (hipStreamWaitEvent's
  * semantics; a never-recorded sync, or one whose latest record has already executed — the host
  * reads the flag word — enqueues nothing).  A flag record from another stream than the previous
