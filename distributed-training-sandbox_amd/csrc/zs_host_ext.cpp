@@ -18,6 +18,8 @@
 //
 // Built against the torch headers of this image (no HIP code): zero_amd/_hostext*.so.
 #include <Python.h>
+#include <c10/core/StreamGuard.h>
+#include <c10/core/impl/DeviceGuardImplInterface.h>
 #include <torch/csrc/autograd/function_hook.h>
 #include <torch/csrc/autograd/variable.h>
 #include <torch/extension.h>
@@ -284,6 +286,87 @@ int64_t attached(const at::Tensor& param) {
   return ch == nullptr ? -1 : static_cast<int64_t>(ch->targets.size());
 }
 
+// One module's side-stream gather, issued and consumed in one call each (round 6, second pass).
+// What _GatherRuntime's Python did per gather — allocate the module's full tensors on the side
+// stream, point the table's receive addresses into the allocation, call the library's synced group
+// (ready wait, the RCCL group of all-gathers, the done record) — and per consumption — the
+// consumer's wait, the allocator's record of the consumer stream, the ViewPlan install.  The
+// library entry points come in as addresses (zs_all_gather_group_synced / zs_sync_wait, include/
+// zero_amd.h): this helper is not linked against libzero_amd.so.
+using SyncedGroupFn = int (*)(void* comm, int64_t n, const uint64_t* send, const uint64_t* recv,
+                              const int64_t* count, int dtype, uintptr_t after, void* ready,
+                              uintptr_t stream, void* done);
+using SyncWaitFn = int (*)(void* sync, uintptr_t stream);
+
+class GatherFast {
+ public:
+  // fn: the synced group's address; comm: the communicator handle (0 with n_coll = 0: the
+  // ordering alone, no collective — the simulated-rank benches); send / count: the module's
+  // chunk-arena slots and element counts; offs: each full tensor's byte offset in the allocation
+  GatherFast(uintptr_t fn, uintptr_t comm, bool collective, std::vector<uint64_t> send,
+             std::vector<int64_t> count, std::vector<uint64_t> offs, int64_t total, int zdtype,
+             at::ScalarType dtype, int64_t device_index)
+      : fn_(reinterpret_cast<SyncedGroupFn>(fn)), comm_(reinterpret_cast<void*>(comm)),
+        collective_(collective), send_(std::move(send)), count_(std::move(count)),
+        offs_(std::move(offs)), total_(total), zdtype_(zdtype), dtype_(dtype),
+        device_(c10::DeviceType::CUDA, static_cast<c10::DeviceIndex>(device_index)) {
+    TORCH_CHECK(fn_ != nullptr, "GatherFast: NULL group function");
+    TORCH_CHECK(send_.size() == count_.size() && send_.size() == offs_.size(),
+                "GatherFast: send, count and offs differ in length");
+    TORCH_CHECK(total_ > 0, "GatherFast: total must be > 0");
+    recv_.assign(send_.size(), 0);
+  }
+
+  // allocate on the side stream (side_id: its torch stream id), fill the receive table, enqueue
+  // the synced group; returns (status, allocation)
+  std::tuple<int, at::Tensor> launch(uintptr_t after, uintptr_t ready, int64_t side_id,
+                                     uintptr_t side_h, uintptr_t done) {
+    at::Tensor hold;
+    {
+      c10::StreamGuard g(c10::Stream::unpack3(side_id, device_.index(), c10::DeviceType::CUDA));
+      hold = at::empty({total_}, at::TensorOptions().dtype(dtype_).device(device_));
+    }
+    const uint64_t base = reinterpret_cast<uint64_t>(hold.data_ptr());
+    for (size_t i = 0; i < recv_.size(); ++i) recv_[i] = base + offs_[i];
+    const int64_t n = collective_ ? static_cast<int64_t>(send_.size()) : 0;
+    const int rc = fn_(comm_, n, n ? send_.data() : nullptr, n ? recv_.data() : nullptr,
+                       n ? count_.data() : nullptr, zdtype_, after, reinterpret_cast<void*>(ready),
+                       side_h, reinterpret_cast<void*>(done));
+    return {rc, hold};
+  }
+
+  int64_t size() const { return static_cast<int64_t>(send_.size()); }
+
+ private:
+  SyncedGroupFn fn_;
+  void* comm_;
+  bool collective_;
+  std::vector<uint64_t> send_, recv_;
+  std::vector<int64_t> count_;
+  std::vector<uint64_t> offs_;
+  int64_t total_;
+  int zdtype_;
+  at::ScalarType dtype_;
+  c10::Device device_;
+};
+
+// The consumer's side of a gather: wait on `wait_sync` (0: none) on the current stream `cur_h`,
+// record the current stream's use of `hold` with the caching allocator (`record`), install the
+// module's parameters from it.  Returns the wait's status.
+int consume(uintptr_t wait_fn, uintptr_t wait_sync, uintptr_t cur_h, const at::Tensor& hold,
+            ViewPlan& vp, bool record) {
+  if (wait_sync) {
+    const int rc = reinterpret_cast<SyncWaitFn>(wait_fn)(reinterpret_cast<void*>(wait_sync), cur_h);
+    if (rc) return rc;
+  }
+  if (record) {
+    const auto* impl = c10::impl::getDeviceGuardImpl(hold.device().type());
+    hold.record_stream(impl->getStream(hold.device()));
+  }
+  vp.install(hold);
+  return 0;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -309,6 +392,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("pending", &GradCounter::pending)
       .def_property_readonly("next", &GradCounter::next)
       .def_property_readonly("counted", &GradCounter::counted);
+  pybind11::class_<GatherFast>(m, "GatherFast")
+      .def(pybind11::init<uintptr_t, uintptr_t, bool, std::vector<uint64_t>, std::vector<int64_t>,
+                          std::vector<uint64_t>, int64_t, int, at::ScalarType, int64_t>())
+      .def("launch", &GatherFast::launch)
+      .def_property_readonly("size", &GatherFast::size);
+  m.def("consume", &consume, "the consumer's wait, the allocator's stream record, the install");
   m.def("attach", &attach, "count `param`'s completed gradients into counter slot `slot`");
   m.def("detach", &detach, "drop every target of `counter` from `param`'s hook");
   m.def("attached", &attached, "targets on `param`'s counting hook (-1: none installed)");

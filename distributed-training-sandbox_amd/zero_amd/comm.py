@@ -211,6 +211,12 @@ class RcclComm:
         """reduce_scatter_group_bound with sync-object ordering (see all_gather_group_synced_bound)."""
         return self._ordered(_lib.lib.zs_reduce_scatter_group_synced, send, recv, count, dtype)
 
+    def all_gather_group_synced_raw(self):
+        """(address of zs_all_gather_group_synced, communicator handle, True): what the host
+        extension's GatherFast calls with its own tables (zero3._GatherRuntime)."""
+        return (ctypes.cast(_lib.lib.zs_all_gather_group_synced, ctypes.c_void_p).value,
+                int(self._h.value or 0), True)
+
     def _ordered(self, fn, send, recv, count, dtype):
         n = len(count)
         sp, rp, cp = send.ctypes.data_as(_PU64), recv.ctypes.data_as(_PU64), count.ctypes.data_as(_PI64)

@@ -37,6 +37,7 @@ on the same side stream, so one communicator sees one totally ordered sequence o
 from __future__ import annotations
 
 import contextlib
+import ctypes
 import os
 import time
 import weakref
@@ -268,6 +269,11 @@ class _GatherRuntime:
         self._vplans = {}
         self.use_hostext = True  # (False: per-parameter install / release, for A/B)
         self._sync_wait = _lib.lib.zs_sync_wait  # (the bound foreign function, looked up once)
+        # the host extension's one-call gather / consume (GatherFast per key; None: Python path)
+        self._gfast = {}
+        self._wait_fn = ctypes.cast(_lib.lib.zs_sync_wait, ctypes.c_void_p).value
+        self._consume = getattr(_hostext, "consume", None) if _hostext is not None else None
+        self.use_gather_fast = True  # (False: the Python gather / consume, for A/B)
         # the gather rate limit (GATHER_INFLIGHT_BYTES): on for an optimizer's side-stream runtime, whose
         # allocations are released through _release_group
         self._throttled = False
@@ -425,9 +431,16 @@ class _GatherRuntime:
             # slots), the done sync its consumers wait on.  Allocated on the side stream, which
             # writes it; the consumer records its own use (materialize)
             send, count, offs, total, dt, es, views, recv, raw, ordered = plan
-            hold = self._side_empty(total, managers[0].shard.dtype)
-            np.add(offs, np.uint64(hold.data_ptr()), out=recv)
-            ordered(cur_h, self._take_ready(ready_h), self._side_h, ev_h)
+            gf = self._gather_fast(key, managers, plan)
+            if gf is not None:  # allocation, receive table and synced group: one C++ call
+                rc, hold = gf.launch(cur_h, self._take_ready(ready_h), self._side_ids[0],
+                                     self._side_h, ev_h)
+                if rc:
+                    _lib.check(rc, "zs_all_gather_group_synced")
+            else:
+                hold = self._side_empty(total, managers[0].shard.dtype)
+                np.add(offs, np.uint64(hold.data_ptr()), out=recv)
+                ordered(cur_h, self._take_ready(ready_h), self._side_h, ev_h)
             self.pending[key] = (_Gathered(managers, hold, views, self._vplan(managers, views)),
                                  done, hold, self._side_h, ev_h)
             self.n_gathers += 1
@@ -522,6 +535,26 @@ class _GatherRuntime:
                     views, recv, raw, ordered)
         self._tables[key] = plan
         return plan
+
+    def _gather_fast(self, key, managers, plan):
+        """The key's GatherFast (csrc/zs_host_ext.cpp): its side-stream allocation, receive table
+        and synced group in one call — or None (no extension, a communicator without the raw
+        synced group, the per-parameter ablation)."""
+        gf = self._gfast.get(key, False)
+        if gf is not False:
+            return gf
+        gf = None
+        raw_of = getattr(self.comm, "all_gather_group_synced_raw", None)
+        if (self.use_hostext and self.use_gather_fast and raw_of is not None and _hostext is not None
+                and hasattr(_hostext, "GatherFast") and self._side_ids is not None):
+            fn, comm_h, collective = raw_of()
+            send, count, offs, total, dt, es, views, recv, raw, ordered = plan
+            gf = _hostext.GatherFast(int(fn), int(comm_h), bool(collective),
+                                     [int(x) for x in send], [int(x) for x in count],
+                                     [int(x) for x in offs], int(total), int(dt),
+                                     managers[0].shard.dtype, int(self._dev_idx))
+        self._gfast[key] = gf
+        return gf
 
     def _vplan(self, managers, views):
         """The module's ViewPlan (shared by its forward and backward keys: the same managers
@@ -672,14 +705,23 @@ class _GatherRuntime:
         side, side_h = self.stream, (cur_h if single else self._side_h)
         for j, ((k, ms), plan) in enumerate(zip(todo, plans)):
             send, count, offs, total, dt, es, views, recv, raw, ordered = plan
+            gf = None
             if single:
                 hold = torch.empty(total, dtype=ms[0].shard.dtype, device=self.device)
             else:  # written by the side stream: allocated there (see _take_ready)
                 if self._throttled:
                     self._throttle(k, ms)
-                hold = self._side_empty(total, ms[0].shard.dtype)
-            np.add(offs, np.uint64(hold.data_ptr()), out=recv)
-            ordered(cur_h, ready_h if j == 0 else 0, side_h, done_h if j == last else 0)
+                gf = self._gather_fast(k, ms, plan)
+            if gf is not None:
+                rc, hold = gf.launch(cur_h, ready_h if j == 0 else 0, self._side_ids[0], side_h,
+                                     done_h if j == last else 0)
+                if rc:
+                    _lib.check(rc, "zs_all_gather_group_synced")
+            else:
+                if not single:
+                    hold = self._side_empty(total, ms[0].shard.dtype)
+                np.add(offs, np.uint64(hold.data_ptr()), out=recv)
+                ordered(cur_h, ready_h if j == 0 else 0, side_h, done_h if j == last else 0)
             self.pending[k] = (_Gathered(ms, hold, views, self._vplan(ms, views)), done_ev, hold,
                                side_h, done_h or None)
             self.n_gathers += 1
@@ -729,6 +771,20 @@ class _GatherRuntime:
         if ev is None and hold is None:  # ws == 1
             for m, full in out:
                 m._install_full(full)
+            return
+        if (wait_h is not None and hold is not None and self._consume is not None
+                and self.use_gather_fast and type(out) is _Gathered and out.vplan is not None):
+            # the wait (once per wave and consuming stream), the allocator's record of this
+            # stream's use, the install: one C++ call
+            need = self._waited.get(wait_h) != cur_h
+            rc = self._consume(self._wait_fn, wait_h if need else 0, cur_h, hold, out.vplan,
+                               alloc_h is not None and alloc_h != cur_h)
+            if rc:
+                _lib.check(rc, "zs_sync_wait")
+            if need:
+                self._waited[wait_h] = cur_h
+            for m in out.ms:
+                m._full = True
             return
         if wait_h is not None:
             if self._waited.get(wait_h) != cur_h:  # once per wave and consuming stream
@@ -1030,6 +1086,7 @@ def register_zero3_hooks(model, param_managers, units=None, reshard_after_forwar
         rt.mark_inputs_changed()  # (a new registration: nothing gathered before it is reused)
         rt.key_managers = {}
         rt._tables = {}  # a key's managers may differ from an earlier registration
+        rt._gfast = {}
         rt._vplans = {}
         rt._fp8_tables = {}
         rt.iteration_callbacks = []  # (an earlier registration's bookkeeping is replaced)

@@ -68,6 +68,9 @@ def main():
     ap.add_argument("--no-counting", action="store_true",
                     help="also time the current runtime with per-parameter Python post-accumulate "
                          "hooks instead of the C++ gradient counters")
+    ap.add_argument("--no-gather-fast", action="store_true",
+                    help="also time the current runtime with the gathers issued and consumed in "
+                         "Python instead of the host extension's GatherFast / consume (round 6)")
     args = ap.parse_args()
     path = baseline_file(args.baseline) if args.baseline != "none" else None
     if args.extract_only:
@@ -111,6 +114,7 @@ def main():
         mod.get = lambda what, dm=None: {"ws": ws, "rank": 0}.get(what) if what in ("ws", "rank") \
             else real_get(what, dm)
         use_hostext = okw.pop("use_hostext", True)
+        gather_fast = okw.pop("gather_fast", True)
         counting = okw.pop("counting", True)
         saved = getattr(mod, "HOSTEXT_COUNTING", None)
         if saved is not None:
@@ -120,6 +124,8 @@ def main():
                                        sync=False, comm=bench._NoComm(ws), **okw)
             if hasattr(opt, "runtime") and opt.runtime is not None:
                 opt.runtime.use_hostext = use_hostext
+                if hasattr(opt.runtime, "use_gather_fast"):
+                    opt.runtime.use_gather_fast = gather_fast
             mod.register_zero3_hooks(model, opt.param_managers)
         finally:
             if saved is not None:
@@ -140,6 +146,8 @@ def main():
         variants["current_events"] = build(z3_new, 0, stream_sync="event")
     if args.single:  # the current runtime with its collectives on the compute stream
         variants["current_single_stream"] = build(z3_new, 0, side_stream=False)
+    if args.no_gather_fast:  # the current runtime's gathers issued / consumed in Python
+        variants["current_no_gather_fast"] = build(z3_new, 0, gather_fast=False)
     if args.no_hostext:  # the current runtime installing / releasing per parameter in Python
         variants["current_no_hostext"] = build(z3_new, 0, use_hostext=False)
         if args.single:
