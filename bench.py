@@ -684,6 +684,13 @@ class _NoComm:
 
         return ctypes.cast(_lib.lib.zs_all_gather_group_synced, ctypes.c_void_p).value, 0, False
 
+    def reduce_scatter_group_synced_raw(self):  # (ReduceFast: the ordering alone)
+        import ctypes
+
+        from zero_amd import _lib
+
+        return ctypes.cast(_lib.lib.zs_reduce_scatter_group_synced, ctypes.c_void_p).value, 0, False
+
     # (the event-ordered forms, which earlier rounds' runtimes bind: tools/z3_host_ab.py)
     def all_gather_group_ordered_bound(self, send, recv, count, dtype):
         return self._ordered("zs_all_gather_group_ordered", dtype)

@@ -16,6 +16,11 @@
 // Python, and Python is called once per completed bucket (or run of buckets) and once per
 // released module instead of once per parameter and counter.
 //
+// Round 6, second pass: GatherFast / consume — a module gather's side-stream allocation, receive
+// table and synced library call in one C++ call, and its consumption (the consumer's wait, the
+// caching allocator's record of the consumer stream, the ViewPlan install) in another; device and
+// stream handling through c10's device-generic guards, so still no HIP code here.
+//
 // Built against the torch headers of this image (no HIP code): zero_amd/_hostext*.so.
 #include <Python.h>
 #include <c10/core/StreamGuard.h>
@@ -350,6 +355,66 @@ class GatherFast {
   c10::Device device_;
 };
 
+// One gradient bucket's reduce-scatter issued in one call (update mode's _GradReducer._launch):
+// every parameter's gradient must be there, dense, of the bucket's dtype and exactly ws chunks
+// long (zero-copy: the gradient itself is the send buffer) — otherwise launch() returns -1 and
+// touches nothing, and the caller takes its general path.  Then the send table, the library's
+// synced group (ready wait, the RCCL group of reduce-scatters, the done record), the allocator's
+// record of the collective stream on each gradient (`record`: it is read there after the
+// gradient is dropped) and `p.grad = None` for each.
+class ReduceFast {
+ public:
+  ReduceFast(uintptr_t fn, uintptr_t comm, bool collective, std::vector<at::Tensor> params,
+             std::vector<uint64_t> recv, std::vector<int64_t> count, int zdtype,
+             at::ScalarType dtype, int64_t ws)
+      : fn_(reinterpret_cast<SyncedGroupFn>(fn)), comm_(reinterpret_cast<void*>(comm)),
+        collective_(collective), params_(std::move(params)), recv_(std::move(recv)),
+        count_(std::move(count)), zdtype_(zdtype), dtype_(dtype), ws_(ws) {
+    TORCH_CHECK(fn_ != nullptr, "ReduceFast: NULL group function");
+    TORCH_CHECK(params_.size() == recv_.size() && params_.size() == count_.size(),
+                "ReduceFast: params, recv and count differ in length");
+    send_.assign(params_.size(), 0);
+    grads_.resize(params_.size());
+  }
+
+  int launch(uintptr_t after, uintptr_t ready, int64_t stream_id, int64_t device_index,
+             uintptr_t stream_h, uintptr_t done, bool record) {
+    for (size_t i = 0; i < params_.size(); ++i) {
+      const at::Tensor& g = params_[i].grad();
+      if (!g.defined() || g.scalar_type() != dtype_ || !g.is_contiguous() ||
+          g.numel() != ws_ * count_[i])
+        return -1;
+      grads_[i] = g;
+      send_[i] = reinterpret_cast<uint64_t>(g.data_ptr());
+    }
+    const int64_t n = collective_ ? static_cast<int64_t>(params_.size()) : 0;
+    const int rc = fn_(comm_, n, n ? send_.data() : nullptr, n ? recv_.data() : nullptr,
+                       n ? count_.data() : nullptr, zdtype_, after, reinterpret_cast<void*>(ready),
+                       stream_h, reinterpret_cast<void*>(done));
+    if (rc == 0) {
+      const c10::Stream st = c10::Stream::unpack3(
+          stream_id, static_cast<c10::DeviceIndex>(device_index), c10::DeviceType::CUDA);
+      for (size_t i = 0; i < params_.size(); ++i) {
+        if (record) grads_[i].record_stream(st);
+        params_[i].mutable_grad().reset();
+      }
+    }
+    for (auto& g : grads_) g.reset();
+    return rc;
+  }
+
+ private:
+  SyncedGroupFn fn_;
+  void* comm_;
+  bool collective_;
+  std::vector<at::Tensor> params_, grads_;
+  std::vector<uint64_t> recv_, send_;
+  std::vector<int64_t> count_;
+  int zdtype_;
+  at::ScalarType dtype_;
+  int64_t ws_;
+};
+
 // The consumer's side of a gather: wait on `wait_sync` (0: none) on the current stream `cur_h`,
 // record the current stream's use of `hold` with the caching allocator (`record`), install the
 // module's parameters from it.  Returns the wait's status.
@@ -398,6 +463,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("launch", &GatherFast::launch)
       .def_property_readonly("size", &GatherFast::size);
   m.def("consume", &consume, "the consumer's wait, the allocator's stream record, the install");
+  pybind11::class_<ReduceFast>(m, "ReduceFast")
+      .def(pybind11::init<uintptr_t, uintptr_t, bool, std::vector<at::Tensor>, std::vector<uint64_t>,
+                          std::vector<int64_t>, int, at::ScalarType, int64_t>())
+      .def("launch", &ReduceFast::launch);
   m.def("attach", &attach, "count `param`'s completed gradients into counter slot `slot`");
   m.def("detach", &detach, "drop every target of `counter` from `param`'s hook");
   m.def("attached", &attached, "targets on `param`'s counting hook (-1: none installed)");

@@ -217,6 +217,12 @@ class RcclComm:
         return (ctypes.cast(_lib.lib.zs_all_gather_group_synced, ctypes.c_void_p).value,
                 int(self._h.value or 0), True)
 
+    def reduce_scatter_group_synced_raw(self):
+        """(address of zs_reduce_scatter_group_synced, communicator handle, True): what the host
+        extension's ReduceFast calls with its own tables (zero3._GradReducer)."""
+        return (ctypes.cast(_lib.lib.zs_reduce_scatter_group_synced, ctypes.c_void_p).value,
+                int(self._h.value or 0), True)
+
     def _ordered(self, fn, send, recv, count, dtype):
         n = len(count)
         sp, rp, cp = send.ctypes.data_as(_PU64), recv.ctypes.data_as(_PU64), count.ctypes.data_as(_PI64)

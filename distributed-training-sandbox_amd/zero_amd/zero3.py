@@ -1376,9 +1376,13 @@ class _GradReducer:
         cs = opt.runtime.stream if opt.world_size > 1 else None  # (None: single-stream mode)
         if cs is not None:
             self._cs_h = cs.cuda_stream
+            self._cs_id = cs.stream_id
         self.timing = None  # optional list of (start, end, bus_bytes) per launched bucket
         self._rs_tables = {}
         self.use_hostext = HOSTEXT_COUNTING  # (False: per-parameter Python hooks, for A/B)
+        self.use_reduce_fast = True  # (False: every bucket launched by the Python below, for A/B)
+        self._rfast = {}             # bucket -> its _hostext.ReduceFast, or None
+        self._group_idx = [np.asarray(g, np.int64) for g in groups]
         self._counter = None     # the C++ gradient counter (register_hooks)
         self.reset()
 
@@ -1502,9 +1506,48 @@ class _GradReducer:
             self._rs_tables[k] = t
         return t
 
+    def _reduce_fast(self, k: int):
+        """Bucket k's ReduceFast (csrc/zs_host_ext.cpp): its gradients' send table, the synced
+        group, the stream records and the gradient resets in one call — or None (no extension, a
+        communicator without the raw synced group, a bf16 exchange, uneven chunks)."""
+        rf = self._rfast.get(k, False)
+        if rf is not False:
+            return rf
+        rf = None
+        opt = self.opt
+        ar = opt._arena
+        raw_of = getattr(opt.comm, "reduce_scatter_group_synced_raw", None)
+        if (self.use_reduce_fast and raw_of is not None and _hostext is not None
+                and hasattr(_hostext, "ReduceFast") and opt._G.dtype == ar.dtype
+                and hasattr(opt.comm, "reduce_scatter_group")
+                and all(self._N_l[i] == opt.world_size * self._S_l[i] for i in self.groups[k])):
+            recv, count, dt, sp, raw, ordered = self._rs_table(k)
+            fn, comm_h, collective = raw_of()
+            rf = _hostext.ReduceFast(int(fn), int(comm_h), bool(collective),
+                                     [opt.params[i] for i in self.groups[k]],
+                                     [int(x) for x in recv], [int(x) for x in count], int(dt),
+                                     ar.dtype, int(opt.world_size))
+        self._rfast[k] = rf
+        return rf
+
     def _launch(self, k: int):
         opt = self.opt
         ar, ws = opt._arena, opt.world_size
+        rf = self._reduce_fast(k) if ws > 1 and self.timing is None else None
+        if rf is not None:
+            rt = opt.runtime
+            cur_h = rt._cur_h()
+            if rt.stream is None:  # single-stream mode: on the stream that produced the grads
+                rc = rf.launch(cur_h, 0, 0, 0, cur_h, 0, False)
+            else:
+                rc = rf.launch(cur_h, self._ready_sync(k, cur_h).h, self._cs_id, rt._dev_idx,
+                               self._cs_h, self._done_h[k] if k == self.K - 1 else 0, True)
+            if rc == 0:
+                self.had_grad[self._group_idx[k]] = True
+                return
+            if rc > 0:
+                _lib.check(rc, "zs_reduce_scatter_group_synced")
+            # (-1: a gradient missing or not a zero-copy send: the general path below)
         if ws == 1:  # nothing to exchange: Adam reads the local grad in place
             for i in self.groups[k]:
                 g = opt.params[i].grad

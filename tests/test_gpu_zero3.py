@@ -184,6 +184,13 @@ def _update_hooks(rank, ws, name, dev, comm=None, backward_hooks=None, side_stre
         plans = [vp for _, vp in opt.runtime._vplans.values()]
         assert zero3._hostext is not None and plans and all(vp is not None for vp in plans)
         assert sum(vp.size for vp in plans) == len(params)
+    if ws > 1 and hasattr(opt.runtime.comm, "reduce_scatter_group_synced_raw"):
+        # (RCCL) the host extension's one-call paths ran: every bucket of even chunks launched by
+        # its ReduceFast, and with the side stream every gather issued by its GatherFast
+        rfs = opt._reducer._rfast
+        assert rfs and all((rf is not None) == (16 % ws == 0) for rf in rfs.values())
+        if side_stream:
+            assert opt.runtime._gfast and all(gf is not None for gf in opt.runtime._gfast.values())
 
 
 def _shards_changed(rank, ws, name, dev, comm=None):

@@ -71,6 +71,9 @@ def main():
     ap.add_argument("--no-gather-fast", action="store_true",
                     help="also time the current runtime with the gathers issued and consumed in "
                          "Python instead of the host extension's GatherFast / consume (round 6)")
+    ap.add_argument("--no-reduce-fast", action="store_true",
+                    help="also time the current runtime with the gradient buckets launched in "
+                         "Python instead of the host extension's ReduceFast (round 6)")
     args = ap.parse_args()
     path = baseline_file(args.baseline) if args.baseline != "none" else None
     if args.extract_only:
@@ -115,6 +118,7 @@ def main():
             else real_get(what, dm)
         use_hostext = okw.pop("use_hostext", True)
         gather_fast = okw.pop("gather_fast", True)
+        reduce_fast = okw.pop("reduce_fast", True)
         counting = okw.pop("counting", True)
         saved = getattr(mod, "HOSTEXT_COUNTING", None)
         if saved is not None:
@@ -126,6 +130,9 @@ def main():
                 opt.runtime.use_hostext = use_hostext
                 if hasattr(opt.runtime, "use_gather_fast"):
                     opt.runtime.use_gather_fast = gather_fast
+            red = getattr(opt, "_reducer", None)
+            if red is not None and hasattr(red, "use_reduce_fast"):
+                red.use_reduce_fast = reduce_fast
             mod.register_zero3_hooks(model, opt.param_managers)
         finally:
             if saved is not None:
@@ -148,6 +155,10 @@ def main():
         variants["current_single_stream"] = build(z3_new, 0, side_stream=False)
     if args.no_gather_fast:  # the current runtime's gathers issued / consumed in Python
         variants["current_no_gather_fast"] = build(z3_new, 0, gather_fast=False)
+    if args.no_reduce_fast:  # ... and its gradient buckets launched in Python
+        variants["current_no_reduce_fast"] = build(z3_new, 0, reduce_fast=False)
+    if args.no_gather_fast and args.no_reduce_fast:
+        variants["current_neither_fast"] = build(z3_new, 0, gather_fast=False, reduce_fast=False)
     if args.no_hostext:  # the current runtime installing / releasing per parameter in Python
         variants["current_no_hostext"] = build(z3_new, 0, use_hostext=False)
         if args.single:
