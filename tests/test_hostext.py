@@ -261,3 +261,39 @@ def test_counter_callbacks_hold_their_owner_weakly():
     for p in ps:
         p.grad = None
     loss().backward()  # the owner is gone: nothing happens
+
+
+# --- GatherFast / ReduceFast: a module gather and a gradient bucket in one call (round 6) -------
+def test_gather_fast_validates_its_tables():
+    ext = _ext()
+    assert ext.GatherFast(1, 0, False, [1, 2], [3, 4], [0, 64], 128, 0, torch.float32, 0).size == 2
+    with pytest.raises(RuntimeError, match="differ in length"):
+        ext.GatherFast(1, 0, False, [1, 2], [3], [0, 64], 128, 0, torch.float32, 0)
+    with pytest.raises(RuntimeError, match="total"):
+        ext.GatherFast(1, 0, False, [1], [3], [0], 0, 0, torch.float32, 0)
+    with pytest.raises(RuntimeError, match="NULL"):
+        ext.GatherFast(0, 0, False, [1], [3], [0], 8, 0, torch.float32, 0)
+
+
+def test_reduce_fast_declines_what_is_not_a_zero_copy_send():
+    """launch() returns -1 and touches nothing (no library call: the function address here is
+    bogus) unless every gradient is present, dense, of the bucket's dtype and exactly ws chunks
+    long — the caller's general path then handles (or refuses) it."""
+    ext = _ext()
+    ws = 2
+    ps = [torch.nn.Parameter(torch.zeros(4, 3)), torch.nn.Parameter(torch.zeros(6))]
+    rf = ext.ReduceFast(12345, 0, True, ps, [0, 0], [6, 3], 0, torch.float32, ws)
+    assert rf.launch(0, 0, 0, 0, 0, 0, False) == -1  # no gradients at all
+    ps[0].grad = torch.ones(4, 3)
+    assert rf.launch(0, 0, 0, 0, 0, 0, False) == -1  # one missing
+    ps[1].grad = torch.ones(6)
+    ps[0].grad = torch.ones(3, 4).t()  # not dense
+    assert rf.launch(0, 0, 0, 0, 0, 0, False) == -1
+    ps[0].grad = torch.ones(4, 3)
+    uneven = ext.ReduceFast(12345, 0, True, ps, [0, 0], [6, 4], 0, torch.float32, ws)
+    assert uneven.launch(0, 0, 0, 0, 0, 0, False) == -1  # 6 elements are not 2 chunks of 4
+    bf = ext.ReduceFast(12345, 0, True, ps, [0, 0], [6, 3], 1, torch.bfloat16, ws)
+    assert bf.launch(0, 0, 0, 0, 0, 0, False) == -1  # fp32 gradients, a bf16 bucket
+    assert ps[0].grad is not None and ps[1].grad is not None  # nothing reset
+    with pytest.raises(RuntimeError, match="differ in length"):
+        ext.ReduceFast(12345, 0, True, ps, [0], [6, 3], 0, torch.float32, ws)
