@@ -16,7 +16,7 @@ case "$step" in
       --timeout 300 --timeout-method thread --durations=20 > "$O/tests_$TS.log" 2>&1; rc=$?
     tail -40 "$O/tests_$TS.log"; fatal $rc; echo "[tests $TS] rc=$rc";;
   suite)  # the whole -m gpu suite as the driver runs it, then smoke()
-    ZS_FAIL_LOG="$O/failures_suite_$TS.txt" timeout -k 10 1000 python -u -m pytest tests -m gpu -q \
+    ZS_CASE_LOG="$O/cases_suite_$TS.txt" ZS_FAIL_LOG="$O/failures_suite_$TS.txt" timeout -k 10 1000 python -u -m pytest tests -m gpu -q \
       --timeout 600 --timeout-method thread --durations=60 > "$O/suite_$TS.log" 2>&1; rc=$?
     tail -80 "$O/suite_$TS.log"; fatal $rc
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" \
