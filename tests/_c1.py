@@ -1,7 +1,8 @@
 """BASELINE.json configs[0] at its real width: the reference MLP 6 × Linear(10000, 10000)
 (600,060,000 fp32 params, zero1.py:237-249) at ws = 2, for the sampled full-width fixtures
 ``tests/golden/c1_z{1,2}_ws2_sampled.npz`` (made by ``make_golden.py c1`` from the reference's own
-ShardedOptimizer on gloo).
+ShardedOptimizer on gloo) — and configs[1], the same MLP at D = 4096 (100,687,872 params) under
+ZeRO-2, ``c2_z2_ws2_sampled.npz``.
 
 The full tensors are too large to commit, so a fixture keeps, per parameter, a fixed sample of
 element indices and the values there (initial, after every step on every rank, final Adam state),
@@ -18,17 +19,18 @@ from __future__ import annotations
 
 import numpy as np
 
-D = 10000
+D = 10000      # configs[0]
+D_C2 = 4096    # configs[1]
 WS = 2
 STEPS = 3
 N_SAMPLE = 2048
 MUL = 2654435761  # odd: k -> k·MUL mod 2^24 is a permutation of the 24-bit residues
 
 
-def shapes():
+def shapes(d: int = D):
     out = []
     for _ in range(6):
-        out += [(D, D), (D,)]
+        out += [(d, d), (d,)]
     return out
 
 
@@ -63,7 +65,7 @@ def sample_idx(i: int, n: int) -> np.ndarray:
     return np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, N_SAMPLE)])).astype(np.int64)
 
 
-def make_model():
+def make_model(d: int = D):
     """The reference's model (zero1.py:237-249) with the fixture's init (torch.manual_seed(0))."""
     import torch
     import torch.nn as nn
@@ -71,7 +73,7 @@ def make_model():
     torch.manual_seed(0)
     layers = []
     for li in range(6):
-        layers.append(nn.Linear(D, D))
+        layers.append(nn.Linear(d, d))
         if li < 5:
             layers.append(nn.ReLU())
     return nn.Sequential(*layers)

@@ -275,7 +275,7 @@ def make_traj(variant, ws, D, mode):
 # ----------------------------------------------------------------------------------------------
 # 2b. configs[0] at its real width, sampled (tests/_c1.py)
 # ----------------------------------------------------------------------------------------------
-def _c1_worker(rank, ws, port, variant, tmpdir):
+def _c1_worker(rank, ws, port, variant, tmpdir, d=None):
     import torch
     import torch.distributed as dist
 
@@ -287,7 +287,7 @@ def _c1_worker(rank, ws, port, variant, tmpdir):
     torch.set_num_threads(4)
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     mod = _load_ref(variant)
-    model = _c1.make_model()
+    model = _c1.make_model(d or _c1.D)
     params = list(model.parameters())
     idx = [_c1.sample_idx(i, p.numel()) for i, p in enumerate(params)]
     rec = {}
@@ -328,16 +328,17 @@ def _c1_worker(rank, ws, port, variant, tmpdir):
     dist.destroy_process_group()
 
 
-def make_c1(variant):
+def make_c1(variant, cfg="c1"):
     import torch.multiprocessing as mp
 
     sys.path.insert(0, str(OUT.parent))
     import _c1
 
+    d = {"c1": _c1.D, "c2": _c1.D_C2}[cfg]
     _PORT[0] += 1
     with tempfile.TemporaryDirectory() as td:
-        mp.spawn(_c1_worker, args=(_c1.WS, _PORT[0], variant, td), nprocs=_c1.WS, join=True)
-        merged = {"ws": np.array(_c1.WS), "D": np.array(_c1.D), "steps": np.array(_c1.STEPS)}
+        mp.spawn(_c1_worker, args=(_c1.WS, _PORT[0], variant, td, d), nprocs=_c1.WS, join=True)
+        merged = {"ws": np.array(_c1.WS), "D": np.array(d), "steps": np.array(_c1.STEPS)}
         for r in range(_c1.WS):
             with np.load(Path(td) / f"rank{r}.npz") as z:
                 for k in z.files:
@@ -348,7 +349,7 @@ def make_c1(variant):
                             assert np.array_equal(merged[k], z[k]), k
                         continue
                     merged[f"r{r}_{k}"] = z[k]
-    name = f"c1_z{variant}_ws{_c1.WS}_sampled.npz"
+    name = f"{cfg}_z{variant}_ws{_c1.WS}_sampled.npz"
     np.savez_compressed(OUT / name, **merged)
     print(name, len(merged), "arrays")
 
@@ -419,6 +420,8 @@ def main():
     if "c1" in which:  # not in the default set: two 600M-parameter ranks, ~20 GB of host memory
         make_c1(1)
         make_c1(2)
+    if "c2" in which:  # configs[1]: the same MLP at D = 4096 under ZeRO-2
+        make_c1(2, "c2")
     if "traj" in which:
         for variant in (1, 2, 3):
             for ws in (1, 2, 3, 4, 8):

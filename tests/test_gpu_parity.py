@@ -361,13 +361,14 @@ def _carry_worker(rank, ws, port, clear):
     sys.stdout.flush()
 
 
-def _c1_worker(rank, ws, port, variants=(1, 2)):
+def _c1_worker(rank, ws, port, cases=(("c1", 1), ("c1", 2), ("c2", 2))):
     """BASELINE configs[0] at its real width against the reference (tests/_c1.py): the reference's
     6 × Linear(10000, 10000) (600,060,000 fp32 params, its own init) through ZeRO-1 and ZeRO-2 at
     ws = 2 for 3 steps of the exact hash gradients; every parameter's sampled elements on this
     rank after every step, and the owned parameters' Adam state, within 1e-6 of the reference's
     (tests/golden/c1_z{1,2}_ws2_sampled.npz), and every parameter's fp64 sum within 1e-6 of
-    Σ|p|.  The model is built once (on the CPU, as the reference's) for both variants."""
+    Σ|p|.  The model is built once per width (on the CPU, as the reference's).  configs[1] (c2):
+    the same MLP at D = 4096 (100,687,872 params) under ZeRO-2."""
     import sys
     from conftest import PKG, REPO  # noqa: F401
     from _gloo_comm import GlooStagedComm, test_comm  # noqa: F401
@@ -377,11 +378,15 @@ def _c1_worker(rank, ws, port, variants=(1, 2)):
     torch.cuda.set_device(0)
     init_pg(rank, ws, port)
     dev = torch.device("cuda:0")
-    model = _c1.make_model()  # the reference's init (torch.manual_seed(0), CPU)
-    init = [p.detach() for p in model.parameters()]
-    del model
-    for variant in variants:
-        z = np.load(GOLDEN / f"c1_z{variant}_ws2_sampled.npz")
+    widths = {"c1": _c1.D, "c2": _c1.D_C2}
+    built = {}
+    for cfg, variant in cases:
+        d = widths[cfg]
+        if d not in built:  # the reference's init (torch.manual_seed(0), CPU)
+            built.clear()
+            built[d] = [p.detach() for p in _c1.make_model(d).parameters()]
+        init = built[d]
+        z = np.load(GOLDEN / f"{cfg}_z{variant}_ws2_sampled.npz")
         assert int(z["ws"]) == ws
         idx = [torch.from_numpy(z[f"idx_{i}"]).to(dev) for i in range(12)]
         for i, p in enumerate(init):

@@ -96,7 +96,8 @@ def test_rccl_zero12(gpu, rccl_env, ws):
 def test_rccl_c1_full_width(gpu, rccl_env):
     """BASELINE configs[0] at its real width (6 × Linear(10000, 10000), 600M fp32 params) at
     ws = 2 through real RCCL, ZeRO-1 (carry) and ZeRO-2, against the reference's sampled run
-    (tests/_c1.py, test_gpu_parity._c1_worker): 2.4 GB reduced and broadcast per step."""
+    (tests/_c1.py, test_gpu_parity._c1_worker): 2.4 GB reduced and broadcast per step; and
+    configs[1] (D = 4096, 100M params) under ZeRO-2."""
     from test_gpu_parity import _c1_worker
 
     spawn_batch(2, [(_c1_worker, ())], all_spawned=True, deadline_s=300)

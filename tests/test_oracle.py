@@ -110,20 +110,21 @@ def test_simulate_with_fixture_grads(golden, variant):
                 assert rel(v, z[f"r{r}_state_{i}_exp_avg_sq"]) <= 1e-6
 
 
-@pytest.mark.parametrize("variant", [1, 2])
-def test_simulate_c1_full_width_samples(golden, variant):
+@pytest.mark.parametrize("cfg,variant", [("c1", 1), ("c1", 2), ("c2", 2)])
+def test_simulate_c1_full_width_samples(golden, cfg, variant):
     """BASELINE configs[0] at its real width (6 × Linear(10000, 10000), ws = 2, 3 steps of the
     exact hash gradients, tests/_c1.py): the restated step run on the fixture's sampled elements
     alone reproduces the reference's sampled params on both ranks after every step (incl. ZeRO-1's
     carry) and the owned params' Adam state, within 1e-6 — and the hash gradients themselves are
-    the ones the reference consumed (their sampled values, recomputed here, drive the match)."""
+    the ones the reference consumed (their sampled values, recomputed here, drive the match).
+    configs[1] (c2): the same MLP at D = 4096 under ZeRO-2."""
     import _c1
 
-    z = golden(f"c1_z{variant}_ws2_sampled.npz")
-    ws, steps = int(z["ws"]), int(z["steps"])
-    assert (ws, steps, int(z["D"])) == (_c1.WS, _c1.STEPS, _c1.D)
+    z = golden(f"{cfg}_z{variant}_ws2_sampled.npz")
+    ws, steps, d = int(z["ws"]), int(z["steps"]), int(z["D"])
+    assert (ws, steps, d) == (_c1.WS, _c1.STEPS, {"c1": _c1.D, "c2": _c1.D_C2}[cfg])
     idx = [z[f"idx_{i}"] for i in range(12)]
-    for i, s in enumerate(_c1.shapes()):  # the fixture's sample is the one tests/_c1.py draws
+    for i, s in enumerate(_c1.shapes(d)):  # the fixture's sample is the one tests/_c1.py draws
         assert np.array_equal(idx[i], _c1.sample_idx(i, int(np.prod(s))))
     init = [z[f"init_{i}"] for i in range(12)]
     out = zo.simulate(variant, ws, init, steps=steps,
