@@ -114,13 +114,15 @@ def _zero3_cases(ws):
                  ("_update_hooks_single", "traj_z2_ws2_d16_distinct.npz"),
                  ("_update_hooks_wave3", "traj_z2_ws2_d16_distinct.npz"),
                  ("_update_hooks_events", "traj_z2_ws2_d16_distinct.npz"),
+                 ("_update_hooks_throttled", "traj_z2_ws2_d16_distinct.npz"),
                  ("_ref_mode_single", "traj_z3_ws2_d16_distinct.npz"),
                  ("_shards_changed", "traj_z2_ws2_d16_distinct.npz")],
              3: [("_update_injected", "traj_z2_ws3_d16_distinct.npz"),
                  ("_update_hooks_single", "traj_z2_ws3_d16_distinct.npz")],
              4: [("_ref_mode", "traj_z3_ws4_d16_distinct.npz"), ("_ref_injected", "traj_z3_ws4_d16_ref.npz"),
                  ("_update_hooks", "traj_z2_ws4_d16_distinct.npz"),
-                 ("_update_hooks_single", "traj_z2_ws4_d16_distinct.npz")],
+                 ("_update_hooks_single", "traj_z2_ws4_d16_distinct.npz"),
+                 ("_update_hooks_throttled", "traj_z2_ws4_d16_distinct.npz")],
              # ws = 8: the exchanges the first 8-GPU run executes — table gathers from the module
              # hooks in forward and backward, backward reduce-scatters, the shard all-reduce
              8: [("_ref_mode", "traj_z3_ws8_d16_distinct.npz"), ("_ref_injected", "traj_z3_ws8_d16_ref.npz"),

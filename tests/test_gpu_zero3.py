@@ -139,7 +139,7 @@ def _update_injected(rank, ws, name, dev, comm=None, dtype=torch.float32):
 
 
 def _update_hooks(rank, ws, name, dev, comm=None, backward_hooks=None, side_stream=True,
-                  gather_wave=None, stream_sync=None):
+                  gather_wave=None, stream_sync=None, inflight_bytes=None):
     """update=True through the real hooks: forward / backward all-gathers, gradients
     reduce-scattered from the post-accumulate-grad hooks during backward, fused Adam on the
     chunks.  Grads come from hipBLAS GEMMs, so the bound vs the CPU reference is 1e-4.  Backward
@@ -157,6 +157,8 @@ def _update_hooks(rank, ws, name, dev, comm=None, backward_hooks=None, side_stre
     opt = zero3.ShardedOptimizer(torch.optim.Adam(model.parameters(), lr=1e-3), update=True,
                                  bucket_mb=2e-3, side_stream=side_stream,
                                  **kw)  # ~2 KB buckets: several launches in backward
+    if inflight_bytes is not None:  # the gather rate limit at its tightest: every launch past
+        opt.runtime.max_inflight_bytes = inflight_bytes  # two outstanding waits for a marker
     zero3.register_zero3_hooks(model, opt.param_managers, backward_hooks=backward_hooks)
     params = list(model.parameters())
     x, y = _xy(z, rank, dev)
@@ -257,6 +259,14 @@ def _update_hooks_events(rank, ws, name, dev, comm=None):
     _update_hooks(rank, ws, name, dev, comm=comm, stream_sync="event")
 
 
+def _update_hooks_throttled(rank, ws, name, dev, comm=None):
+    """update mode with the gather rate limit at one byte: at most two gathered allocations
+    outstanding, every further launch first waits on the host for the oldest release marker — with
+    real collectives between the ranks, this must neither deadlock (a marker only covers work
+    already enqueued, and every rank issues the same collective sequence) nor change a bit."""
+    _update_hooks(rank, ws, name, dev, comm=comm, inflight_bytes=1)
+
+
 def _update_hooks_wave3(rank, ws, name, dev, comm=None):
     """update mode with gathers ordered in waves of 3 (six Linear modules: two waves per pass)."""
     _update_hooks(rank, ws, name, dev, comm=comm, gather_wave=3)
@@ -310,7 +320,8 @@ Z3_CASES = [("_ref_mode", w, f"traj_z3_ws{w}_d16_distinct.npz") for w in (2, 4, 
     [("_update_hooks", w, f"traj_z2_ws{w}_d16_{m}.npz")
      for w, m in ((2, "distinct"), (3, "distinct"), (4, "distinct"), (8, "ref"), (8, "distinct"))] + \
     [("_update_hooks_module", w, f"traj_z2_ws{w}_d16_distinct.npz") for w in (2, 4)] + \
-    [("_update_hooks_events", w, f"traj_z2_ws{w}_d16_distinct.npz") for w in (2, 3)]
+    [("_update_hooks_events", w, f"traj_z2_ws{w}_d16_distinct.npz") for w in (2, 3)] + \
+    [("_update_hooks_throttled", w, f"traj_z2_ws{w}_d16_distinct.npz") for w in (2, 4)]
 
 
 @pytest.mark.parametrize("ws", [2, 3, 4, 8])
