@@ -1472,8 +1472,16 @@ def bench_train_smollm3(args, world, rank, dev, use_nccl):
     cfg = sm.smollm3_config(layers=args.train_layers)
     model = sm.build_model(cfg, dev)
     params = sum(p.numel() for p in model.parameters())
+    sim = args.simulate_ws > 1 and args.zero == 3
+    if sim:  # DIAGNOSTIC: rank 0 of a simulate_ws-rank job, collectives skipped (buffers untouched)
+        assert world == 1, "--simulate-ws is a single-GPU diagnostic"
+        sim_ws, real_get = args.simulate_ws, zero3.get
+        zero3.get = lambda what, dm=None: {"ws": sim_ws, "rank": 0}.get(what) \
+            if what in ("ws", "rank") else real_get(what, dm)
     if args.zero == 3:
         comm, _ = _zero3_comm(args, world, rank, dev)
+        if sim:
+            comm = _NoComm(args.simulate_ws)
         kw = {} if comm is None else {"comm": comm}
         opt = zero3.ShardedOptimizer(torch.optim.AdamW(model.parameters(), lr=1e-5), update=True,
                                      sync=False, bucket_mb=args.bucket_mb or 512.0, **kw)
@@ -1524,6 +1532,24 @@ def bench_train_smollm3(args, world, rank, dev, use_nccl):
                           "segments": torch.cuda.memory_stats(dev).get("segment.all.current"),
                           "reserved_gib": torch.cuda.memory_reserved(dev) / (1 << 30)}),
               file=sys.stderr, flush=True)
+    if sim:
+        rt = opt.runtime
+        print(json.dumps({"diagnostic": f"simulate-ws {args.simulate_ws}: rank 0's SmolLM3 ZeRO-3 "
+                          "training step with every hook, gather allocation, release and bucket "
+                          "launch of a ws-rank job, the collectives themselves skipped (their "
+                          "buffers hold whatever memory held: the loss is meaningless; NOT the "
+                          "metric)", "ms_per_step": ms, "tokens_per_s_per_rank": tok_s,
+                          "gathers_per_step": rt.n_gathers / max(1, args.steps + args.warmup),
+                          "reduce_buckets": opt._reducer.K, "seq": args.seq, "batch": batch,
+                          "layers": cfg.num_hidden_layers,
+                          "gather_throttle_waits": rt.n_throttle_waits,
+                          "gather_inflight_limit_gb": (rt.max_inflight_bytes or 0) / 1e9,
+                          "allocator": {k: torch.cuda.memory_stats(dev).get(k) for k in (
+                              "num_alloc_retries", "num_device_alloc", "num_device_free",
+                              "reserved_bytes.all.peak")}}), flush=True)
+        _teardown(opt)
+        dist.destroy_process_group()
+        return None
     if rank == 0:
         print(json.dumps({
             "metric": f"SmolLM3-3B ZeRO-{3 if args.zero == 3 else 2} training throughput "

@@ -49,6 +49,7 @@ int& zs::sync_host_flags() {  // (zs_tune "sync_host_flags"; zs_common.h)
 
 namespace zs {
 hipError_t flag_write(uint64_t* flag, uint64_t value, hipStream_t st);  // zs_kernels.hip
+hipError_t flag_wait_launch(const uint64_t* flag, uint64_t value, hipStream_t st);  // zs_kernels.hip
 }
 
 extern "C" {
@@ -415,6 +416,7 @@ bool flag_reached(const uint64_t* w, uint64_t e) { return __atomic_load_n(w, __A
 // `st` waits for the word to reach `e` unless the host already sees it there
 hipError_t flag_wait(const zs_sync* s, hipStream_t st, uint64_t e) {
   if (e == 0 || (s->host_word && flag_reached(s->flag, e))) return hipSuccess;
+  if (zs::sync_wait_kernel()) return zs::flag_wait_launch(s->flag, e, st);
   return hipStreamWaitValue64(st, s->flag, e, hipStreamWaitValueGte, ~uint64_t(0));
 }
 }  // namespace

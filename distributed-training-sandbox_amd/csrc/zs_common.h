@@ -18,6 +18,11 @@ int& sync_host_flags();
 // zs_tune("sync_write_kernel"): 1 (default) = a flag record is flag_write_kernel (zs_kernels.hip),
 // 0 = hipStreamWriteValue64; flag_write enqueues the former (declared where hip types are known)
 int& sync_write_kernel();
+// zs_tune("sync_write_fence"): 1 (default) = the record kernel's store is a system-scope release,
+// 0 = relaxed; zs_tune("sync_wait_kernel"): 1 = a flag wait is flag_wait_kernel (a polling wave
+// with s_sleep), 0 (default) = hipStreamWaitValue64
+int& sync_write_fence();
+int& sync_wait_kernel();
 
 inline int fail(int code, const char* fmt, ...) {
   char buf[512];

@@ -1754,8 +1754,30 @@ int zs_adamset_stats(const zs_adamset* as, int64_t* elems, int64_t* bytes) {
 // hipStreamWriteValue64 does, without the runtime's stream-operation command: on this stack that
 // command costs a HIP runtime thread ~20 us of CPU per record (profiles/r06_z3_thr_*.json: 1.5 ms
 // of the simulated ws = 8 C5 iteration's 102 records), a kernel launch does not.
+template <bool kFence>
 __global__ __launch_bounds__(64) void flag_write_kernel(uint64_t* flag, uint64_t value) {
-  if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  // kFence: a system-scope release (an L2 write-back first); without it a relaxed store straight
+  // to memory (sc0 sc1) — the stream's earlier kernels made their writes visible at their own end
+  if (threadIdx.x == 0) {
+    if (kFence)
+      __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    else
+      __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// A stream-flag wait as one wave that polls the word with s_sleep between loads (zs_tune
+// "sync_wait_kernel" 1).  hipStreamWaitValue64 on this stack is a runtime kernel
+// (__amd_rocclr_streamOpsWait) spinning without pause: a side stream waiting for the compute stream
+// keeps it busy for milliseconds beside the compute stream's GEMMs (profiles/r06_sm3_sim8 kernel
+// stats).  Gives up after ~2^24 polls (about a minute) rather than hold the GPU forever.
+__global__ __launch_bounds__(64) void flag_wait_kernel(const uint64_t* flag, uint64_t value) {
+  if (threadIdx.x == 0) {
+    for (uint32_t i = 0; i < (1u << 24); ++i) {
+      if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= value) break;
+      __builtin_amdgcn_s_sleep(64);
+    }
+  }
 }
 
 namespace zs {
@@ -1763,9 +1785,25 @@ int& sync_write_kernel() {  // zs_tune("sync_write_kernel"): 1 = flag_write_kern
   static int v = 1;
   return v;
 }
+int& sync_write_fence() {  // zs_tune("sync_write_fence"): 1 = release store, 0 = relaxed store
+  static int v = 1;
+  return v;
+}
+int& sync_wait_kernel() {  // zs_tune("sync_wait_kernel"): 1 = flag_wait_kernel, 0 = hipStreamWaitValue64
+  static int v = 0;
+  return v;
+}
 
 hipError_t flag_write(uint64_t* flag, uint64_t value, hipStream_t st) {
-  hipLaunchKernelGGL(flag_write_kernel, dim3(1), dim3(64), 0, st, flag, value);
+  if (sync_write_fence())
+    hipLaunchKernelGGL(flag_write_kernel<true>, dim3(1), dim3(64), 0, st, flag, value);
+  else
+    hipLaunchKernelGGL(flag_write_kernel<false>, dim3(1), dim3(64), 0, st, flag, value);
+  return hipGetLastError();
+}
+
+hipError_t flag_wait_launch(const uint64_t* flag, uint64_t value, hipStream_t st) {
+  hipLaunchKernelGGL(flag_wait_kernel, dim3(1), dim3(64), 0, st, flag, value);
   return hipGetLastError();
 }
 }  // namespace zs
@@ -1802,6 +1840,12 @@ int zs_tune(const char* key, int64_t value, int64_t* previous) {
     ok = value == 0 || value == 1;
   } else if (std::strcmp(key, "sync_write_kernel") == 0) {
     slot = &zs::sync_write_kernel();
+    ok = value == 0 || value == 1;
+  } else if (std::strcmp(key, "sync_write_fence") == 0) {
+    slot = &zs::sync_write_fence();
+    ok = value == 0 || value == 1;
+  } else if (std::strcmp(key, "sync_wait_kernel") == 0) {
+    slot = &zs::sync_wait_kernel();
     ok = value == 0 || value == 1;
   } else {
     return zs::fail(ZS_ERR_INVALID, "zs_tune: unknown key '%s'", key);
