@@ -19,8 +19,8 @@ int& sync_host_flags();
 // 0 = hipStreamWriteValue64; flag_write enqueues the former (declared where hip types are known)
 int& sync_write_kernel();
 // zs_tune("sync_write_fence"): 1 (default) = the record kernel's store is a system-scope release,
-// 0 = relaxed; zs_tune("sync_wait_kernel"): 1 = a flag wait is flag_wait_kernel (a polling wave
-// with s_sleep), 0 (default) = hipStreamWaitValue64
+// 0 = relaxed; zs_tune("sync_wait_kernel"): 1 (default) = a flag wait is flag_wait_kernel (a
+// polling wave with s_sleep), 0 = hipStreamWaitValue64
 int& sync_write_fence();
 int& sync_wait_kernel();
 

@@ -1790,7 +1790,7 @@ int& sync_write_fence() {  // zs_tune("sync_write_fence"): 1 = release store, 0 
   return v;
 }
 int& sync_wait_kernel() {  // zs_tune("sync_wait_kernel"): 1 = flag_wait_kernel, 0 = hipStreamWaitValue64
-  static int v = 0;
+  static int v = 1;
   return v;
 }
 

@@ -279,7 +279,8 @@ def test_tune_knobs_validate_and_restore():
                                     (b"dq_wg_per_cu", 8, 129, 0), (b"scale_nt", 1, 2, -1),
                                     (b"convert_nt", 0, -2, -1), (b"copy_nt", 1, 3, -1),
                                     (b"adam_wg_per_cu", 64, 1025, 0), (b"sync_host_flags", 0, 2, 1),
-                                    (b"sync_write_kernel", 0, 2, 1)):
+                                    (b"sync_write_kernel", 0, 2, 1), (b"sync_write_fence", 0, 2, 1),
+                                    (b"sync_wait_kernel", 0, 2, 1)):
         assert lib.zs_tune(key, good, ctypes.byref(prev)) == _lib.ZS_OK
         assert prev.value == default
         assert lib.zs_tune(key, bad, None) == _lib.ZS_ERR_INVALID

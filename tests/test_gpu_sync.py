@@ -12,15 +12,28 @@ pytestmark = pytest.mark.gpu
 SLEEP_CYCLES = 50_000_000  # ~20 ms of a spinning kernel: the producer is far behind the host
 
 
-@pytest.fixture(params=["store_kernel", "write_value"])
+FLAG_METHODS = {  # zs_tune knobs: (sync_write_kernel, sync_write_fence, sync_wait_kernel)
+    "store_kernel+wait_kernel": (1, 1, 1),      # the defaults (round 6)
+    "store_kernel+wait_value": (1, 1, 0),
+    "write_value+wait_value": (0, 1, 0),        # round 5: hipStreamWriteValue64 / WaitValue64
+    "relaxed_store+wait_kernel": (1, 0, 1),
+}
+
+
+@pytest.fixture(params=list(FLAG_METHODS))
 def flag_record(request):
-    """How a flag sync's record writes its word: the library's one-wave store kernel (default,
-    round 6) or hipStreamWriteValue64 (zs_tune sync_write_kernel 0); both must order alike."""
+    """How a flag sync's record writes its word and its wait waits: the library's one-wave store
+    kernel (a system-scope release, or relaxed) or hipStreamWriteValue64, and its s_sleep polling
+    wave or hipStreamWaitValue64 — every combination must order alike."""
     from zero_amd import _lib
 
-    _lib.call("zs_tune", b"sync_write_kernel", int(request.param == "store_kernel"), None)
+    w, f, k = FLAG_METHODS[request.param]
+    _lib.call("zs_tune", b"sync_write_kernel", w, None)
+    _lib.call("zs_tune", b"sync_write_fence", f, None)
+    _lib.call("zs_tune", b"sync_wait_kernel", k, None)
     yield request.param
-    _lib.call("zs_tune", b"sync_write_kernel", 1, None)
+    for key in (b"sync_write_kernel", b"sync_write_fence", b"sync_wait_kernel"):
+        _lib.call("zs_tune", key, 1, None)
 
 
 @pytest.mark.parametrize("kind", ["flag", "event"])
