@@ -256,7 +256,8 @@ class Sync:
     (``kind=_lib.ZS_SYNC_EVENT``) or a stream memory operation on a flag word in pinned host memory
     (``_lib.ZS_SYNC_FLAG``: a 64-bit epoch stored on the producer stream by a one-wave release-store
     kernel (round 6; ``hipStreamWriteValue64`` with zs_tune "sync_write_kernel" 0),
-    hipStreamWaitValue64 >= it on the consumer; a wait whose record has already executed is
+    a wait for >= it on the consumer (a one-wave polling kernel; ``hipStreamWaitValue64`` with
+    zs_tune "sync_wait_kernel" 0); a wait whose record has already executed is
     skipped on the host; epochs never wrap).  A wait on a pending HIP event keeps one HIP
     runtime thread polling for as long as it is pending; a flag wait is resolved by the GPU and
     costs the host nothing (profiles/r05_event_poll_probe.jsonl).  ``record(stream_h)`` /

@@ -331,7 +331,10 @@ int zs_device_alloc_chunked(int64_t bytes, int64_t chunk_bytes, void** out);
  * fallback the library takes by itself when pinned memory is refused), "sync_write_kernel" (1: a
  * flag sync's record is a one-wave kernel storing the epoch with a system-scope release; 0:
  * hipStreamWriteValue64 — same ordering, the runtime's stream-operation command costs more host
- * time).  *previous (may be NULL) gets the old value;
+ * time), "sync_write_fence" (1: that store is a system-scope release; 0: relaxed), "sync_wait_kernel"
+ * (1: a flag wait is a one-wave kernel polling the word with s_sleep between loads; 0:
+ * hipStreamWaitValue64, on this stack a runtime kernel spinning without pause beside the compute
+ * stream's kernels).  *previous (may be NULL) gets the old value;
  * ZS_ERR_INVALID for an unknown key or value. */
 int zs_tune(const char* key, int64_t value, int64_t* previous);
 
@@ -397,8 +400,8 @@ int zs_stream_wait_event(uintptr_t stream, uint64_t event);
 /* Sync objects (ABI v12; v13: 64-bit epochs): a cross-stream ordering point that is either a HIP
  * event (ZS_SYNC_EVENT) or a stream memory operation on a flag word in pinned host-coherent memory
  * (ZS_SYNC_FLAG: the epoch stored on the producer — a one-wave store kernel with a system-scope
- * release, or hipStreamWriteValue64 (zs_tune "sync_write_kernel") — and hipStreamWaitValue64 >= it
- * on the consumer; epochs only grow and never wrap).  zs_sync_record enqueues the producer side on
+ * release, or hipStreamWriteValue64 (zs_tune "sync_write_kernel") — and a wait for >= it on the
+ * consumer — a one-wave polling kernel, or hipStreamWaitValue64 (zs_tune "sync_wait_kernel"); epochs only grow and never wrap).  zs_sync_record enqueues the producer side on
  * `stream`; zs_sync_wait makes `stream` wait for the latest record (hipStreamWaitEvent's
  * semantics; a never-recorded sync, or one whose latest record has already executed — the host
  * reads the flag word — enqueues nothing).  A flag record from another stream than the previous
