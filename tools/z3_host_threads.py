@@ -55,6 +55,8 @@ def main():
     ap.add_argument("--alternate-write", action="store_true",
                     help="interleaved A/B in one process: even blocks record flags with the store "
                          "kernel, odd blocks with hipStreamWriteValue64")
+    ap.add_argument("--alternate", default=None,
+                    help="interleaved A/B of any zs_tune knob: even blocks KNOB=1, odd blocks KNOB=0")
     ap.add_argument("--stall-ms", type=float, default=0.0,
                     help="per-iteration host times; an iteration longer than this dumps every "
                          "thread's Python stack to stderr (first 4 only)")
@@ -143,6 +145,8 @@ def main():
     for b in range(args.blocks):
         if args.alternate_write:
             zlib.call("zs_tune", b"sync_write_kernel", 1 - b % 2, None)
+        if args.alternate:
+            zlib.call("zs_tune", args.alternate.encode(), 1 - b % 2, None)
         torch.cuda.synchronize()
         s0, w0, c0 = snap(), time.perf_counter(), time.process_time()
         its = []
@@ -174,7 +178,8 @@ def main():
             except OSError:
                 names[t] = "?"
         rows.append({"block": b, **({"flag_record": ("store kernel", "hipStreamWriteValue64")[b % 2]}
-                                    if args.alternate_write else {}), "wall_ms": round(w / n * 1e3, 3), "cpu_ms": round(c / n * 1e3, 3),
+                                    if args.alternate_write else {}),
+                     **({args.alternate: 1 - b % 2} if args.alternate else {}), "wall_ms": round(w / n * 1e3, 3), "cpu_ms": round(c / n * 1e3, 3),
                      "main_thread_ms": round(main / n * 1e3, 3),
                      "autograd_thread_ms": round(bwd / n * 1e3, 3),
                      "other_threads_ms": round(other / n * 1e3, 3),
@@ -195,6 +200,12 @@ def main():
                                            "autograd_thread_ms", "other_threads_ms")},
             "gathers_per_iteration": 2 * len(model.layers), "reduce_buckets": opt._reducer.K,
             "blocks": rows}
+    if args.alternate:
+        for j in (0, 1):
+            sub = rows[j::2]
+            summ[f"median_{args.alternate}={1 - j}"] = {
+                k: sorted(r[k] for r in sub)[len(sub) // 2]
+                for k in ("wall_ms", "cpu_ms", "main_thread_ms", "autograd_thread_ms", "other_threads_ms")}
     if args.alternate_write:
         for j, name in enumerate(("store kernel", "hipStreamWriteValue64")):
             sub = rows[j::2]
