@@ -135,7 +135,8 @@ def main():
 
 
 def profile_iters(step, n):
-    """Own time per function over n iterations, both threads (cProfile per thread, merged)."""
+    """Own time per function over n iterations, per thread (main: forward, step; autograd: the
+    backward hooks), one cProfile each."""
     import cProfile
     import pstats
     import threading
@@ -165,16 +166,19 @@ def profile_iters(step, n):
     for p in profs.values():
         p.disable()
     zero3._GatherRuntime.materialize = orig
-    st = None
-    for p in profs.values():
-        st = pstats.Stats(p) if st is None else st.add(p)
-    rows = []
-    for (fn, line, name), (cc, nc, tt, ct, _) in st.stats.items():
-        rows.append((tt, ct, nc, f"{Path(fn).name}:{line}:{name}"))
-    rows.sort(reverse=True)
-    return [{"fn": r[3], "own_ms_per_iter": round(r[0] / n * 1e3, 4),
+    main = threading.get_ident()
+    out = {}
+    for tid, p in profs.items():
+        st = pstats.Stats(p)
+        rows = []
+        for (fn, line, name), (cc, nc, tt, ct, _) in st.stats.items():
+            rows.append((tt, ct, nc, f"{Path(fn).name}:{line}:{name}"))
+        rows.sort(reverse=True)
+        out["main" if tid == main else "autograd"] = [
+            {"fn": r[3], "own_ms_per_iter": round(r[0] / n * 1e3, 4),
              "cum_ms_per_iter": round(r[1] / n * 1e3, 4), "calls_per_iter": r[2] / n}
-            for r in rows[:45]]
+            for r in rows[:30]]
+    return out
 
 
 def model_floor(model, shards, x, warmup, n):
