@@ -50,6 +50,7 @@ int& zs::sync_host_flags() {  // (zs_tune "sync_host_flags"; zs_common.h)
 namespace zs {
 hipError_t flag_write(uint64_t* flag, uint64_t value, hipStream_t st);  // zs_kernels.hip
 hipError_t flag_wait_launch(const uint64_t* flag, uint64_t value, hipStream_t st);  // zs_kernels.hip
+uint32_t* wait_timeout_word();  // zs_kernels.hip: set by a flag wait kernel that gave up
 }
 
 extern "C" {
@@ -454,8 +455,18 @@ int zs_sync_destroy(zs_sync* s) {
   return ZS_OK;
 }
 
+// a flag wait kernel gave up (about a minute without its record): its stream went on unordered
+static int flag_wait_check() {
+  const uint32_t* w = zs::wait_timeout_word();
+  if (w != nullptr && __atomic_load_n(w, __ATOMIC_ACQUIRE) != 0)
+    return zs::fail(ZS_ERR_HIP, "a stream-flag wait timed out on the GPU (no record within ~1 min): "
+                    "cross-stream ordering was lost; results since then are not trustworthy");
+  return ZS_OK;
+}
+
 int zs_sync_record(zs_sync* s, uintptr_t stream) {
   ZS_REQUIRE(s != nullptr, "zs_sync_record: NULL sync");
+  if (int rc = flag_wait_check()) return rc;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (s->kind == ZS_SYNC_EVENT) {
     ZS_HIP(hipEventRecord(s->event, st));
@@ -475,6 +486,7 @@ int zs_sync_record(zs_sync* s, uintptr_t stream) {
 
 int zs_sync_wait(zs_sync* s, uintptr_t stream) {
   ZS_REQUIRE(s != nullptr, "zs_sync_wait: NULL sync");
+  if (int rc = flag_wait_check()) return rc;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (s->kind == ZS_SYNC_EVENT) {
     ZS_HIP(hipStreamWaitEvent(st, s->event, 0));

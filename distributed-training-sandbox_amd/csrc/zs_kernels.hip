@@ -1770,13 +1770,19 @@ __global__ __launch_bounds__(64) void flag_write_kernel(uint64_t* flag, uint64_t
 // "sync_wait_kernel" 1).  hipStreamWaitValue64 on this stack is a runtime kernel
 // (__amd_rocclr_streamOpsWait) spinning without pause: a side stream waiting for the compute stream
 // keeps it busy for milliseconds beside the compute stream's GEMMs (profiles/r06_sm3_sim8 kernel
-// stats).  Gives up after ~2^24 polls (about a minute) rather than hold the GPU forever.
-__global__ __launch_bounds__(64) void flag_wait_kernel(const uint64_t* flag, uint64_t value) {
+// stats).  Gives up after ~2^24 polls (about a minute) rather than hold the GPU forever, and then
+// stores 1 into `timed_out` (a pinned host word): the next sync call on the host fails loudly
+// (zs_comm.cpp flag_wait_check) instead of the lost ordering passing silently.
+__global__ __launch_bounds__(64) void flag_wait_kernel(const uint64_t* flag, uint64_t value,
+                                                       uint32_t* timed_out) {
   if (threadIdx.x == 0) {
-    for (uint32_t i = 0; i < (1u << 24); ++i) {
+    uint32_t i = 0;
+    for (; i < (1u << 24); ++i) {
       if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= value) break;
       __builtin_amdgcn_s_sleep(64);
     }
+    if (i == (1u << 24) && timed_out != nullptr)
+      __hip_atomic_store(timed_out, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -1802,8 +1808,23 @@ hipError_t flag_write(uint64_t* flag, uint64_t value, hipStream_t st) {
   return hipGetLastError();
 }
 
+// the pinned host word flag_wait_kernel marks on a timeout (nullptr when pinned memory is refused)
+uint32_t* wait_timeout_word() {
+  static uint32_t* w = [] {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocPortable | hipHostMallocMapped) !=
+        hipSuccess) {
+      (void)hipGetLastError();
+      return static_cast<uint32_t*>(nullptr);
+    }
+    *static_cast<volatile uint32_t*>(p) = 0;
+    return static_cast<uint32_t*>(p);
+  }();
+  return w;
+}
+
 hipError_t flag_wait_launch(const uint64_t* flag, uint64_t value, hipStream_t st) {
-  hipLaunchKernelGGL(flag_wait_kernel, dim3(1), dim3(64), 0, st, flag, value);
+  hipLaunchKernelGGL(flag_wait_kernel, dim3(1), dim3(64), 0, st, flag, value, wait_timeout_word());
   return hipGetLastError();
 }
 }  // namespace zs
